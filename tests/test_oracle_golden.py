@@ -1,0 +1,185 @@
+"""Pin the CPU oracle against golden vectors produced by the reference's own
+modules (tests/golden/make_golden.py).  CPU only."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import loss as oloss
+from oracle import nerf as onerf
+from oracle import pixbw as opb
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return np.max(np.abs(a - b) / np.maximum(np.abs(b), 1.0))
+
+
+# --------------------------------------------------------------------------- radiance field
+@pytest.mark.parametrize("rd", [1, 3])
+def test_radiance_field_matches_reference(golden_dir, rd):
+    z = _load(golden_dir, f"mlp_rd{rd}.npz")
+    p = onerf.build_params(rd, int(z["seed"]))
+    # same weights as the reference's construction under the same seed
+    for name in z["param_names"]:
+        assert abs(p[str(name)].double().sum().item() - float(z[f"wsum:{name}"])) < 1e-9 * max(1, abs(float(z[f"wsum:{name}"]))) + 1e-6
+    for k in p:
+        p[k].requires_grad_(True)
+    x = torch.from_numpy(z["x"])
+    d = torch.from_numpy(z["d"])
+    rgb, sig = onerf.radiance_field(p, x, d)
+    # bitwise-level agreement with the reference's fp32 forward (same torch ops on CPU)
+    assert rel_err(rgb.detach(), z["rgb_f32"]) < 1e-6
+    assert rel_err(sig.detach(), z["sigma_f32"]) < 1e-6
+    # and the reference's own fp32-vs-fp64 gap is small too
+    assert rel_err(z["rgb_f32"], z["rgb_f64"]) < 1e-5
+    ((rgb * torch.from_numpy(z["g_rgb"])).sum() + (sig * torch.from_numpy(z["g_sigma"])).sum()).backward()
+    for name in z["param_names"]:
+        name = str(name)
+        g = p[name].grad.numpy().astype(np.float64)
+        ref_norm = float(z[f"gnorm_f32:{name}"])
+        assert abs(np.linalg.norm(g) - ref_norm) <= 1e-5 * max(ref_norm, 1e-6) + 1e-9, name
+        if f"grad:{name}" in z.files:
+            ref = z[f"grad:{name}"]
+            scale = max(np.abs(ref).max(), 1e-6)
+            assert np.abs(g - ref).max() <= 1e-5 * scale, name
+
+
+def test_encoding_layout():
+    v = torch.tensor([[0.1, -0.2, 0.3]])
+    e = onerf.encode(v, 2)
+    # [v, sin(v), sin(2v), cos(v), cos(2v)] scale-major / dim-minor
+    exp = [0.1, -0.2, 0.3] + [math.sin(a) for a in (0.1, -0.2, 0.3, 0.2, -0.4, 0.6)] \
+        + [math.cos(a) for a in (0.1, -0.2, 0.3, 0.2, -0.4, 0.6)]
+    assert np.allclose(e.numpy()[0], exp, atol=1e-6)
+
+
+def test_trunc_exp_backward_clamp():
+    x = torch.tensor([0.0, 10.0, 20.0], requires_grad=True)
+    y = onerf._TruncExp.apply(x)
+    y.sum().backward()
+    assert torch.allclose(x.grad, torch.exp(torch.tensor([0.0, 10.0, 15.0])))
+
+
+# --------------------------------------------------------------------------- compositing (unpinned)
+def test_composite_vs_bruteforce():
+    g = torch.Generator().manual_seed(0)
+    R, N, rd = 5, 37, 3
+    t0 = torch.sort(torch.rand(R, N, generator=g) * 4 + 1, dim=-1).values
+    t1 = t0 + torch.rand(R, N, generator=g) * 0.05
+    rgb = torch.rand(R, N, rd, generator=g)
+    sig = torch.rand(R, N, generator=g) * 30
+    bk = torch.tensor([0.3, 0.5, 0.7])
+    c, o, dpt, _ = onerf.composite(t0, t1, rgb, sig, bk)
+    c2, o2, d2 = onerf.composite_bruteforce_f64(t0, t1, rgb, sig, bk)
+    assert rel_err(c, c2) < 1e-5 and rel_err(o, o2) < 1e-5 and rel_err(dpt, d2) < 1e-5
+
+
+def test_sampler_strata_and_miss():
+    o = torch.tensor([[0.0, 0.0, -4.0], [0.0, 5.0, -4.0]])
+    d = torch.tensor([[0.0, 0.0, 1.0], [0.0, 0.0, 1.0]])
+    u = torch.tensor([0.25, 0.5])
+    t0, t1 = onerf.stratified_samples(o, d, u, onerf.AABB_CHAIR, 1.43, 6.63, 8)
+    mid = (t0 + t1) / 2
+    # ray 0 crosses the box on z in [2.5, 5.5]
+    assert torch.allclose(mid[0], 2.5 + (torch.arange(8) + 0.25) / 8 * 3.0)
+    assert torch.allclose(t1[0] - t0[0], torch.full((8,), 3.0 / 8))
+    # ray 1 misses the box: zero-width intervals -> zero weights
+    assert torch.all(t1[1] == t0[1])
+
+
+# --------------------------------------------------------------------------- FOH
+def test_foh_matches_reference(golden_dir):
+    z = _load(golden_dir, "foh.npz")
+    for tag, dt_ in (("f64", torch.float64), ("f32", torch.float32)):
+        A = torch.from_numpy(z["A"]).to(dt_)
+        B = torch.from_numpy(z["B"]).to(dt_)
+        dt = torch.from_numpy(z["dt"]).to(dt_)
+        Ad, Bd, Btd = opb.foh_discretise(A, B, dt)
+        tol = 1e-12 if tag == "f64" else 1e-5
+        assert rel_err(Ad, z[f"Ad_{tag}_eff"]) < tol
+        assert rel_err(Bd, z[f"Bd_{tag}_eff"]) < tol
+        assert rel_err(Btd, z[f"Btd_{tag}_eff"]) < tol
+    # efficient vs block-expm agree in the reference itself (f64)
+    assert rel_err(z["Ad_f64_eff"], z["Ad_f64_blk"]) < 1e-9
+
+
+# --------------------------------------------------------------------------- pixel bandwidth
+def _intensity_of(ts, z):
+    t = ts * 1e-9
+    base, amp, freq, phase = (torch.from_numpy(z[k]) for k in ("base", "amp", "freq", "phase"))
+    return base * torch.exp(amp * torch.sin(2 * np.pi * freq * t + phase))
+
+
+@pytest.mark.parametrize("fname", ["pixbw_S16_eds.npz", "pixbw_S30_eds.npz", "pixbw_S16_pert.npz"])
+def test_pixel_bandwidth_matches_reference(golden_dir, fname):
+    z = _load(golden_dir, fname)
+    calib = {k.split(":", 1)[1]: z[k] for k in z.files if k.startswith("calib:")}
+    base_prm = opb.calib_to_params(calib)
+    call_ts = torch.from_numpy(z["call_ts"])
+    coef = torch.from_numpy(z["coef"])
+    for gi, gname in enumerate(("gen_dirac", "gen_unif")):
+        gen = torch.from_numpy(z[gname])
+        for dtag, dtype in (("f32", torch.float32), ("f64", torch.float64)):
+            # parameters exactly as the module holds them: softplus(original)
+            originals = {}
+            prm = {"tau_in_it_eff_prod": torch.tensor(np.float32(base_prm["tau_in_it_eff_prod"])).to(dtype)}
+            for pn in opb.PARAM_NAMES:
+                orig = torch.tensor(z[f"orig_{dtag}:{pn}"], dtype=dtype).requires_grad_(True)
+                originals[pn] = orig
+                prm[pn] = torch.nn.functional.softplus(orig, beta=1, threshold=20)
+            pb = opb.PixelBandwidthOracle(prm, int(z["min_ts"]))
+            leaves = []
+
+            def fn(ts):
+                it = _intensity_of(ts, z).to(dtype).detach().requires_grad_(True)
+                leaves.append(it)
+                return it
+
+            outs = [pb(gen, call_ts[c], fn, reset_diff=(c == 0)) for c in range(4)]
+            total = sum((outs[c] * coef[c].to(dtype)).sum() for c in range(4))
+            total.backward()
+            tol = 1e-7 if dtag == "f64" else 2e-6
+            for c in range(4):
+                assert rel_err(outs[c].detach(), z[f"logit_g{gi}_{dtag}_c{c}"]) < tol, (c, dtag)
+                ref = z[f"dit_g{gi}_{dtag}_c{c}"]
+                assert np.abs(leaves[c].grad.numpy() - ref).max() <= (1e-6 if dtag == "f64" else 1e-3) * np.abs(ref).max()
+            for pn in opb.PARAM_NAMES:
+                ref = z[f"dparam_g{gi}_{dtag}:{pn}"]
+                got = originals[pn].grad.numpy()
+                assert abs(got - ref) <= (1e-6 if dtag == "f64" else 2e-3) * max(abs(ref), 1e-30), (pn, dtag)
+
+
+# --------------------------------------------------------------------------- loss / event model
+@pytest.mark.parametrize("t", ["huber_l1", "l1_huber", "mse_mse"])
+def test_loss_matches_reference(golden_dir, t):
+    z = _load(golden_dir, "loss.npz")
+    fd, ft = t.split("_")
+    d_lid = torch.from_numpy(z[f"{t}:d_lid"]).requires_grad_(True)
+    s_lid = torch.from_numpy(z[f"{t}:s_lid"]).requires_grad_(True)
+    mct = torch.tensor(0.225, requires_grad=True)
+    end_ts = torch.from_numpy(z[f"{t}:end_ts"])
+    start_ts = torch.from_numpy(z[f"{t}:start_ts"])
+    Ld, Lt = oloss.event_loss(torch.from_numpy(z[f"{t}:lid"]), end_ts, start_ts, d_lid,
+                              (end_ts - start_ts) * 1.0, torch.from_numpy(z[f"{t}:d_valid"]),
+                              s_lid, torch.from_numpy(z[f"{t}:s_valid"]), mct, fd, ft)
+    assert rel_err(Ld.detach(), z[f"{t}:L_diff"]) < 1e-6
+    assert rel_err(Lt.detach(), z[f"{t}:L_tv"]) < 1e-6
+    (Ld + 1e-3 * Lt).backward()
+    assert np.abs(d_lid.grad.numpy() - z[f"{t}:g_d_lid"]).max() < 1e-9
+    assert np.abs(s_lid.grad.numpy() - z[f"{t}:g_s_lid"]).max() < 1e-9
+    assert rel_err(mct.grad.numpy(), z[f"{t}:g_mct"]) < 1e-5
+
+
+def test_contrast_threshold_matches_reference(golden_dir):
+    z = _load(golden_dir, "ct.npz")
+    lid = oloss.contrast_log_intensity_diff(torch.from_numpy(z["num_pos"]), torch.from_numpy(z["num_neg"]),
+                                            torch.from_numpy(z["pos_ct"]), torch.from_numpy(z["neg_ct"]))
+    assert np.array_equal(lid.numpy(), z["lid"])
