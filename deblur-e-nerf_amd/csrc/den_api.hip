@@ -1,0 +1,316 @@
+// den_api.hip -- C ABI of libden.so (declared in include/den_api.h).
+// Single translation unit: includes every kernel file.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "../../include/den_api.h"
+#include "den_dw.hip"
+#include "den_misc.hip"
+#include "den_pixbw.hip"
+#include "den_render.hip"
+
+using namespace den;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define DEN_HIP(call)                                                                               \
+  do {                                                                                              \
+    hipError_t e_ = (call);                                                                         \
+    if (e_ != hipSuccess) return fail(DEN_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define DEN_LAUNCHED()                                                                    \
+  do {                                                                                    \
+    hipError_t e_ = hipGetLastError();                                                    \
+    if (e_ != hipSuccess) return fail(DEN_EHIP, std::string("launch: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct WsLayout {
+  size_t act[NACT];
+  size_t rec, bkgd_partial, dw_partial, total;
+  int splits;
+  int64_t per_split;
+};
+
+constexpr int64_t DW_BLOCK_MAX = 8LL * 11 * 1024;  // floats per split for the largest layer (L5: MT 8, NT+1 11)
+
+WsLayout ws_layout(const den_render_desc* d) {
+  WsLayout L{};
+  const int64_t n = (int64_t)d->n_rays * d->n_samples;
+  size_t off = 0;
+  const int es = es_of(d->mode);
+  for (int a = 0; a < NACT; ++a) {
+    L.act[a] = off;
+    if (d->train) off += align256((size_t)n * act_width(d->mode, a) * es);
+  }
+  L.rec = off;
+  if (d->train) off += align256((size_t)n * 16);
+  L.bkgd_partial = off;
+  off += align256((size_t)4 * d->n_rays * 4);
+  // weight-gradient split-K: >= 2048 samples per split, <= 256 splits
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(256, n / 2048));
+  int64_t per = (n + splits - 1) / splits;
+  per = (per + DW_BK_MAX - 1) / DW_BK_MAX * DW_BK_MAX;
+  splits = (n + per - 1) / per;
+  L.splits = (int)splits;
+  L.per_split = per;
+  L.dw_partial = off;
+  if (d->train) off += align256((size_t)splits * DW_BLOCK_MAX * 4);
+  L.total = off;
+  return L;
+}
+
+int check_desc(const den_render_desc* d) {
+  if (!d) return fail(DEN_EINVAL, "null desc");
+  if (d->mode != DEN_MODE_F32 && d->mode != DEN_MODE_BF16) return fail(DEN_EINVAL, "mode must be 0 (F32) or 1 (BF16)");
+  if (d->radiance_dim != 1 && d->radiance_dim != 3) return fail(DEN_EUNSUPPORTED, "radiance_dim must be 1 or 3");
+  if (d->n_rays <= 0) return fail(DEN_EINVAL, "n_rays must be > 0");
+  const int wgs = wg_samples(d->mode);
+  if (d->n_samples < 64 || d->n_samples > wgs || wgs % d->n_samples != 0)
+    return fail(DEN_EUNSUPPORTED, "n_samples must be 64..WG tile (128 F32 / 256 BF16) and divide it");
+  if (((int64_t)d->n_rays * d->n_samples) % wgs != 0)
+    return fail(DEN_EUNSUPPORTED, "n_rays * n_samples must be a multiple of the workgroup tile");
+  return DEN_OK;
+}
+
+template <int MODE>
+RenderArgs<MODE> make_args(const den_render_desc* d, const den_render_io* io, const WsLayout& L) {
+  RenderArgs<MODE> A{};
+  A.n_samples = d->n_samples;
+  A.n_rays = d->n_rays;
+  A.rd = d->radiance_dim;
+  A.train = d->train;
+  A.has_bkgd = d->has_bkgd;
+  A.points = d->points;
+  for (int i = 0; i < 6; ++i) A.aabb[i] = d->aabb[i];
+  A.near_p = d->near_plane;
+  A.far_p = d->far_plane;
+  A.rays_o = io->rays_o;
+  A.rays_d = io->rays_d;
+  A.jitter = io->jitter;
+  A.bias = io->bias_pk;
+  A.bkgd = io->bkgd;
+  char* ws = (char*)io->workspace;
+  for (int a = 0; a < NACT; ++a) A.act[a] = ws ? ws + L.act[a] : nullptr;
+  A.rec = ws ? (float*)(ws + L.rec) : nullptr;
+  A.bkgd_partial = ws ? (float*)(ws + L.bkgd_partial) : nullptr;
+  A.out_rgb = io->out_rgb;
+  A.out_opacity = io->out_opacity;
+  A.out_depth = io->out_depth;
+  return A;
+}
+
+template <int MODE, int MT, int N1, int N2>
+int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, int a_dz, int a_x1, int a_x2,
+              int n1_feat, float* grad, hipStream_t s, int m_off = 0) {
+  DwArgs P{};
+  P.A = ws + L.act[a_dz] + (size_t)m_off * es_of(MODE);
+  P.lda = act_width(MODE, a_dz);
+  P.B1 = ws + L.act[a_x1];
+  P.B2 = a_x2 >= 0 ? ws + L.act[a_x2] : nullptr;
+  P.n = (int64_t)d->n_rays * d->n_samples;
+  P.per_split = L.per_split;
+  P.partial = (float*)(ws + L.dw_partial);
+  hipLaunchKernelGGL((dw_gemm_kernel<MODE, MT, N1, N2>), dim3(L.splits), dim3(64 * MT), 0, s, P);
+  DEN_LAUNCHED();
+  DwReduceArgs R{};
+  R.partial = P.partial;
+  R.splits = L.splits;
+  R.MT = MT;
+  R.NT = (N1 + N2) / 32;
+  R.m_off = m_off;
+  R.layer = layer;
+  R.mode = MODE;
+  R.rd = d->radiance_dim;
+  R.n1 = N1;
+  R.n1_feat = n1_feat;
+  R.grad = grad;
+  const int64_t per = (int64_t)MT * (R.NT + 1) * 1024;
+  hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+template <int MODE>
+int render_fwd_impl(const den_render_desc* d, const den_render_io* io, hipStream_t s) {
+  WsLayout L = ws_layout(d);
+  RenderArgs<MODE> A = make_args<MODE>(d, io, L);
+  A.w = (const char*)io->w_fwd;
+  const int64_t n = (int64_t)d->n_rays * d->n_samples;
+  hipLaunchKernelGGL(render_fwd_kernel<MODE>, dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s, A);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+template <int MODE>
+int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den_render_grad* g, hipStream_t s) {
+  WsLayout L = ws_layout(d);
+  RenderArgs<MODE> A = make_args<MODE>(d, io, L);
+  A.w = (const char*)io->w_bwd;
+  A.d_rgb = g->d_rgb;
+  A.d_opacity = g->d_opacity;
+  A.d_depth = g->d_depth;
+  const int64_t n = (int64_t)d->n_rays * d->n_samples;
+  hipLaunchKernelGGL(render_bwd_kernel<MODE>, dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s, A);
+  DEN_LAUNCHED();
+  char* ws = (char*)io->workspace;
+  float* G = g->grad_params;
+  int rc;
+  if ((rc = launch_dw<MODE, 8, 64, 0>(d, L, ws, 0, D_Z0 + 0, A_PE, -1, 0, G, s)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 1, D_Z0 + 1, A_S0 + 0, -1, 0, G, s)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 2, D_Z0 + 2, A_S0 + 1, -1, 0, G, s)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 3, D_Z0 + 3, A_S0 + 2, -1, 0, G, s)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 4, D_Z0 + 4, A_S0 + 3, -1, 0, G, s)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 8, 256, 64>(d, L, ws, 5, D_Z0 + 5, A_S0 + 4, A_PE, WIDTH, G, s)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 6, D_Z0 + 6, A_S0 + 5, -1, 0, G, s)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 7, D_Z0 + 7, A_S0 + 6, -1, 0, G, s)) != DEN_OK) return rc;
+  // [bottleneck | sigma]: the 256 bottleneck rows, then the sigma tile (row 256)
+  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, L_B, D_ZB, A_S0 + 7, -1, 0, G, s)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 1, 256, 0>(d, L, ws, L_B, D_ZB, A_S0 + 7, -1, 0, G, s, WIDTH)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 4, 256, 32>(d, L, ws, L_G, D_ZG, A_BT, A_VE, WIDTH, G, s)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 1, 128, 0>(d, L, ws, L_R, D_ZR, A_G, -1, 0, G, s)) != DEN_OK) return rc;
+  if (g->grad_bkgd) {
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(256), 0, s, d->radiance_dim, d->n_rays,
+                       (const float*)(ws + L.bkgd_partial), g->grad_bkgd);
+    DEN_LAUNCHED();
+  }
+  return DEN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int den_version(void) { return DEN_VERSION; }
+const char* den_last_error(void) { return g_err.c_str(); }
+
+int64_t den_param_count(int32_t rd) { return (rd == 1 || rd == 3) ? param_count(rd) : -1; }
+int64_t den_param_offset(int32_t rd, int32_t idx) {
+  if ((rd != 1 && rd != 3) || idx < 0 || idx > 24) return -1;
+  return param_offset(rd, idx);
+}
+
+size_t den_packed_fwd_bytes(int32_t mode) { return (mode == 0 || mode == 1) ? (size_t)fwd_bytes(mode) : 0; }
+size_t den_packed_bwd_bytes(int32_t mode) { return (mode == 0 || mode == 1) ? (size_t)bwd_bytes(mode) : 0; }
+size_t den_packed_bias_bytes(int32_t mode) { return (mode == 0 || mode == 1) ? (size_t)bias_floats(mode) * 4 : 0; }
+
+int den_pack_weights(int32_t mode, int32_t rd, const float* params, void* w_fwd, void* w_bwd, float* bias_pk,
+                     void* stream) {
+  if (mode != 0 && mode != 1) return fail(DEN_EINVAL, "bad mode");
+  if (rd != 1 && rd != 3) return fail(DEN_EUNSUPPORTED, "radiance_dim must be 1 or 3");
+  if (!params || !w_fwd || !w_bwd || !bias_pk) return fail(DEN_EINVAL, "null pointer");
+  PackArgs P{mode, rd, params, w_fwd, w_bwd, bias_pk};
+  const int es = es_of(mode);
+  const int64_t total = fwd_bytes(mode) / es + bwd_bytes(mode) / es + bias_floats(mode);
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, P);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+size_t den_render_workspace_bytes(const den_render_desc* d) {
+  if (check_desc(d) != DEN_OK) return 0;
+  return ws_layout(d).total;
+}
+
+int den_render_fwd(const den_render_desc* d, const den_render_io* io, void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (!io || !io->rays_o || !io->rays_d || !io->jitter || !io->w_fwd || !io->bias_pk || !io->out_rgb ||
+      !io->out_opacity || !io->out_depth)
+    return fail(DEN_EINVAL, "null pointer in den_render_io");
+  if (d->has_bkgd && !io->bkgd) return fail(DEN_EINVAL, "has_bkgd but bkgd == NULL");
+  if (d->points && d->has_bkgd) return fail(DEN_EINVAL, "points mode has no background");
+  if (!io->workspace) return fail(DEN_EINVAL, "workspace is required (den_render_workspace_bytes)");
+  return d->mode == 0 ? render_fwd_impl<0>(d, io, (hipStream_t)stream) : render_fwd_impl<1>(d, io, (hipStream_t)stream);
+}
+
+int den_render_bwd(const den_render_desc* d, const den_render_io* io, const den_render_grad* g, void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (!d->train) return fail(DEN_EINVAL, "den_render_bwd needs a train=1 forward");
+  if (!io || !io->workspace || !io->w_bwd || !io->rays_o || !io->rays_d || !io->jitter)
+    return fail(DEN_EINVAL, "null pointer in den_render_io");
+  if (!g || !g->d_rgb || !g->grad_params) return fail(DEN_EINVAL, "null pointer in den_render_grad");
+  if (d->has_bkgd && !io->bkgd) return fail(DEN_EINVAL, "has_bkgd but bkgd == NULL");
+  return d->mode == 0 ? render_bwd_impl<0>(d, io, g, (hipStream_t)stream)
+                      : render_bwd_impl<1>(d, io, g, (hipStream_t)stream);
+}
+
+int den_sum_partials(int32_t n, int32_t nb, const float* part, float* out, void* stream) {
+  if (n <= 0 || nb <= 0 || !part || !out) return fail(DEN_EINVAL, "bad arguments");
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, n, nb, part, out);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_adam_step(int64_t n, float* p, const float* g, float* m, float* v, float lr, float beta1, float beta2,
+                  float eps, float wd, int64_t step, void* stream) {
+  if (n <= 0 || !p || !g || !m || !v || step < 1) return fail(DEN_EINVAL, "bad arguments");
+  // torch forms these in Python double and rounds them to f32 when applied
+  const double b1 = (double)beta1, b2 = (double)beta2;
+  const double bc1 = 1.0 - std::pow(b1, (double)step);
+  const double bc2 = 1.0 - std::pow(b2, (double)step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2s = (float)std::sqrt(bc2);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, p, g, m,
+                     v, step_size, (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), eps, wd, bc2s);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+size_t den_event_loss_workspace_bytes(int32_t N) {
+  const int nb = (N + LOSS_BLOCK - 1) / LOSS_BLOCK;
+  return (size_t)(2 * nb + 2 + nb) * 4;
+}
+
+int den_event_loss_fwd(int32_t N, int32_t fn, const float* x, const float* target, const uint8_t* valid,
+                       const float* c, float* loss, void* ws, void* stream) {
+  if (N <= 0 || fn < 0 || fn > 2 || !x || !c || !loss || !ws) return fail(DEN_EINVAL, "bad arguments");
+  const int nb = (N + LOSS_BLOCK - 1) / LOSS_BLOCK;
+  float* part = (float*)ws;
+  float* count = part + 2 * nb;
+  hipLaunchKernelGGL(loss_partial_kernel, dim3(nb), dim3(LOSS_BLOCK), 0, (hipStream_t)stream, N, fn, x, target, valid,
+                     c, part);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(LOSS_BLOCK), 0, (hipStream_t)stream, nb, part, loss, count);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_event_loss_bwd(int32_t N, int32_t fn, const float* x, const float* target, const uint8_t* valid,
+                       const float* c, const float* gout, float* d_x, float* d_target, float* d_c, void* ws,
+                       void* stream) {
+  if (N <= 0 || fn < 0 || fn > 2 || !x || !c || !gout || !d_x || !d_c || !ws) return fail(DEN_EINVAL, "bad arguments");
+  const int nb = (N + LOSS_BLOCK - 1) / LOSS_BLOCK;
+  float* part = (float*)ws;
+  float* count = part + 2 * nb;
+  float* dcp = count + 2;
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3(nb), dim3(LOSS_BLOCK), 0, (hipStream_t)stream, N, fn, x, target, valid, c,
+                     gout, count, d_x, d_target, dcp);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, 1, nb, (const float*)dcp, d_c);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_event_target(int32_t N, const double* ts_diff, const float* lid, const int64_t* end_ts,
+                     const double* start_ts, const float* c, float* target, void* stream) {
+  if (N <= 0 || !ts_diff || !lid || !end_ts || !start_ts || !c || !target) return fail(DEN_EINVAL, "bad arguments");
+  hipLaunchKernelGGL(event_target_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, N, ts_diff, lid,
+                     end_ts, start_ts, c, target);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+}  // extern "C"

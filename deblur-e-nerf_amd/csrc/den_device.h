@@ -1,0 +1,269 @@
+// den_device.h -- device-side helpers: MFMA traits, exact-f32 sampler math,
+// activations, wave scans, weight-chunk staging.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "den_geom.h"
+
+namespace den {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int MODE> struct Tr;
+
+// BF16 perf mode: v_mfma_f32_32x32x16_bf16. Lane l: col = l&31, group h = l>>5.
+template <> struct Tr<1> {
+  static constexpr int TM = 32, KI = 16, NG = 2, REGS = 16, FPT = 2 /* frags per tile */;
+  using Acc = f32x16;
+  using Frag = bf16x8;
+  static __device__ __forceinline__ Acc mfma(const Frag& a, const Frag& b, const Acc& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ Frag zero_frag() {
+    Frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (__bf16)0.0f;
+    return f;
+  }
+};
+
+// F32 parity mode: v_mfma_f32_16x16x4_f32 (exact f32 FMA chain). Lane l: col = l&15, group g = l>>4.
+template <> struct Tr<0> {
+  static constexpr int TM = 16, KI = 4, NG = 4, REGS = 4, FPT = 4;
+  using Acc = f32x4;
+  using Frag = float;
+  static __device__ __forceinline__ Acc mfma(float a, float b, const Acc& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ Frag zero_frag() { return 0.0f; }
+};
+
+template <int MODE>
+__device__ __forceinline__ void acc_to_frags(const typename Tr<MODE>::Acc& a, typename Tr<MODE>::Frag* f) {
+  if constexpr (MODE == 1) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)a[8 * s + j];
+      f[s] = v;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f[r] = a[r];
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ typename Tr<MODE>::Acc acc_zero() {
+  typename Tr<MODE>::Acc a;
+#pragma unroll
+  for (int r = 0; r < Tr<MODE>::REGS; ++r) a[r] = 0.0f;
+  return a;
+}
+
+// Store a lane's REGS accumulator values (stored order) as operand dtype.
+template <int MODE>
+__device__ __forceinline__ void store_tile_vals(void* row_base_bytes, const typename Tr<MODE>::Acc& a) {
+  if constexpr (MODE == 1) {
+    uint32_t w[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      __bf16 lo = (__bf16)a[2 * q], hi = (__bf16)a[2 * q + 1];
+      w[q] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+    }
+    uint4* p = (uint4*)row_base_bytes;
+    p[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    p[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  } else {
+    *(f32x4*)row_base_bytes = a;
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ typename Tr<MODE>::Acc load_tile_vals(const void* row_base_bytes) {
+  typename Tr<MODE>::Acc a;
+  if constexpr (MODE == 1) {
+    const uint4* p = (const uint4*)row_base_bytes;
+    uint4 u0 = p[0], u1 = p[1];
+    uint32_t w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      a[2 * q] = __uint_as_float(w[q] << 16);
+      a[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  } else {
+    a = *(const f32x4*)row_base_bytes;
+  }
+  return a;
+}
+
+// ------------------------------------------------------------------ activations
+// torch.nn.functional.softplus(x, beta, threshold=20) and its derivative.
+template <bool EXACT>
+__device__ __forceinline__ float softplus_b100(float z) {
+  float bz = z * 100.0f;
+  if (bz > 20.0f) return z;
+  if constexpr (EXACT) return log1pf(expf(bz)) / 100.0f;
+  else return __logf(1.0f + __expf(bz)) * 0.01f;
+}
+// derivative from the activation's own output s = softplus(z): sigmoid(100 z) = 1 - exp(-100 s)
+template <bool EXACT>
+__device__ __forceinline__ float dsoftplus_b100_from_out(float s) {
+  if constexpr (EXACT) return -expm1f(-100.0f * s);
+  else return 1.0f - __expf(-100.0f * s);
+}
+__device__ __forceinline__ float softplus_b1(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+
+// ------------------------------------------------------------------ exact f32 sampler math
+// Mirrors oracle/nerf.py op-for-op (no FMA contraction), so that positions and
+// hence encodings are bit-identical to the PyTorch CPU restatement.
+struct RayGeom {
+  float tmin, span;  // span = 0 for a ray that misses the box
+};
+
+__device__ __forceinline__ RayGeom ray_geom(const float* o, const float* d, const float* aabb, float near_p,
+                                            float far_p) {
+#pragma clang fp contract(off)
+  float tmn = -INFINITY, tmx = INFINITY;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float inv = __fdiv_rn(1.0f, d[a]);
+    float t1 = (aabb[a] - o[a]) * inv;
+    float t2 = (aabb[3 + a] - o[a]) * inv;
+    tmn = fmaxf(tmn, fminf(t1, t2));
+    tmx = fminf(tmx, fmaxf(t1, t2));
+  }
+  if (near_p >= 0.0f) tmn = fmaxf(tmn, near_p);
+  if (far_p >= 0.0f) tmx = fminf(tmx, far_p);
+  RayGeom g;
+  g.tmin = tmn;
+  g.span = (tmx > tmn) ? (tmx - tmn) : 0.0f;
+  return g;
+}
+
+__device__ __forceinline__ void sample_interval(const RayGeom& g, int k, float u, int n, float* t0, float* t1) {
+#pragma clang fp contract(off)
+  float s = __fdiv_rn((float)k + u, (float)n);
+  float mid = g.tmin + s * g.span;
+  float half = 0.5f * __fdiv_rn(g.span, (float)n);
+  *t0 = mid - half;
+  *t1 = mid + half;
+}
+
+// contracted position x' = 2*pi*((x - lo)/(hi - lo) - 0.5) and selector
+__device__ __forceinline__ void contract(const float* o, const float* d, float t0, float t1, const float* aabb,
+                                         float* xc, float* sel) {
+#pragma clang fp contract(off)
+  float tt = t0 + t1;
+  bool in = true;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float pos = o[a] + __fdiv_rn(d[a] * tt, 2.0f);
+    float xh = __fdiv_rn(pos - aabb[a], aabb[3 + a] - aabb[a]);
+    in = in && (xh > 0.0f) && (xh < 1.0f);
+    xc[a] = 6.2831855f * (xh - 0.5f);
+  }
+  *sel = in ? 1.0f : 0.0f;
+}
+
+__device__ __forceinline__ void contract_point(const float* pos, const float* aabb, float* xc, float* sel) {
+#pragma clang fp contract(off)
+  bool in = true;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float xh = __fdiv_rn(pos[a] - aabb[a], aabb[3 + a] - aabb[a]);
+    in = in && (xh > 0.0f) && (xh < 1.0f);
+    xc[a] = 6.2831855f * (xh - 0.5f);
+  }
+  *sel = in ? 1.0f : 0.0f;
+}
+
+// encoding feature f of [v, sin(v*2^k), sin(v*2^k + pi/2)] (scale-major, dim-minor)
+template <bool EXACT>
+__device__ __forceinline__ float enc_feature(const float* v, int f, int n_deg) {
+#pragma clang fp contract(off)
+  const int nd = 3 * n_deg;
+  if (f < 3) return v[f];
+  if (f < 3 + 2 * nd) {
+    int q = f - 3;
+    bool cosine = q >= nd;
+    if (cosine) q -= nd;
+    float xb = v[q % 3] * (float)(1 << (q / 3));
+    if (cosine) xb = xb + 1.5707964f;
+    if constexpr (EXACT) return sinf(xb);
+    else return __sinf(xb);
+  }
+  return 0.0f;
+}
+
+// ------------------------------------------------------------------ wave primitives
+__device__ __forceinline__ float wave_incl_scan(float v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    float o = __shfl_up(v, off, 64);
+    if (lane >= off) v += o;
+  }
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ------------------------------------------------------------------ weight chunk staging
+// A chunk (one packed TM-row tile of a layer, <= 20 KiB) is copied global ->
+// registers (issued before the MFMA block of the current chunk) -> LDS
+// (written after it), double-buffered, one barrier per chunk.
+constexpr int WG_THREADS = 512;
+constexpr int CHUNK_MAX = 64 * 320;  // 20 KiB
+constexpr int STAGE_ROUNDS = (CHUNK_MAX + WG_THREADS * 16 - 1) / (WG_THREADS * 16);
+
+struct Stage {
+  uint4 v[STAGE_ROUNDS];
+};
+__device__ __forceinline__ void stage_load(Stage& st, const char* g, int bytes) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < STAGE_ROUNDS; ++q) {
+    int off = q * WG_THREADS * 16 + t * 16;
+    if (off < bytes) st.v[q] = *(const uint4*)(g + off);
+  }
+}
+__device__ __forceinline__ void stage_store(const Stage& st, char* lds, int bytes) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < STAGE_ROUNDS; ++q) {
+    int off = q * WG_THREADS * 16 + t * 16;
+    if (off < bytes) *(uint4*)(lds + off) = st.v[q];
+  }
+}
+
+// MFMA block over one LDS chunk: acc += A(chunk) * B(x[0..KS)).
+template <int MODE, int KS>
+__device__ __forceinline__ void mfma_chunk(const char* lds_chunk, const typename Tr<MODE>::Frag* x,
+                                           typename Tr<MODE>::Acc& acc) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (MODE == 1) {
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      bf16x8 a = *(const bf16x8*)(lds_chunk + k * 1024 + lane * 16);
+      acc = Tr<1>::mfma(a, x[k], acc);
+    }
+  } else {
+    static_assert(KS % 4 == 0, "f32 k-steps come in groups of 4");
+#pragma unroll
+    for (int k4 = 0; k4 < KS / 4; ++k4) {
+      f32x4 a = *(const f32x4*)(lds_chunk + k4 * 1024 + lane * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = Tr<0>::mfma(a[q], x[4 * k4 + q], acc);
+    }
+  }
+}
+
+}  // namespace den

@@ -1,0 +1,227 @@
+// den_dw.hip -- weight/bias gradients of the fused MLP:
+//   dW_l[o][i] = sum_n dz_l[n][o] * x_l[n][i],   db_l[o] = sum_n dz_l[n][o]
+// a GEMM whose contraction runs over all ray samples (16.8M at the benchmark
+// size).  Split-K over samples: workgroup s owns a contiguous sample range
+// and the WHOLE (M x N) output of the layer, so every byte of dz and x is read
+// from HBM exactly once.  One wave per 32-row tile of dz; each wave keeps all
+// N/32 column tiles (+ one all-ones tile that yields db) in accumulators.
+// Partials are reduced deterministically by dw_reduce_kernel, which also undoes
+// the stored-order permutation and scatters into the reference's flat
+// parameter layout (den_geom.h param_offset).
+//
+// BF16: v_mfma_f32_32x32x16_bf16, operands with samples as k read from a
+//       row-major [sample][feature] LDS image by ds_read_b64_tr_b16.
+// F32 : v_mfma_f32_32x32x2_f32, plain ds_read_b32 fragments.
+#include "den_device.h"
+
+namespace den {
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+struct DwArgs {
+  const char* A;       // dz  [n][lda] (stored order; the GEMM uses columns [0, M))
+  int lda;             // row pitch of A in elements
+  const char* B1;      // x   [n][N1]
+  const char* B2;      // x'  [n][N2] (second input segment, may be null when N2 = 0)
+  int64_t n;           // samples
+  int64_t per_split;   // samples per split (multiple of 32)
+  float* partial;      // [splits][MT][NT+1][64 lanes][16]
+};
+
+constexpr int DW_BK_MAX = 32;  // samples per LDS stage (16 for register-heavy shapes)
+
+template <int MODE>
+DEN_HD constexpr int dw_pad_bytes(int W) {
+  // BF16: choose the row pitch so that 4 consecutive rows start 16 banks apart
+  // (conflict-free transposed reads); F32 reads are conflict-free for any pitch.
+  return MODE == 1 ? 4 * (((16 - (W / 2)) % 64 + 64) % 64) : 16;
+}
+
+template <int MODE, int MT, int N1, int N2>
+__global__ __launch_bounds__(64 * MT) void dw_gemm_kernel(DwArgs P) {
+  constexpr int M = 32 * MT, N = N1 + N2, NT = N / 32;
+  constexpr int DW_BK = (NT + 1) * 16 > 160 ? 16 : 32;
+  constexpr int ES = es_of(MODE);
+  constexpr int PA = M * ES + dw_pad_bytes<MODE>(M), PB = N * ES + dw_pad_bytes<MODE>(N);
+  constexpr int IMG = DW_BK * (PA + PB);
+  constexpr int THREADS = 64 * MT;
+  constexpr int UA = M * ES / 16, UB1 = N1 * ES / 16, UB2 = N2 * ES / 16, UB = UB1 + UB2;  // 16-B units per row
+  constexpr int UNITS = DW_BK * (UA + UB);
+  constexpr int UPT = (UNITS + THREADS - 1) / THREADS;
+  __shared__ __attribute__((aligned(16))) char lds[2 * IMG];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t k_begin = (int64_t)blockIdx.x * P.per_split;
+  const int64_t k_end = min(P.n, k_begin + P.per_split);
+  const int nchunks = (int)((k_end - k_begin + DW_BK - 1) / DW_BK);
+
+  f32x16 acc[NT + 1];
+#pragma unroll
+  for (int t = 0; t <= NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+
+  uint4 st[UPT];
+  auto load = [&](int ch) {
+    const int64_t k0 = k_begin + (int64_t)ch * DW_BK;
+#pragma unroll
+    for (int q = 0; q < UPT; ++q) {
+      int u = q * THREADS + threadIdx.x;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (u < UNITS) {
+        int row = u / (UA + UB), cu = u % (UA + UB);
+        int64_t kr = k0 + row;
+        if (kr < k_end) {
+          const char* src;
+          if (cu < UA) src = P.A + kr * ((int64_t)P.lda * ES) + cu * 16;
+          else if (cu < UA + UB1) src = P.B1 + kr * (N1 * ES) + (cu - UA) * 16;
+          else src = P.B2 + kr * (N2 * ES) + (cu - UA - UB1) * 16;
+          v = *(const uint4*)src;
+        }
+      }
+      st[q] = v;
+    }
+  };
+  auto store = [&](int slot) {
+    char* img = lds + slot * IMG;
+#pragma unroll
+    for (int q = 0; q < UPT; ++q) {
+      int u = q * THREADS + threadIdx.x;
+      if (u < UNITS) {
+        int row = u / (UA + UB), cu = u % (UA + UB);
+        char* dst = cu < UA ? img + row * PA + cu * 16 : img + DW_BK * PA + row * PB + (cu - UA) * 16;
+        *(uint4*)dst = st[q];
+      }
+    }
+  };
+
+  if (nchunks > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const bool more = ch + 1 < nchunks;
+    if (more) load(ch + 1);
+    const char* imgA = lds + (ch & 1) * IMG;
+    const char* imgB = imgA + DW_BK * PA;
+    if constexpr (MODE == 1) {
+      // ones fragment (bf16 1.0 = 0x3f80)
+      bf16x8 ones;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+      const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1, h = lane >> 5;
+#pragma unroll
+      for (int kk = 0; kk < DW_BK / 16; ++kk) {
+        const int row0 = kk * 16 + 8 * h + q;
+        auto tr_frag = [&](const char* img, int pitch, int col0) {
+          const char* a0 = img + row0 * pitch + (col0 + 16 * g1 + 4 * p) * 2;
+          v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
+          v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(a0 + 4 * pitch));
+          bf16x8 f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            f[j] = __builtin_bit_cast(__bf16, (short)lo[j]);
+            f[4 + j] = __builtin_bit_cast(__bf16, (short)hi[j]);
+          }
+          return f;
+        };
+        bf16x8 a = tr_frag(imgA, PA, 32 * wave);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          bf16x8 b = tr_frag(imgB, PB, 32 * t);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[t], 0, 0, 0);
+        }
+        acc[NT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, ones, acc[NT], 0, 0, 0);
+      }
+    } else {
+      const int c = lane & 31, h = lane >> 5;
+#pragma unroll 4
+      for (int kk = 0; kk < DW_BK / 2; ++kk) {
+        const int row = 2 * kk + h;
+        float a = *(const float*)(imgA + row * PA + (32 * wave + c) * 4);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          float b = *(const float*)(imgB + row * PB + (32 * t + c) * 4);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+        }
+        acc[NT] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, 1.0f, acc[NT], 0, 0, 0);
+      }
+    }
+    if (more) store((ch + 1) & 1);
+    __syncthreads();
+  }
+
+  float* out = P.partial + (((int64_t)blockIdx.x * MT + wave) * (NT + 1)) * 1024;
+#pragma unroll
+  for (int t = 0; t <= NT; ++t) {
+    f32x4* o4 = (f32x4*)(out + t * 1024 + lane * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+      o4[q] = v;
+    }
+  }
+}
+
+// Reduce over splits + scatter into the flat parameter gradient.
+// Element e of the [MT][NT+1][64][16] block: tile (mt, nt), lane, reg.
+struct DwReduceArgs {
+  const float* partial;
+  int splits, MT, NT;
+  int m_off;       // chain-feature offset of A's first column (stored order)
+  int layer;       // forward layer id (den_geom.h)
+  int mode;        // chain mode (stored-order permutation)
+  int rd;
+  int n1;          // width of the first input segment (features of x before the second segment)
+  int n1_feat;     // chain-feature offset of the second segment (e.g. 256 for [h4, pe])
+  float* grad;     // flat params layout
+};
+
+__global__ void dw_reduce_kernel(DwReduceArgs R) {
+  const int64_t per = (int64_t)R.MT * (R.NT + 1) * 1024;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= per) return;
+  float s = 0.0f;
+  for (int sp = 0; sp < R.splits; ++sp) s += R.partial[sp * per + e];
+  const int reg = (int)(e & 15), lane = (int)((e >> 4) & 63);
+  const int64_t tile = e >> 10;
+  const int nt = (int)(tile % (R.NT + 1)), mt = (int)(tile / (R.NT + 1));
+  const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5), col = lane & 31;
+  // stored position -> chain feature (per TM-wide tile of the chain mode)
+  const int TMc = tm_of(R.mode);
+  const int m = R.m_off + 32 * mt + row;
+  const int o = (m / TMc) * TMc + stored_to_row(R.mode, m % TMc);
+  int t, rr, cc;
+  if (nt == R.NT) {  // ones tile -> bias gradient (column 0 only)
+    if (col != 0) return;
+    if (!ref_bias_coord(R.layer, o, R.rd, &t, &rr)) return;
+    R.grad[param_offset(R.rd, 2 * t + 1) + rr] = s;
+    return;
+  }
+  const int n = 32 * nt + col;
+  int f;
+  if (n < R.n1) f = (n / TMc) * TMc + stored_to_row(R.mode, n % TMc);
+  else {
+    int n2 = n - R.n1;
+    f = R.n1_feat + (n2 / TMc) * TMc + stored_to_row(R.mode, n2 % TMc);
+  }
+  if (!ref_coord(R.layer, o, f, R.rd, &t, &rr, &cc)) return;
+  R.grad[param_offset(R.rd, 2 * t) + (int64_t)rr * ref_in(t) + cc] = s;
+}
+
+template __global__ void dw_gemm_kernel<1, 8, 64, 0>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 8, 256, 0>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 8, 256, 64>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 4, 256, 32>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 1, 128, 0>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 1, 256, 0>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 8, 64, 0>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 8, 256, 0>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 8, 256, 64>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 1, 256, 0>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 4, 256, 32>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 1, 128, 0>(DwArgs);
+
+}  // namespace den

@@ -1,0 +1,230 @@
+// den_misc.hip -- weight packing, Adam, deterministic partial sums, event loss.
+#include "den_device.h"
+
+namespace den {
+
+// ------------------------------------------------------------------ weight packing
+// One thread per packed element.  Forward chunk (layer l, row tile i):
+//   BF16: [kappa][lane][8]   lane -> row 32i+(lane&31), group lane>>5, element j
+//   F32 : [kappa/4][lane][4] lane -> row 16i+(lane&15), group lane>>4
+// element = W_l[row][chain_feature(kappa, group, j)].
+// Backward chunk (transposed layer j, row tile i): rows = chain inputs of
+// layer bwd_layer(j), k = its (padded) outputs: element = W_l[out][in].
+struct PackArgs {
+  int mode, rd;
+  const float* params;
+  void* w_fwd;
+  void* w_bwd;
+  float* bias;
+};
+
+__device__ __forceinline__ float param_w(const PackArgs& P, int l, int o, int f) {
+  int t, r, c;
+  if (!ref_coord(l, o, f, P.rd, &t, &r, &c)) return 0.0f;
+  return P.params[param_offset(P.rd, 2 * t) + (int64_t)r * ref_in(t) + c];
+}
+
+__device__ __forceinline__ void decode_elem(int mode, int64_t e, int* kappa, int* lane, int* j) {
+  if (mode == 1) {
+    *kappa = (int)(e / 512);
+    *lane = (int)((e / 8) % 64);
+    *j = (int)(e % 8);
+  } else {
+    *kappa = (int)((e / 256) * 4 + (e % 4));
+    *lane = (int)((e / 4) % 64);
+    *j = 0;
+  }
+}
+
+__global__ void pack_kernel(PackArgs P) {
+  const int mode = P.mode, TM = tm_of(mode), ES = es_of(mode);
+  const int64_t nf = fwd_bytes(mode) / ES, nb = bwd_bytes(mode) / ES, nbias = bias_floats(mode);
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < nf) {
+    int l = 0;
+    while (l + 1 < NL && fwd_layer_offset(mode, l + 1) / ES <= e) ++l;
+    const int64_t in_layer = e - fwd_layer_offset(mode, l) / ES;
+    const int64_t per_chunk = chunk_bytes_K(fwd_K(mode, l)) / ES;
+    const int i = (int)(in_layer / per_chunk);
+    int kappa, lane, j;
+    decode_elem(mode, in_layer % per_chunk, &kappa, &lane, &j);
+    const int grp = lane / TM;
+    const int o = TM * i + lane % TM;
+    const float v = param_w(P, l, o, chain_feature(mode, kappa, grp, j));
+    if (mode == 1) ((__bf16*)P.w_fwd)[e] = (__bf16)v;
+    else ((float*)P.w_fwd)[e] = v;
+    return;
+  }
+  e -= nf;
+  if (e < nb) {
+    int jb = 0;
+    while (jb + 1 < NBL && bwd_layer_offset(mode, jb + 1) / ES <= e) ++jb;
+    const int l = bwd_layer(jb);
+    const int64_t in_layer = e - bwd_layer_offset(mode, jb) / ES;
+    const int64_t per_chunk = chunk_bytes_K(bwd_K(mode, jb)) / ES;
+    const int i = (int)(in_layer / per_chunk);
+    int kappa, lane, j;
+    decode_elem(mode, in_layer % per_chunk, &kappa, &lane, &j);
+    const int grp = lane / TM;
+    const int in_f = TM * i + lane % TM;
+    const int out_f = chain_feature(mode, kappa, grp, j);
+    const float v = param_w(P, l, out_f, in_f);
+    if (mode == 1) ((__bf16*)P.w_bwd)[e] = (__bf16)v;
+    else ((float*)P.w_bwd)[e] = v;
+    return;
+  }
+  e -= nb;
+  if (e < nbias) {
+    const int chunk = (int)(e / TM), q = (int)(e % TM);
+    int l = 0;
+    while (l + 1 < NL && fwd_chunk_index(mode, l + 1) <= chunk) ++l;
+    const int i = chunk - fwd_chunk_index(mode, l);
+    const int o = TM * i + stored_to_row(mode, q);
+    int t, r;
+    P.bias[e] = ref_bias_coord(l, o, P.rd, &t, &r) ? P.params[param_offset(P.rd, 2 * t + 1) + r] : 0.0f;
+  }
+}
+
+// ------------------------------------------------------------------ Adam (torch.optim.Adam, single-tensor path)
+//   g += wd * p ; m.lerp_(g, 1-b1) ; v = v*b2 + (1-b2)*g*g
+//   p += -(lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+// Scalars are formed in double on the host and rounded to f32 exactly as torch
+// rounds its Python-float scalars.
+__global__ void adam_kernel(int64_t n, float* p, const float* g, float* m, float* v, float step_size, float w1,
+                            float b2, float w2, float eps, float wd, float bc2_sqrt) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float gi = g[i];
+  const float pi = p[i];
+  if (wd != 0.0f) gi = gi + wd * pi;
+  const float mo = m[i];
+  const float mi = w1 < 0.5f ? mo + w1 * (gi - mo) : gi - (gi - mo) * (1.0f - w1);
+  const float vi = v[i] * b2 + w2 * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] = pi + (-step_size) * (mi / denom);
+}
+
+// ------------------------------------------------------------------ partial sums
+__global__ void sum_partials_kernel(int n, int nb, const float* part, float* out) {
+  const int j = blockIdx.x;
+  if (j >= n) return;
+  float s = 0.0f;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) s += part[(int64_t)j * nb + b];
+  __shared__ float red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[j] = red[0];
+}
+
+// ------------------------------------------------------------------ event loss (loss.py:34-96)
+__device__ __forceinline__ float err_fn(int fn, float d) {
+  float ad = fabsf(d);
+  if (fn == 0) return ad;                                   // l1
+  if (fn == 1) return d * d;                                // mse
+  return ad < 1.0f ? 0.5f * d * d : (ad - 0.5f);            // huber, delta = 1
+}
+__device__ __forceinline__ float derr_fn(int fn, float d) {
+  if (fn == 0) return d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+  if (fn == 1) return 2.0f * d;
+  return d < -1.0f ? -1.0f : (d > 1.0f ? 1.0f : d);
+}
+
+constexpr int LOSS_BLOCK = 256;
+
+// pass 1: per-block (sum err, count)
+__global__ void loss_partial_kernel(int N, int fn, const float* x, const float* target, const uint8_t* valid,
+                                    const float* c, float* part) {
+  __shared__ float se[LOSS_BLOCK], sc[LOSS_BLOCK];
+  int i = blockIdx.x * LOSS_BLOCK + threadIdx.x;
+  float e = 0.0f, k = 0.0f;
+  if (i < N && (!valid || valid[i])) {
+    float a = x[i] / c[0];
+    float t = target ? target[i] : 0.0f;
+    e = err_fn(fn, a - t);
+    k = 1.0f;
+  }
+  se[threadIdx.x] = e;
+  sc[threadIdx.x] = k;
+  __syncthreads();
+  for (int w = LOSS_BLOCK / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      se[threadIdx.x] += se[threadIdx.x + w];
+      sc[threadIdx.x] += sc[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = se[0];
+    part[gridDim.x + blockIdx.x] = sc[0];
+  }
+}
+// pass 2: fixed-order final sum -> loss, count
+__global__ void loss_final_kernel(int nb, const float* part, float* loss, float* count) {
+  __shared__ float se[LOSS_BLOCK], sc[LOSS_BLOCK];
+  float e = 0.0f, k = 0.0f;
+  for (int b = threadIdx.x; b < nb; b += LOSS_BLOCK) {
+    e += part[b];
+    k += part[nb + b];
+  }
+  se[threadIdx.x] = e;
+  sc[threadIdx.x] = k;
+  __syncthreads();
+  for (int w = LOSS_BLOCK / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      se[threadIdx.x] += se[threadIdx.x + w];
+      sc[threadIdx.x] += sc[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    loss[0] = se[0] / sc[0];  // NaN on zero valid events, as torch's empty mean
+    count[0] = sc[0];
+  }
+}
+// backward: dL/dx, dL/dtarget per event, per-block partials of dL/dc
+__global__ void loss_bwd_kernel(int N, int fn, const float* x, const float* target, const uint8_t* valid,
+                                const float* c, const float* gout, const float* count, float* dx, float* dtarget,
+                                float* dc_part) {
+  __shared__ float sd[LOSS_BLOCK];
+  int i = blockIdx.x * LOSS_BLOCK + threadIdx.x;
+  float dcv = 0.0f;
+  if (i < N) {
+    float gx = 0.0f, gt = 0.0f;
+    if (!valid || valid[i]) {
+      const float cc = c[0];
+      float a = x[i] / cc;
+      float t = target ? target[i] : 0.0f;
+      float gerr = gout[0] / count[0];
+      float de = derr_fn(fn, a - t) * gerr;
+      gx = de / cc;
+      gt = -de;
+      dcv = de * (-x[i] / (cc * cc));
+    }
+    dx[i] = gx;
+    if (dtarget) dtarget[i] = gt;
+  }
+  sd[threadIdx.x] = dcv;
+  __syncthreads();
+  for (int w = LOSS_BLOCK / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) sd[threadIdx.x] += sd[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dc_part[blockIdx.x] = sd[0];
+}
+
+// target (loss.py:74-77): f32( ts_diff * (lid / (end - start)) / c ), f64 arithmetic
+__global__ void event_target_kernel(int N, const double* ts_diff, const float* lid, const int64_t* end_ts,
+                                    const double* start_ts, const float* c, float* target) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double grad = (double)lid[i] / ((double)end_ts[i] - start_ts[i]);
+  target[i] = (float)(ts_diff[i] * grad / (double)c[0]);
+}
+
+}  // namespace den

@@ -1,0 +1,287 @@
+"""ctypes binding of libden.so (include/den_api.h) + torch.autograd Functions.
+
+This is the ONLY compute path of the package: there is no CPU or PyTorch
+fallback.  If libden.so is missing, or no HIP device is present, every op
+raises.  PyTorch provides device memory (the caching allocator), the current
+HIP stream and autograd plumbing; the arithmetic happens in the HIP kernels.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DEN_LIB", os.path.join(os.path.dirname(_HERE), "libden.so"))
+
+MODE_F32 = 0
+MODE_BF16 = 1
+_MODES = {"f32": MODE_F32, "fp32": MODE_F32, "float32": MODE_F32, "bf16": MODE_BF16, "bfloat16": MODE_BF16}
+ERROR_FNS = {"l1": 0, "mse": 1, "huber": 2}
+
+
+class DenError(RuntimeError):
+    pass
+
+
+class RenderDesc(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("radiance_dim", ctypes.c_int32), ("n_rays", ctypes.c_int32),
+                ("n_samples", ctypes.c_int32), ("aabb", ctypes.c_float * 6), ("near_plane", ctypes.c_float),
+                ("far_plane", ctypes.c_float), ("train", ctypes.c_int32), ("has_bkgd", ctypes.c_int32),
+                ("points", ctypes.c_int32)]
+
+
+class RenderIO(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("rays_o", "rays_d", "jitter", "w_fwd", "w_bwd", "bias_pk", "bkgd",
+                                               "workspace", "out_rgb", "out_opacity", "out_depth")]
+
+
+class RenderGrad(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("d_rgb", "d_opacity", "d_depth", "grad_params", "grad_bkgd")]
+
+
+_lib = None
+
+_SIGS = {
+    "den_version": (ctypes.c_int, []),
+    "den_last_error": (ctypes.c_char_p, []),
+    "den_param_count": (ctypes.c_int64, [ctypes.c_int32]),
+    "den_param_offset": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    "den_packed_fwd_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "den_packed_bwd_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "den_packed_bias_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "den_pack_weights": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 5),
+    "den_render_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(RenderDesc)]),
+    "den_render_fwd": (ctypes.c_int, [ctypes.POINTER(RenderDesc), ctypes.POINTER(RenderIO), ctypes.c_void_p]),
+    "den_render_bwd": (ctypes.c_int, [ctypes.POINTER(RenderDesc), ctypes.POINTER(RenderIO),
+                                      ctypes.POINTER(RenderGrad), ctypes.c_void_p]),
+    "den_sum_partials": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p]),
+    "den_adam_step": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_float] * 5
+                      + [ctypes.c_int64, ctypes.c_void_p]),
+    "den_event_loss_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "den_event_loss_fwd": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 7),
+    "den_event_loss_bwd": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 10),
+    "den_event_target": (ctypes.c_int, [ctypes.c_int32] + [ctypes.c_void_p] * 7),
+    "den_pixbw_sample_ts": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]),
+    "den_pixbw_fwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 10),
+    "den_pixbw_blocks": (ctypes.c_int, [ctypes.c_int32]),
+    "den_pixbw_bwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 14),
+}
+
+
+def lib():
+    """Load libden.so (raises DenError if it is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DenError(f"HIP library not found at {LIB_PATH}: build it with `python __graft_entry__.py` "
+                           "(there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return sorted(_SIGS)
+
+
+def _check(rc):
+    if rc != 0:
+        raise DenError(f"libden error {rc}: {lib().den_last_error().decode()}")
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_device(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise DenError("libden ops need HIP device tensors (there is no CPU fallback)")
+
+
+def mode_id(mode):
+    if isinstance(mode, int):
+        return mode
+    return _MODES[str(mode).lower()]
+
+
+def param_count(rd):
+    return lib().den_param_count(rd)
+
+
+def param_offset(rd, idx):
+    return lib().den_param_offset(rd, idx)
+
+
+# ----------------------------------------------------------------------------- packed weights
+class PackedWeights:
+    """Device buffers holding the MFMA fragment layouts of the MLP weights."""
+
+    def __init__(self, mode, rd, device):
+        L = lib()
+        self.mode, self.rd = mode_id(mode), rd
+        self.fwd = torch.empty(L.den_packed_fwd_bytes(self.mode), dtype=torch.uint8, device=device)
+        self.bwd = torch.empty(L.den_packed_bwd_bytes(self.mode), dtype=torch.uint8, device=device)
+        self.bias = torch.empty(L.den_packed_bias_bytes(self.mode) // 4, dtype=torch.float32, device=device)
+        self.version = None
+
+    def pack(self, flat_params):
+        _require_device(flat_params)
+        assert flat_params.dtype == torch.float32 and flat_params.is_contiguous()
+        _check(lib().den_pack_weights(self.mode, self.rd, _ptr(flat_params), _ptr(self.fwd), _ptr(self.bwd),
+                                      _ptr(self.bias), _stream(flat_params.device)))
+
+
+# ----------------------------------------------------------------------------- render
+def _desc(cfg, n_rays, n_samples, train, has_bkgd, points=False):
+    d = RenderDesc()
+    d.mode = cfg["mode"]
+    d.radiance_dim = cfg["rd"]
+    d.n_rays = n_rays
+    d.n_samples = n_samples
+    for i, v in enumerate(cfg["aabb"]):
+        d.aabb[i] = float(v)
+    d.near_plane = -1.0 if cfg.get("near") is None else float(cfg["near"])
+    d.far_plane = -1.0 if cfg.get("far") is None else float(cfg["far"])
+    d.train = int(train)
+    d.has_bkgd = int(has_bkgd)
+    d.points = int(points)
+    return d
+
+
+def wg_samples(mode):
+    return 128 if mode_id(mode) == MODE_F32 else 256
+
+
+def render_workspace_bytes(desc):
+    n = lib().den_render_workspace_bytes(ctypes.byref(desc))
+    if n == 0:
+        raise DenError(lib().den_last_error().decode())
+    return n
+
+
+class RenderFunction(torch.autograd.Function):
+    """Fused sampler + encoding + MLP + compositing (den_render_fwd/bwd).
+
+    inputs: rays_o (R,3), rays_d (R,3), jitter (R), bkgd (rd) or None, flat
+    params (P,) f32, plus non-tensor config; outputs colour (R,rd), opacity (R),
+    depth (R) (un-normalised).  ``points=True`` evaluates the radiance field at
+    given points instead: rays_o = positions (n,3), rays_d = directions (n,3),
+    outputs rgb (n,rd), sigma (n), unused (n)."""
+
+    @staticmethod
+    def forward(ctx, rays_o, rays_d, jitter, bkgd, flat, cfg, packed, n_samples, points):
+        _require_device(rays_o, rays_d, jitter, bkgd, flat)
+        R = rays_o.shape[0]
+        rd = cfg["rd"]
+        train = torch.is_grad_enabled() and (flat.requires_grad or (bkgd is not None and bkgd.requires_grad))
+        train = train or ctx.needs_input_grad[4] or (bkgd is not None and ctx.needs_input_grad[3])
+        n_rays = R
+        desc = _desc(cfg, n_rays if not points else R // n_samples, n_samples, train, bkgd is not None, points)
+        ws = torch.empty(render_workspace_bytes(desc), dtype=torch.uint8, device=rays_o.device)
+        out_rgb = torch.empty(R, rd, dtype=torch.float32, device=rays_o.device)
+        out_op = torch.empty(R, dtype=torch.float32, device=rays_o.device)
+        out_dp = torch.empty(R, dtype=torch.float32, device=rays_o.device)
+        io = RenderIO(_ptr(rays_o), _ptr(rays_d), _ptr(jitter), _ptr(packed.fwd), _ptr(packed.bwd),
+                      _ptr(packed.bias), _ptr(bkgd), _ptr(ws), _ptr(out_rgb), _ptr(out_op), _ptr(out_dp))
+        _check(lib().den_render_fwd(ctypes.byref(desc), ctypes.byref(io), _stream(rays_o.device)))
+        ctx.desc, ctx.io_keep = desc, (rays_o, rays_d, jitter, bkgd, ws, packed)
+        ctx.flat_shape = flat.shape
+        ctx.has_bkgd = bkgd is not None
+        return out_rgb, out_op, out_dp
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_op, g_dp):
+        rays_o, rays_d, jitter, bkgd, ws, packed = ctx.io_keep
+        dev = rays_o.device
+        g_rgb = torch.zeros_like(g_rgb) if g_rgb is None else g_rgb.contiguous()
+        g_op = None if g_op is None else g_op.contiguous()
+        g_dp = None if g_dp is None else g_dp.contiguous()
+        grad_flat = torch.empty(ctx.flat_shape, dtype=torch.float32, device=dev)
+        grad_bkgd = torch.empty(bkgd.shape, dtype=torch.float32, device=dev) if ctx.has_bkgd else None
+        io = RenderIO(_ptr(rays_o), _ptr(rays_d), _ptr(jitter), _ptr(packed.fwd), _ptr(packed.bwd),
+                      _ptr(packed.bias), _ptr(bkgd), _ptr(ws), None, None, None)
+        gr = RenderGrad(_ptr(g_rgb), _ptr(g_op), _ptr(g_dp), _ptr(grad_flat), _ptr(grad_bkgd))
+        _check(lib().den_render_bwd(ctypes.byref(ctx.desc), ctypes.byref(io), ctypes.byref(gr), _stream(dev)))
+        return None, None, None, grad_bkgd, grad_flat, None, None, None, None
+
+
+def render(rays_o, rays_d, jitter, bkgd, flat, cfg, packed, n_samples):
+    return RenderFunction.apply(rays_o.contiguous(), rays_d.contiguous(), jitter.contiguous(),
+                                None if bkgd is None else bkgd.contiguous(), flat, cfg, packed, n_samples, False)
+
+
+def field(points, dirs, flat, cfg, packed):
+    """Radiance field at arbitrary points (n,3)/(n,3): -> rgb (n,rd), sigma (n)."""
+    n = points.shape[0]
+    tile = wg_samples(cfg["mode"])
+    pad = (-n) % tile
+    if pad:
+        points = torch.cat([points, points.new_zeros(pad, 3)])
+        dirs = torch.cat([dirs, dirs.new_zeros(pad, 3) + torch.tensor([0.0, 0.0, 1.0], device=dirs.device)])
+    # "rays" of `tile` points each; the jitter buffer is unused in point mode
+    dummy = torch.zeros(points.shape[0], device=points.device)
+    rgb, sig, _ = RenderFunction.apply(points.contiguous(), dirs.contiguous(), dummy, None, flat, cfg, packed,
+                                       tile, True)
+    return rgb[:n], sig[:n]
+
+
+# ----------------------------------------------------------------------------- reductions / adam
+def sum_partials(part, n, nb, out):
+    _check(lib().den_sum_partials(n, nb, _ptr(part), _ptr(out), _stream(part.device)))
+
+
+def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):
+    _require_device(param, grad, exp_avg, exp_avg_sq)
+    _check(lib().den_adam_step(param.numel(), _ptr(param), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), lr, beta1,
+                               beta2, eps, weight_decay, int(step), _stream(param.device)))
+
+
+# ----------------------------------------------------------------------------- event loss
+class EventLossFunction(torch.autograd.Function):
+    """mean_{valid} err(x / c - target)  (loss.py:62-96)."""
+
+    @staticmethod
+    def forward(ctx, x, target, c, valid, error_fn):
+        _require_device(x, target, c, valid)
+        N = x.numel()
+        ws = torch.empty(lib().den_event_loss_workspace_bytes(N) // 4 + 1, dtype=torch.float32, device=x.device)
+        out = torch.empty((), dtype=torch.float32, device=x.device)
+        v = None if valid is None else valid.to(torch.uint8).contiguous()
+        _check(lib().den_event_loss_fwd(N, ERROR_FNS[error_fn], _ptr(x), _ptr(target), _ptr(v), _ptr(c), _ptr(out),
+                                        _ptr(ws), _stream(x.device)))
+        ctx.save_for_backward(x, target, c)
+        ctx.v, ctx.ws, ctx.fn = v, ws, error_fn
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, target, c = ctx.saved_tensors
+        N = x.numel()
+        dx = torch.empty_like(x)
+        dt = torch.empty_like(x) if target is not None and ctx.needs_input_grad[1] else None
+        dc = torch.empty((), dtype=torch.float32, device=x.device)
+        g = g.contiguous().to(torch.float32)
+        _check(lib().den_event_loss_bwd(N, ERROR_FNS[ctx.fn], _ptr(x), _ptr(target), _ptr(ctx.v), _ptr(c), _ptr(g),
+                                        _ptr(dx), _ptr(dt), _ptr(dc), _ptr(ctx.ws), _stream(x.device)))
+        return dx, dt, dc.reshape(c.shape), None, None
+
+
+def event_target(ts_diff, lid, end_ts, start_ts, c):
+    _require_device(ts_diff, lid, end_ts, start_ts, c)
+    N = lid.numel()
+    out = torch.empty(N, dtype=torch.float32, device=lid.device)
+    _check(lib().den_event_target(N, _ptr(ts_diff.double().contiguous()), _ptr(lid.float().contiguous()),
+                                  _ptr(end_ts.long().contiguous()), _ptr(start_ts.double().contiguous()),
+                                  _ptr(c.float().reshape(1).contiguous()), _ptr(out), _stream(lid.device)))
+    return out

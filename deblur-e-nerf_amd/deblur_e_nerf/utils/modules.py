@@ -1,0 +1,47 @@
+"""Parametrisations used by the model components (reference utils/modules.py:58-94).
+
+Scalar parameter transforms stay in PyTorch (host glue on a handful of
+scalars); they are applied through torch.nn.utils.parametrize exactly as the
+reference does, so parameter names (``parametrizations.<name>.original``) and
+checkpoints match.
+"""
+import torch
+
+
+class Softplus(torch.nn.Module):
+    def __init__(self, beta=1, threshold=20):
+        super().__init__()
+        self.beta = beta
+        self.threshold = threshold
+
+    def forward(self, x):
+        return torch.nn.functional.softplus(x, self.beta, self.threshold)
+
+    def right_inverse(self, y):
+        # inverse softplus, linear above the threshold
+        return torch.where(y * self.beta > self.threshold, y, torch.log(torch.expm1(self.beta * y)) / self.beta)
+
+
+class ScaledShiftedSigmoid(torch.nn.Module):
+    """scale * sigmoid(x / scale) + low; keeps sigmoid's gradient profile."""
+
+    def __init__(self, low=0, high=1):
+        super().__init__()
+        self.low = low
+        self.scale = high - low
+
+    def forward(self, x):
+        return self.scale * torch.sigmoid(x / self.scale) + self.low
+
+    def right_inverse(self, y):
+        return self.scale * torch.logit((y - self.low) / self.scale)
+
+
+def freeze(module):
+    for p in module.parameters():
+        p.requires_grad_(False)
+
+
+def unfreeze(module):
+    for p in module.parameters():
+        p.requires_grad_(True)

@@ -1,0 +1,208 @@
+/*
+ * den_api.h -- C ABI of libden.so, the MI355X-native (gfx950) hot path of
+ * Deblur e-NeRF: fused stratified sampling + positional encoding + 8x256 NeRF
+ * MLP (MFMA) + alpha compositing, its backward, the pixel-bandwidth sensor
+ * model and the event loss.
+ *
+ * Plain C: pointers, sizes and an opaque stream handle (hipStream_t passed as
+ * void*).  No torch types.  Every device pointer is caller-owned device memory
+ * (the PyTorch caching allocator on the Python side); the library allocates
+ * nothing and keeps no state except a thread-local last-error string.
+ * All calls are stream-ordered and capturable into a hipGraph.
+ *
+ * Return value of every int function: 0 on success, otherwise a DEN_E* code;
+ * den_last_error() gives text.  Nothing in the library aborts or exits.
+ *
+ * The reference interface each entry point replaces (paths relative to the
+ * reference repo wengflow/deblur-e-nerf @ 2024-10-22):
+ *   den_render_fwd   <- deblur_e_nerf/models/nerf.py:230-286 NeRF.forward ->
+ *                       external/utils.py:38-140 render_image (nerfacc
+ *                       ray_marching + rendering) -> external/mlp.py:350-358
+ *                       VanillaNeRFRadianceField.forward ->
+ *                       external/vol_rendering.py:16-128 rendering
+ *   den_render_bwd   <- torch autograd through the same chain (nerfacc's
+ *                       custom transmittance backward + nn.Linear backward)
+ *   den_dw_reduce /  <- the weight-gradient half of nn.Linear backward
+ *   den_dw_gemm         (cuBLAS split-K in the reference)
+ *   den_pack_weights <- (no reference counterpart: MFMA fragment layout)
+ *   den_pixbw_*      <- deblur_e_nerf/models/pixel_bandwidth.py:298-494
+ *                       PixelBandwidth.sample_intensity / forward and
+ *                       utils/control.py:29-123 foh_cont2discrete
+ *   den_event_loss_* <- deblur_e_nerf/loss_metric/loss.py:34-96 Loss.compute
+ *   den_event_target
+ *   den_adam_step    <- torch.optim.Adam as configured by
+ *                       deblur_e_nerf/models/deblur_e_nerf.py:1055-1112
+ */
+#ifndef DEN_API_H
+#define DEN_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DEN_VERSION 1
+
+enum den_status {
+  DEN_OK = 0,
+  DEN_EINVAL = 1,      /* bad argument / null pointer / inconsistent sizes */
+  DEN_EUNSUPPORTED = 2,/* shape or configuration outside what the kernels implement */
+  DEN_EHIP = 3         /* a HIP runtime call failed */
+};
+
+/* Arithmetic mode of the fused MLP. */
+enum den_mode {
+  DEN_MODE_F32 = 0,  /* parity mode: f32 operands, f32 MFMA (16x16x4), exact f32 FMA chains */
+  DEN_MODE_BF16 = 1  /* perf mode: bf16 operands, f32 accumulate (32x32x16 MFMA) */
+};
+
+/* Radiance-field / renderer configuration.  The MLP shape is the reference's
+ * `mlp` arch (configs/train/synthetic.yaml:104-114): depth 8, width 256, skip
+ * after layer 4, condition depth 1 width 128, pos-enc degree 10, view-enc
+ * degree 4, softplus(beta=100) hidden activation, shifted_trunc_exp density,
+ * softplus radiance.  radiance_dim in {1, 3}. */
+typedef struct den_render_desc {
+  int32_t mode;            /* den_mode */
+  int32_t radiance_dim;    /* 1 or 3 */
+  int32_t n_rays;          /* rays in this call */
+  int32_t n_samples;       /* samples per ray, fixed count; must divide the
+                              workgroup tile (128 samples in F32 mode, 256 in BF16) */
+  float aabb[6];           /* min xyz, max xyz (nerf.py:212, AABB contraction) */
+  float near_plane;        /* < 0 => none */
+  float far_plane;         /* < 0 => none */
+  int32_t train;           /* 1: keep activations in the workspace for den_render_bwd */
+  int32_t has_bkgd;        /* 1: composite over bkgd (render_bkgd, nerf.py:219-230) */
+  int32_t points;          /* 1: evaluate the radiance field at given points instead of
+                              rendering rays (VanillaNeRFRadianceField.forward, mlp.py:350-358):
+                              rays_o/rays_d = per-point positions/directions (n,3),
+                              n = n_rays*n_samples; out_rgb = rgb (n,rd), out_opacity =
+                              sigma (n); in den_render_bwd d_rgb/d_opacity are dL/drgb,
+                              dL/dsigma per point. */
+} den_render_desc;
+
+/* Device buffers of one render call. */
+typedef struct den_render_io {
+  const float* rays_o;     /* (R,3) */
+  const float* rays_d;     /* (R,3) unit directions */
+  const float* jitter;     /* (R)   stratified offset u in [0,1) */
+  const void* w_fwd;       /* packed forward fragments   (den_pack_weights) */
+  const void* w_bwd;       /* packed transposed fragments (den_pack_weights) */
+  const float* bias_pk;    /* packed biases               (den_pack_weights) */
+  const float* bkgd;       /* (rd) post-activation background, or NULL */
+  void* workspace;         /* den_render_workspace_bytes() bytes */
+  float* out_rgb;          /* (R,rd) composited radiance */
+  float* out_opacity;      /* (R) */
+  float* out_depth;        /* (R) sum_i w_i t_mid_i (not yet divided by opacity) */
+} den_render_io;
+
+/* Upstream gradients / outputs of den_render_bwd. */
+typedef struct den_render_grad {
+  const float* d_rgb;      /* (R,rd) dL/d out_rgb */
+  const float* d_opacity;  /* (R) or NULL */
+  const float* d_depth;    /* (R) or NULL */
+  float* grad_params;      /* flat f32 gradient buffer, reference state-dict order
+                              of nerf.radiance_field.mlp.* (den_param_count) --
+                              OVERWRITTEN (not accumulated) */
+  float* grad_bkgd;        /* (rd) dL/d bkgd (post-activation), or NULL -- overwritten */
+} den_render_grad;
+
+int den_version(void);
+const char* den_last_error(void);
+
+/* Number of f32 parameters of the MLP (595,844 for rd=3) and the offset of the
+ * tensor `idx` in the flat buffer, in the reference's named_parameters() order:
+ * base.hidden_layers.{0..7}.{weight,bias}, sigma_layer.output_layer.{w,b},
+ * bottleneck_layer.output_layer.{w,b}, rgb_layer.hidden_layers.0.{w,b},
+ * rgb_layer.output_layer.{w,b}  (24 tensors). */
+int64_t den_param_count(int32_t radiance_dim);
+int64_t den_param_offset(int32_t radiance_dim, int32_t idx);
+
+/* Sizes of the packed weight buffers for a mode. */
+size_t den_packed_fwd_bytes(int32_t mode);
+size_t den_packed_bwd_bytes(int32_t mode);
+size_t den_packed_bias_bytes(int32_t mode);
+
+/* flat f32 params (den_param_count) -> MFMA fragment layouts. */
+int den_pack_weights(int32_t mode, int32_t radiance_dim, const float* params,
+                     void* w_fwd, void* w_bwd, float* bias_pk, void* stream);
+
+size_t den_render_workspace_bytes(const den_render_desc* desc);
+
+int den_render_fwd(const den_render_desc* desc, const den_render_io* io, void* stream);
+
+/* Requires the workspace of a preceding den_render_fwd with train=1 and the
+ * same desc/io.  Writes grad_params (overwrite) and grad_bkgd. */
+int den_render_bwd(const den_render_desc* desc, const den_render_io* io,
+                   const den_render_grad* grad, void* stream);
+
+/* ---------------------------------------------------------------- pixel bandwidth
+ * Per-event pixel-bandwidth model (pixel_bandwidth.py).  Parameters are the
+ * post-softplus values (the module's parametrised attributes) in this order:
+ *   [0] tau_in_it_eff_prod (buffer) [1] tau_mil_it_eff_prod [2] A_amp_inv
+ *   [3] A_loop_inv [4] tau_out [5] tau_sf [6] tau_diff                        */
+#define DEN_PIXBW_NPARAM 7
+
+/* sample_ts (S,N) f64 from gen (S-1,N) f64 and output_ts (N) f64
+ * (pixel_bandwidth.py:311-360; un-clamped). */
+int den_pixbw_sample_ts(int32_t S, int32_t N, const double* gen, const double* output_ts,
+                        double omega_c_min, double max_cumprob, double* sample_ts, void* stream);
+
+/* Forward.  intensity (S,N) f32, sample_ts (S,N) f64.  reset != 0: writes
+ * delta_out (N) and returns out = sf log-intensity; otherwise reads delta_in
+ * (N) and reset_ts (N) f64 and applies the decay.  weights_out (S,N,o) f32
+ * optional (may be NULL). */
+int den_pixbw_fwd(int32_t S, int32_t N, int32_t reset, const float* intensity,
+                  const double* sample_ts, const double* output_ts, const float* params,
+                  const float* delta_in, const double* reset_ts, float* out,
+                  float* delta_out, void* stream);
+
+/* Backward.  d_out (N), d_delta_out (N, reset only, may be NULL) ->
+ * d_intensity (S,N) (overwrite), d_delta_in (N, non-reset only; overwrite),
+ * d_params_partial (DEN_PIXBW_NPARAM x n_blocks f32 partial sums; the caller
+ * sums them with den_sum_partials).  n_blocks = den_pixbw_blocks(N). */
+int den_pixbw_blocks(int32_t N);
+int den_pixbw_bwd(int32_t S, int32_t N, int32_t reset, const float* intensity,
+                  const double* sample_ts, const double* output_ts, const float* params,
+                  const float* delta_in, const double* reset_ts, const float* d_out,
+                  const float* d_delta_out, float* d_intensity, float* d_delta_in,
+                  float* d_params_partial, void* stream);
+
+/* ---------------------------------------------------------------- event loss
+ * One term of Loss.compute (loss.py:62-96) over N events:
+ *   err_i = f(x_i / c - t_i),  L = mean_{i valid} err_i
+ * x = rendered log-intensity difference (f32), c = normalising constant (the
+ * mean contrast threshold, or 1), t = normalised target (NULL => 0, the TV
+ * term).  error_fn: 0 = l1, 1 = mse, 2 = huber(delta = 1).  valid: u8 mask or
+ * NULL (all valid).  No valid event => L = NaN (torch's empty mean).
+ * workspace: den_event_loss_workspace_bytes(N), shared by fwd and bwd (bwd
+ * reads the valid count left by fwd). */
+size_t den_event_loss_workspace_bytes(int32_t N);
+int den_event_loss_fwd(int32_t N, int32_t error_fn, const float* x, const float* target, const uint8_t* valid,
+                       const float* norm_c, float* loss, void* workspace, void* stream);
+/* g_loss = dTotal/dL (device scalar).  Writes d_x (N), d_target (N, may be NULL)
+ * and d_c (1) = dTotal/dc through the x/c input (target's c-dependence is the
+ * caller's chain rule through d_target). */
+int den_event_loss_bwd(int32_t N, int32_t error_fn, const float* x, const float* target, const uint8_t* valid,
+                       const float* norm_c, const float* g_loss, float* d_x, float* d_target, float* d_c,
+                       void* workspace, void* stream);
+/* Normalised diff-term target (loss.py:74-77), f64 arithmetic rounded to f32:
+ *   t_i = f32( ts_diff_i * (lid_i / (end_ts_i - start_ts_i)) / c ) */
+int den_event_target(int32_t N, const double* ts_diff, const float* lid, const int64_t* end_ts,
+                     const double* start_ts, const float* norm_c, float* target, void* stream);
+
+/* ---------------------------------------------------------------- reductions / optimizer */
+/* out[j] = sum_b partial[j*n_blocks + b] for j < n (deterministic order). */
+int den_sum_partials(int32_t n, int32_t n_blocks, const float* partial, float* out, void* stream);
+
+/* torch.optim.Adam (amsgrad=False, L2 weight decay added to the gradient) on a
+ * flat f32 buffer; per-element lr / weight decay via group ids. */
+int den_adam_step(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                  float lr, float beta1, float beta2, float eps, float weight_decay,
+                  int64_t step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DEN_API_H */
