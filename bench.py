@@ -1,0 +1,203 @@
+"""Train-step throughput of the Deblur e-NeRF render + event-measurement hot path.
+
+Workload (BASELINE.json configs[1]): chair-like synthetic scene, 2^17 rays x 128
+samples per step through the 8x256 `mlp` NeRF, pixel-bandwidth model off, rays
+= 4 render groups (diff start/end, TV start/end) x 32768 events, Huber diff +
+1e-3 L1 TV loss, backward, all-reduce, Adam.  Strong scaling: the 2^17-ray step
+is split over the ranks (reference DDP semantics: per-GPU batch = eff // gpus).
+
+    python bench.py [--gpus N --steps K --warmup W]     (N > 1 via torch.distributed.run)
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline
+accounting.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "deblur-e-nerf_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# algorithmic MACs per sample of the forward MLP: 593,152 (rd=1) / 593,408 (rd=3)
+MAC_PER_SAMPLE = {1: 593152, 3: 593408}
+PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rays", type=int, default=131072)
+    ap.add_argument("--samples", type=int, default=128)
+    ap.add_argument("--rd", type=int, default=1)
+    ap.add_argument("--mode", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rays", type=int, default=2048, help="rays of the bounded CPU-baseline sample")
+    return ap.parse_args()
+
+
+def phase_times(ts, reps=3):
+    """Average duration of each phase, measured with HIP events on the stream
+    the kernels are launched on (torch's current stream)."""
+    import ctypes
+    from deblur_e_nerf import _native as nat
+    L = nat.lib()
+    st = nat._stream(ts.dev)
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    acc = {"render_fwd": 0.0, "bwd_chain": 0.0, "bwd_dw": 0.0, "other": 0.0}
+    for _ in range(reps):
+        e = [ev() for _ in range(6)]
+        e[0].record()
+        ts.bkgd = torch.nn.functional.softplus(ts.bkgd_orig)
+        ts.io.bkgd = nat._ptr(ts.bkgd)
+        nat._check(L.den_render_fwd(ctypes.byref(ts.desc), ctypes.byref(ts.io), st))
+        e[1].record()
+        args = (ts.N, ts.rd, 2, 0, int(ts.has_bkgd), ts.min_int, ts.wl[0], ts.wl[1], nat._ptr(ts.rgb),
+                nat._ptr(ts.opacity), nat._ptr(ts.channel), nat._ptr(ts.target), nat._ptr(ts.c), nat._ptr(ts.ev_ws))
+        nat._check(L.den_event_step_fwd(*args, nat._ptr(ts.loss), st))
+        nat._check(L.den_event_step_bwd(*args, nat._ptr(ts.d_rgb), st))
+        e[2].record()
+        gr = nat.RenderGrad(nat._ptr(ts.d_rgb), None, None, nat._ptr(ts.grad), nat._ptr(ts.grad_bkgd))
+        nat._check(L.den_render_bwd_part(ctypes.byref(ts.desc), ctypes.byref(ts.io), ctypes.byref(gr), 1, st))
+        e[3].record()
+        nat._check(L.den_render_bwd_part(ctypes.byref(ts.desc), ctypes.byref(ts.io), ctypes.byref(gr), 2, st))
+        e[4].record()
+        ts.allreduce()
+        ts.optimizer_step()
+        e[5].record()
+        torch.cuda.synchronize()
+        acc["render_fwd"] += e[0].elapsed_time(e[1])
+        acc["other"] += e[1].elapsed_time(e[2]) + e[4].elapsed_time(e[5])
+        acc["bwd_chain"] += e[2].elapsed_time(e[3])
+        acc["bwd_dw"] += e[3].elapsed_time(e[4])
+    return {k: v / reps for k, v in acc.items()}
+
+
+def cpu_baseline(n_rays, n_samples, rd, threads):
+    """The oracle (PyTorch-CPU restatement of the reference path) timed on a
+    bounded sample: n_rays rays through render fwd + event loss + backward +
+    Adam (the same step as the GPU line, fewer rays)."""
+    from oracle import loss as oloss
+    from oracle import nerf as onerf
+    from deblur_e_nerf.train import synthetic_batch
+    torch.set_num_threads(threads)
+    N = n_rays // 4
+    b = synthetic_batch(N, seed=99)
+    p = onerf.build_params(rd, 0)
+    params = list(p.values())
+    for t in params:
+        t.requires_grad_(True)
+    bk = torch.tensor([0.5413] * rd, requires_grad=True)
+    opt = torch.optim.Adam([{"params": params, "weight_decay": 1e-6}, {"params": [bk]}], lr=0.01)
+    c = torch.tensor(0.25)
+
+    def step():
+        opt.zero_grad()
+        bkgd = torch.nn.functional.softplus(bk)
+        col, op, _, _ = onerf.render_rays(p, b["rays_o"], b["rays_d"], b["jitter"], n_samples=n_samples, bkgd=bkgd)
+        y = torch.log(col[:, 0] + 1e-3).view(4, N)
+        Ld, Lt = oloss.event_loss(b["lid"], b["end_ts"], b["start_ts"], y[1] - y[0], b["ts_diff"],
+                                  torch.ones(N, dtype=torch.bool), y[3] - y[2], torch.ones(N, dtype=torch.bool), c)
+        (Ld + 1e-3 * Lt).backward()
+        opt.step()
+
+    step()  # warm-up
+    t0 = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        step()
+    dt = (time.perf_counter() - t0) / reps
+    return dict(value=round(n_rays / dt, 2), unit="rays/s", cores=threads, kind="port",
+                sample=f"oracle (PyTorch CPU) train step on {n_rays} rays x {n_samples} samples "
+                       f"(render fwd + event loss + backward + Adam), {reps} timed reps after 1 warm-up, "
+                       f"{dt:.2f} s/step")
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    from deblur_e_nerf.train import TrainStep, synthetic_batch
+
+    assert a.rays % (4 * world) == 0
+    n_events = a.rays // 4 // world
+    ts = TrainStep(n_events, n_samples=a.samples, radiance_dim=a.rd, mode=a.mode, device=dev)
+    ts.load_batch(**synthetic_batch(n_events, rank=rank, world=world, device="cpu"))
+    for _ in range(a.warmup):
+        ts.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ts.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    loss = ts.loss[:3].tolist()
+    ms = elapsed / a.steps * 1e3
+    rays_per_step = a.rays
+    value = rays_per_step * a.steps / elapsed
+
+    phases = phase_times(ts)
+    n_local = ts.R * ts.S
+    flop_fwd = 2.0 * MAC_PER_SAMPLE[a.rd] * n_local
+    fwd_ms = phases["render_fwd"]
+    achieved = flop_fwd / (fwd_ms * 1e-3) / 1e12
+    step_flop = 3.0 * flop_fwd
+    roofline = {"bound": "mfma", "kernel": "render_fwd_kernel (fused sampler+encoding+MLP fwd+compositing)",
+                "achieved": round(achieved, 2), "peak": PEAK_TFLOPS[a.mode], "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_TFLOPS[a.mode], 4), "traffic": None,
+                "flop_per_launch": flop_fwd, "kernel_ms": round(fwd_ms, 3),
+                # whole train step (fwd + 2x bwd algorithmic FLOPs of this rank) vs the peak of one GPU
+                "step_frac": round(step_flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.mode], 4),
+                "phases_ms": {k: round(v, 3) for k, v in phases.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            threads = min(16, len(os.sched_getaffinity(0)))
+            cpu = cpu_baseline(a.cpu_rays, a.samples, a.rd, threads)
+        except Exception as e:  # pragma: no cover - reported, not fatal
+            cpu = {"error": repr(e)}
+    if rank == 0:
+        out = {
+            "metric": "train-step rays/sec at 131072 rays x 128 samples",
+            "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": a.mode, "data": "synthetic (chair-like rays/events, PyTorch default-init weights)",
+            "config": {"workload": f"chair synthetic, pixel-bandwidth off, {a.rays} rays x {a.samples} samples, "
+                                   f"mlp 8x256 rd={a.rd}, fwd+bwd+allreduce+Adam",
+                       "rays_per_step": a.rays, "samples_per_ray": a.samples, "events_per_step": a.rays // 4,
+                       "parallelism": f"ray-dp{world}"},
+            "loss": [round(x, 6) for x in loss],
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -154,7 +154,8 @@ int render_fwd_impl(const den_render_desc* d, const den_render_io* io, hipStream
 }
 
 template <int MODE>
-int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den_render_grad* g, hipStream_t s) {
+int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den_render_grad* g, hipStream_t s,
+                    int parts) {
   WsLayout L = ws_layout(d);
   RenderArgs<MODE> A = make_args<MODE>(d, io, L);
   A.w = (const char*)io->w_bwd;
@@ -162,8 +163,11 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
   A.d_opacity = g->d_opacity;
   A.d_depth = g->d_depth;
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
-  hipLaunchKernelGGL(render_bwd_kernel<MODE>, dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s, A);
-  DEN_LAUNCHED();
+  if (parts & 1) {
+    hipLaunchKernelGGL(render_bwd_kernel<MODE>, dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s, A);
+    DEN_LAUNCHED();
+  }
+  if (!(parts & 2)) return DEN_OK;
   char* ws = (char*)io->workspace;
   float* G = g->grad_params;
   int rc;
@@ -243,8 +247,19 @@ int den_render_bwd(const den_render_desc* d, const den_render_io* io, const den_
     return fail(DEN_EINVAL, "null pointer in den_render_io");
   if (!g || !g->d_rgb || !g->grad_params) return fail(DEN_EINVAL, "null pointer in den_render_grad");
   if (d->has_bkgd && !io->bkgd) return fail(DEN_EINVAL, "has_bkgd but bkgd == NULL");
-  return d->mode == 0 ? render_bwd_impl<0>(d, io, g, (hipStream_t)stream)
-                      : render_bwd_impl<1>(d, io, g, (hipStream_t)stream);
+  return d->mode == 0 ? render_bwd_impl<0>(d, io, g, (hipStream_t)stream, 3)
+                      : render_bwd_impl<1>(d, io, g, (hipStream_t)stream, 3);
+}
+
+int den_render_bwd_part(const den_render_desc* d, const den_render_io* io, const den_render_grad* g, int32_t part,
+                        void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (part != 1 && part != 2) return fail(DEN_EINVAL, "part must be 1 (dz chain) or 2 (weight gradients)");
+  if (!d->train || !io || !io->workspace || !io->w_bwd || !g || !g->d_rgb || !g->grad_params)
+    return fail(DEN_EINVAL, "null pointer / train=0");
+  return d->mode == 0 ? render_bwd_impl<0>(d, io, g, (hipStream_t)stream, part)
+                      : render_bwd_impl<1>(d, io, g, (hipStream_t)stream, part);
 }
 
 int den_sum_partials(int32_t n, int32_t nb, const float* part, float* out, void* stream) {
@@ -309,6 +324,51 @@ int den_event_target(int32_t N, const double* ts_diff, const float* lid, const i
   if (N <= 0 || !ts_diff || !lid || !end_ts || !start_ts || !c || !target) return fail(DEN_EINVAL, "bad arguments");
   hipLaunchKernelGGL(event_target_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, N, ts_diff, lid,
                      end_ts, start_ts, c, target);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+size_t den_event_step_workspace_bytes(int32_t N) {
+  const int nb = (N + LOSS_BLOCK - 1) / LOSS_BLOCK;
+  return (size_t)(4 * nb + 8) * 4;
+}
+
+static EventStepArgs make_event_args(int32_t N, int32_t rd, int32_t fn_d, int32_t fn_t, int32_t has_bkgd,
+                                     float min_int, float w_d, float w_t, const float* radiance, const float* opacity,
+                                     const int64_t* channel, const float* target, const float* c, void* ws,
+                                     float* out, float* d_radiance) {
+  EventStepArgs E{};
+  E.N = N; E.rd = rd; E.fn_d = fn_d; E.fn_t = fn_t; E.has_bkgd = has_bkgd;
+  E.min_int = min_int; E.w_d = w_d; E.w_t = w_t;
+  E.radiance = radiance; E.opacity = opacity; E.channel = channel; E.target = target; E.c = c;
+  E.part = (float*)ws; E.out = out; E.d_radiance = d_radiance;
+  return E;
+}
+
+int den_event_step_fwd(int32_t N, int32_t rd, int32_t fn_d, int32_t fn_t, int32_t has_bkgd, float min_int, float w_d,
+                       float w_t, const float* radiance, const float* opacity, const int64_t* channel,
+                       const float* target, const float* c, void* ws, float* out, void* stream) {
+  if (N <= 0 || (rd != 1 && rd != 3) || fn_d < 0 || fn_d > 2 || fn_t < 0 || fn_t > 2 || !radiance || !target || !c ||
+      !ws || !out || (!has_bkgd && !opacity) || (rd > 1 && !channel))
+    return fail(DEN_EINVAL, "bad arguments");
+  EventStepArgs E = make_event_args(N, rd, fn_d, fn_t, has_bkgd, min_int, w_d, w_t, radiance, opacity, channel,
+                                    target, c, ws, out, nullptr);
+  const int nb = (N + LOSS_BLOCK - 1) / LOSS_BLOCK;
+  hipLaunchKernelGGL(event_step_partial_kernel, dim3(nb), dim3(LOSS_BLOCK), 0, (hipStream_t)stream, E);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(event_step_final_kernel, dim3(1), dim3(LOSS_BLOCK), 0, (hipStream_t)stream, E, nb);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_event_step_bwd(int32_t N, int32_t rd, int32_t fn_d, int32_t fn_t, int32_t has_bkgd, float min_int, float w_d,
+                       float w_t, const float* radiance, const float* opacity, const int64_t* channel,
+                       const float* target, const float* c, void* ws, float* d_radiance, void* stream) {
+  if (N <= 0 || !radiance || !target || !c || !ws || !d_radiance || (!has_bkgd && !opacity) || (rd > 1 && !channel))
+    return fail(DEN_EINVAL, "bad arguments");
+  EventStepArgs E = make_event_args(N, rd, fn_d, fn_t, has_bkgd, min_int, w_d, w_t, radiance, opacity, channel,
+                                    target, c, ws, nullptr, d_radiance);
+  hipLaunchKernelGGL(event_step_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, E);
   DEN_LAUNCHED();
   return DEN_OK;
 }

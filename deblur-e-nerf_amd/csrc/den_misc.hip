@@ -228,3 +228,113 @@ __global__ void event_target_kernel(int N, const double* ts_diff, const float* l
 }
 
 }  // namespace den
+
+namespace den {
+// ------------------------------------------------------------------ fused event step (pixel bandwidth off)
+// The measurement path of DeblurENeRF.training_step (deblur_e_nerf.py:472-549)
+// for pixel_bandwidth.enable = false, fused over the 4 render groups
+// [diff start, diff end, tv start, tv end] x N events:
+//   I = radiance(+bayer channel) + min_int ; y = log I (deblur_e_nerf.py:1153-1157, 1203)
+//   L_diff = mean_valid f_d((y1 - y0)/c - t) ; L_tv = mean_valid f_t((y3 - y2)/c)   (loss.py:62-96)
+//   valid = is_valid(start) | is_valid(end), is_valid = opacity > 0 unless has_bkgd (1204-1207)
+// total = w_d L_diff + w_t L_tv.
+struct EventStepArgs {
+  int N, rd, fn_d, fn_t, has_bkgd;
+  float min_int, w_d, w_t;
+  const float* radiance;   // [4][N][rd]
+  const float* opacity;    // [4][N]
+  const int64_t* channel;  // [N] or null
+  const float* target;     // [N] normalised diff target
+  const float* c;          // [1]
+  float* part;             // [4][nb] partial sums: err_d, cnt_d, err_t, cnt_t
+  float* out;              // [4]: L_diff, L_tv, total, (scratch)
+  float* d_radiance;       // [4][N][rd]
+};
+
+__device__ __forceinline__ float ev_logI(const EventStepArgs& E, int g, int i) {
+  const int ch = (E.rd > 1 && E.channel) ? (int)E.channel[i] : 0;
+  return logf(E.radiance[((int64_t)g * E.N + i) * E.rd + ch] + E.min_int);
+}
+__device__ __forceinline__ bool ev_valid(const EventStepArgs& E, int g0, int i) {
+  if (E.has_bkgd) return true;
+  return E.opacity[(int64_t)g0 * E.N + i] > 0.0f || E.opacity[(int64_t)(g0 + 1) * E.N + i] > 0.0f;
+}
+
+__global__ void event_step_partial_kernel(EventStepArgs E) {
+  __shared__ float s[4][LOSS_BLOCK];
+  const int i = blockIdx.x * LOSS_BLOCK + threadIdx.x;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (i < E.N) {
+    const float c = E.c[0];
+    if (ev_valid(E, 0, i)) {
+      float x = ev_logI(E, 1, i) - ev_logI(E, 0, i);
+      v[0] = err_fn(E.fn_d, x / c - E.target[i]);
+      v[1] = 1.0f;
+    }
+    if (ev_valid(E, 2, i)) {
+      float x = ev_logI(E, 3, i) - ev_logI(E, 2, i);
+      v[2] = err_fn(E.fn_t, x / c);
+      v[3] = 1.0f;
+    }
+  }
+  for (int q = 0; q < 4; ++q) s[q][threadIdx.x] = v[q];
+  __syncthreads();
+  for (int w = LOSS_BLOCK / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+      for (int q = 0; q < 4; ++q) s[q][threadIdx.x] += s[q][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    for (int q = 0; q < 4; ++q) E.part[q * gridDim.x + blockIdx.x] = s[q][0];
+}
+
+__global__ void event_step_final_kernel(EventStepArgs E, int nb) {
+  __shared__ float s[4][LOSS_BLOCK];
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b = threadIdx.x; b < nb; b += LOSS_BLOCK)
+    for (int q = 0; q < 4; ++q) v[q] += E.part[q * nb + b];
+  for (int q = 0; q < 4; ++q) s[q][threadIdx.x] = v[q];
+  __syncthreads();
+  for (int w = LOSS_BLOCK / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+      for (int q = 0; q < 4; ++q) s[q][threadIdx.x] += s[q][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float Ld = s[0][0] / s[1][0], Lt = s[2][0] / s[3][0];
+    E.out[0] = Ld;
+    E.out[1] = Lt;
+    E.out[2] = E.w_d * Ld + E.w_t * Lt;
+    E.out[3] = 0.0f;
+    E.part[0] = s[1][0];  // keep the valid counts for the backward
+    E.part[1] = s[3][0];
+  }
+}
+
+// d total / d radiance for the 4 groups (zeros on the channels not selected)
+__global__ void event_step_bwd_kernel(EventStepArgs E) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E.N) return;
+  const float c = E.c[0];
+  const float cnt_d = E.part[0], cnt_t = E.part[1];
+  const int ch = (E.rd > 1 && E.channel) ? (int)E.channel[i] : 0;
+  float dy[4] = {0.f, 0.f, 0.f, 0.f};
+  if (ev_valid(E, 0, i)) {
+    float x = ev_logI(E, 1, i) - ev_logI(E, 0, i);
+    float g = derr_fn(E.fn_d, x / c - E.target[i]) * (E.w_d / cnt_d) / c;
+    dy[1] = g;
+    dy[0] = -g;
+  }
+  if (ev_valid(E, 2, i)) {
+    float x = ev_logI(E, 3, i) - ev_logI(E, 2, i);
+    float g = derr_fn(E.fn_t, x / c) * (E.w_t / cnt_t) / c;
+    dy[3] = g;
+    dy[2] = -g;
+  }
+  for (int g = 0; g < 4; ++g) {
+    const int64_t base = ((int64_t)g * E.N + i) * E.rd;
+    const float I = E.radiance[base + ch] + E.min_int;
+    for (int k = 0; k < E.rd; ++k) E.d_radiance[base + k] = (k == ch) ? dy[g] / I : 0.0f;
+  }
+}
+}  // namespace den

@@ -54,6 +54,8 @@ _SIGS = {
     "den_render_fwd": (ctypes.c_int, [ctypes.POINTER(RenderDesc), ctypes.POINTER(RenderIO), ctypes.c_void_p]),
     "den_render_bwd": (ctypes.c_int, [ctypes.POINTER(RenderDesc), ctypes.POINTER(RenderIO),
                                       ctypes.POINTER(RenderGrad), ctypes.c_void_p]),
+    "den_render_bwd_part": (ctypes.c_int, [ctypes.POINTER(RenderDesc), ctypes.POINTER(RenderIO),
+                                           ctypes.POINTER(RenderGrad), ctypes.c_int32, ctypes.c_void_p]),
     "den_sum_partials": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]),
     "den_adam_step": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_float] * 5
@@ -62,6 +64,9 @@ _SIGS = {
     "den_event_loss_fwd": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 7),
     "den_event_loss_bwd": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 10),
     "den_event_target": (ctypes.c_int, [ctypes.c_int32] + [ctypes.c_void_p] * 7),
+    "den_event_step_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "den_event_step_fwd": (ctypes.c_int, [ctypes.c_int32] * 5 + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 8),
+    "den_event_step_bwd": (ctypes.c_int, [ctypes.c_int32] * 5 + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 8),
     "den_pixbw_sample_ts": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]),
     "den_pixbw_fwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 10),

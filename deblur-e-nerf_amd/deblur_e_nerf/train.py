@@ -1,0 +1,157 @@
+"""Native training step of the render + event-measurement hot path.
+
+``TrainStep`` is one ``DeblurENeRF.training_step`` + DDP gradient all-reduce +
+``Adam.step`` (deblur_e_nerf.py:396-586, 1055-1112; scripts/run.py:84-100)
+for the synthetic configuration of BASELINE.json (chair, pixel-bandwidth model
+off, mlp arch), with every array operation in libden.so:
+
+  den_event_target -> den_render_fwd (4 render groups x N events in ONE launch)
+  -> den_event_step_fwd/bwd (log-intensity, Huber diff + L1 TV losses and their
+  gradient) -> den_render_bwd (compositing adjoint, MLP backward, split-K weight
+  gradients) -> RCCL all-reduce of one flat f32 gradient buffer (ranks > 1)
+  -> den_adam_step (L2 weight decay 1e-6 on the MLP) -> den_pack_weights.
+
+The only PyTorch arithmetic is the softplus parametrisation of the rd-element
+render background (a scalar parameter transform, as utils/modules.py keeps).
+"""
+import ctypes
+import math
+
+import torch
+import torch.distributed as dist
+
+from . import _native as nat
+from .external import mlp, ngp
+
+ERR = nat.ERROR_FNS
+
+
+class TrainStep:
+    def __init__(self, n_events, n_samples=128, radiance_dim=1, mode="bf16", seed=0, device="cuda",
+                 aabb=(-1.5, -1.5, -1.5, 1.5, 1.5, 1.5), near=1.43, far=6.63, lr=0.01, weight_decay=1e-6,
+                 loss_weight=(1.0, 1e-3), error_fn=("huber", "l1"), min_modeled_intensity=1e-3,
+                 mean_contrast_threshold=0.25, alpha_over_white_bg=True):
+        self.N, self.S, self.rd, self.mode = n_events, n_samples, radiance_dim, nat.mode_id(mode)
+        self.dev = torch.device(device)
+        self.R = 4 * n_events
+        torch.manual_seed(seed)
+        field = mlp.VanillaNeRFRadianceField(
+            list(aabb), radiance_dim=radiance_dim, hidden_activation=torch.nn.Softplus(beta=100),
+            density_activation=ngp.shifted_trunc_exp, radiance_activation=torch.nn.Softplus(beta=1),
+            mode=mode)
+        self.P = nat.param_count(radiance_dim)
+        self.flat = field.flat_params.detach().to(self.dev).contiguous()
+        assert self.flat.numel() == self.P
+        # one flat gradient buffer [MLP params | render bkgd] -> one collective per step
+        self.gbuf = torch.zeros(self.P + radiance_dim, device=self.dev)
+        self.grad = self.gbuf[: self.P]
+        self.grad_bkgd = self.gbuf[self.P:]
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
+        self.has_bkgd = bool(alpha_over_white_bg)
+        # nerf.py:219-228: Parameter(ones(rd)) under a softplus parametrisation
+        self.bkgd_orig = torch.full((radiance_dim,), math.log(math.expm1(1.0)), device=self.dev)
+        self.bm = torch.zeros_like(self.bkgd_orig)
+        self.bv = torch.zeros_like(self.bkgd_orig)
+        self.t = 0
+        self.lr, self.wd = lr, weight_decay
+        self.wl, self.fn = loss_weight, error_fn
+        self.min_int = min_modeled_intensity
+        self.c = torch.tensor([mean_contrast_threshold], device=self.dev)
+        self.cfg = dict(mode=self.mode, rd=radiance_dim, aabb=list(aabb), near=near, far=far)
+        self.packed = nat.PackedWeights(self.mode, radiance_dim, self.dev)
+        self.packed.pack(self.flat)
+        self.desc = nat._desc(self.cfg, self.R, n_samples, True, self.has_bkgd)
+        self.ws = torch.empty(nat.render_workspace_bytes(self.desc), dtype=torch.uint8, device=self.dev)
+        self.rgb = torch.empty(self.R, radiance_dim, device=self.dev)
+        self.opacity = torch.empty(self.R, device=self.dev)
+        self.depth = torch.empty(self.R, device=self.dev)
+        self.d_rgb = torch.empty_like(self.rgb)
+        self.ev_ws = torch.empty(nat.lib().den_event_step_workspace_bytes(n_events) // 4 + 1, device=self.dev)
+        self.loss = torch.zeros(4, device=self.dev)
+        self.target = torch.empty(n_events, device=self.dev)
+
+    # ---------------------------------------------------------------- batch
+    def load_batch(self, rays_o, rays_d, jitter, lid, end_ts, start_ts, ts_diff, channel=None):
+        """rays_* : (4N, 3) for groups [diff start, diff end, tv start, tv end];
+        lid (N) f32 measured log-intensity change; end_ts (N) i64; start_ts, ts_diff (N) f64."""
+        d = self.dev
+        self.rays_o = rays_o.to(d, torch.float32).contiguous()
+        self.rays_d = rays_d.to(d, torch.float32).contiguous()
+        self.jitter = jitter.to(d, torch.float32).contiguous()
+        self.lid = lid.to(d, torch.float32).contiguous()
+        self.end_ts = end_ts.to(d, torch.int64).contiguous()
+        self.start_ts = start_ts.to(d, torch.float64).contiguous()
+        self.ts_diff = ts_diff.to(d, torch.float64).contiguous()
+        self.channel = None if channel is None else channel.to(d, torch.int64).contiguous()
+
+    # ---------------------------------------------------------------- phases
+    def forward(self):
+        L, st = nat.lib(), nat._stream(self.dev)
+        self.bkgd = torch.nn.functional.softplus(self.bkgd_orig) if self.has_bkgd else None
+        nat._check(L.den_event_target(self.N, nat._ptr(self.ts_diff), nat._ptr(self.lid), nat._ptr(self.end_ts),
+                                      nat._ptr(self.start_ts), nat._ptr(self.c), nat._ptr(self.target), st))
+        self.io = nat.RenderIO(nat._ptr(self.rays_o), nat._ptr(self.rays_d), nat._ptr(self.jitter),
+                               nat._ptr(self.packed.fwd), nat._ptr(self.packed.bwd), nat._ptr(self.packed.bias),
+                               nat._ptr(self.bkgd), nat._ptr(self.ws), nat._ptr(self.rgb), nat._ptr(self.opacity),
+                               nat._ptr(self.depth))
+        nat._check(L.den_render_fwd(ctypes.byref(self.desc), ctypes.byref(self.io), st))
+        args = (self.N, self.rd, ERR[self.fn[0]], ERR[self.fn[1]], int(self.has_bkgd), self.min_int, self.wl[0],
+                self.wl[1], nat._ptr(self.rgb), nat._ptr(self.opacity), nat._ptr(self.channel),
+                nat._ptr(self.target), nat._ptr(self.c), nat._ptr(self.ev_ws))
+        nat._check(L.den_event_step_fwd(*args, nat._ptr(self.loss), st))
+        nat._check(L.den_event_step_bwd(*args, nat._ptr(self.d_rgb), st))
+
+    def backward(self):
+        st = nat._stream(self.dev)
+        gr = nat.RenderGrad(nat._ptr(self.d_rgb), None, None, nat._ptr(self.grad),
+                            nat._ptr(self.grad_bkgd) if self.has_bkgd else None)
+        nat._check(nat.lib().den_render_bwd(ctypes.byref(self.desc), ctypes.byref(self.io), ctypes.byref(gr), st))
+
+    def allreduce(self):
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(self.gbuf, op=dist.ReduceOp.SUM)
+            self.gbuf.div_(dist.get_world_size())
+
+    def optimizer_step(self):
+        self.t += 1
+        nat.adam_step(self.flat, self.grad, self.m, self.v, self.lr, 0.9, 0.999, 1e-8, self.wd, self.t)
+        if self.has_bkgd:
+            g_orig = self.grad_bkgd * torch.sigmoid(self.bkgd_orig)  # softplus(beta=1) parametrisation chain rule
+            nat.adam_step(self.bkgd_orig, g_orig.contiguous(), self.bm, self.bv, self.lr, 0.9, 0.999, 1e-8, 0.0,
+                          self.t)
+        self.packed.pack(self.flat)
+
+    def step(self):
+        self.forward()
+        self.backward()
+        self.allreduce()
+        self.optimizer_step()
+        return self.loss
+
+
+def synthetic_batch(n_events, seed=1234, radius=4.03, device="cpu", rank=0, world=1):
+    """Synthetic chair-like event batch.  Each event is one
+    pixel seen from a camera on a sphere around the AABB; its four render
+    timestamps (diff start/end, tv start/end) move the camera slightly.
+    Returns the (4N,3) rays, jitter and the event fields; rank r of `world`
+    gets the r-th contiguous shard of the events."""
+    g = torch.Generator().manual_seed(seed)
+    N = n_events * world
+    v = torch.randn(N, 3, generator=g)
+    c0 = v / v.norm(dim=-1, keepdim=True) * radius
+    look = -c0 / c0.norm(dim=-1, keepdim=True) + (torch.rand(N, 3, generator=g) * 2 - 1) * math.sin(0.3)
+    look = look / look.norm(dim=-1, keepdim=True)
+    motion = torch.randn(4, N, 3, generator=g) * 0.01  # camera motion across the 4 timestamps
+    o = (c0[None] + motion).reshape(4 * N, 3)
+    d = look[None].expand(4, N, 3).reshape(4 * N, 3)
+    jitter = torch.rand(4 * N, generator=g)
+    pos = torch.rand(N, generator=g) < 0.5
+    lid = torch.where(pos, 0.25, -0.25).float()
+    end_ts = (torch.rand(N, generator=g, dtype=torch.float64) * 9e8 + 1e8).floor().long()
+    start_ts = end_ts.double() - (-torch.log(torch.rand(N, generator=g, dtype=torch.float64)) * 1e6 + 1e3)
+    ts_diff = end_ts.double() - start_ts
+    sl = slice(rank * n_events, (rank + 1) * n_events)
+    o4, d4, j4 = (t.reshape(4, N, *t.shape[1:])[:, sl].reshape(4 * n_events, *t.shape[1:]) for t in (o, d, jitter))
+    return dict(rays_o=o4.to(device), rays_d=d4.to(device), jitter=j4.to(device), lid=lid[sl].to(device),
+                end_ts=end_ts[sl].to(device), start_ts=start_ts[sl].to(device), ts_diff=ts_diff[sl].to(device))

@@ -136,6 +136,11 @@ int den_render_fwd(const den_render_desc* desc, const den_render_io* io, void* s
  * same desc/io.  Writes grad_params (overwrite) and grad_bkgd. */
 int den_render_bwd(const den_render_desc* desc, const den_render_io* io,
                    const den_render_grad* grad, void* stream);
+/* den_render_bwd in two stream-ordered halves (for profiling / overlap):
+ * part 1 = compositing adjoint + MLP dz chain (one kernel), part 2 = weight /
+ * bias / background gradients from the dz written by part 1. */
+int den_render_bwd_part(const den_render_desc* desc, const den_render_io* io,
+                        const den_render_grad* grad, int32_t part, void* stream);
 
 /* ---------------------------------------------------------------- pixel bandwidth
  * Per-event pixel-bandwidth model (pixel_bandwidth.py).  Parameters are the
@@ -191,6 +196,23 @@ int den_event_loss_bwd(int32_t N, int32_t error_fn, const float* x, const float*
  *   t_i = f32( ts_diff_i * (lid_i / (end_ts_i - start_ts_i)) / c ) */
 int den_event_target(int32_t N, const double* ts_diff, const float* lid, const int64_t* end_ts,
                      const double* start_ts, const float* norm_c, float* target, void* stream);
+
+/* Fused measurement step for pixel_bandwidth.enable = false
+ * (DeblurENeRF.training_step, deblur_e_nerf.py:472-549): radiance of the 4
+ * render groups [diff start, diff end, tv start, tv end] x N events (rd
+ * channels, bayer channel per event when rd = 3) -> I = radiance + min_int,
+ * y = log I, L_diff = mean_valid f_d((y1-y0)/c - target),
+ * L_tv = mean_valid f_t((y3-y2)/c), total = w_d L_diff + w_t L_tv.
+ * valid = opacity > 0 at start or end unless has_bkgd (deblur_e_nerf.py:1204-1207).
+ * out[0..2] = L_diff, L_tv, total.  The bwd writes d total / d radiance
+ * (4,N,rd) and must follow the fwd on the same workspace. */
+size_t den_event_step_workspace_bytes(int32_t N);
+int den_event_step_fwd(int32_t N, int32_t rd, int32_t fn_d, int32_t fn_t, int32_t has_bkgd, float min_int,
+                       float w_d, float w_t, const float* radiance, const float* opacity, const int64_t* channel,
+                       const float* target, const float* norm_c, void* workspace, float* out, void* stream);
+int den_event_step_bwd(int32_t N, int32_t rd, int32_t fn_d, int32_t fn_t, int32_t has_bkgd, float min_int,
+                       float w_d, float w_t, const float* radiance, const float* opacity, const int64_t* channel,
+                       const float* target, const float* norm_c, void* workspace, float* d_radiance, void* stream);
 
 /* ---------------------------------------------------------------- reductions / optimizer */
 /* out[j] = sum_b partial[j*n_blocks + b] for j < n (deterministic order). */
