@@ -65,6 +65,19 @@ __device__ __forceinline__ typename Tr<MODE>::Acc acc_zero() {
   return a;
 }
 
+// Store a lane's operand fragments of one tile (stored order: regs 0..REGS-1).
+template <int MODE>
+__device__ __forceinline__ void store_tile_frags(void* row_base_bytes, const typename Tr<MODE>::Frag* f) {
+  if constexpr (MODE == 1) {
+    bf16x8* p = (bf16x8*)row_base_bytes;
+    p[0] = f[0];
+    p[1] = f[1];
+  } else {
+    f32x4 v = {f[0], f[1], f[2], f[3]};
+    *(f32x4*)row_base_bytes = v;
+  }
+}
+
 // Store a lane's REGS accumulator values (stored order) as operand dtype.
 template <int MODE>
 __device__ __forceinline__ void store_tile_vals(void* row_base_bytes, const typename Tr<MODE>::Acc& a) {
@@ -116,6 +129,25 @@ __device__ __forceinline__ float dsoftplus_b100_from_out(float s) {
   if constexpr (EXACT) return -expm1f(-100.0f * s);
   else return 1.0f - __expf(-100.0f * s);
 }
+// BF16 path, base-2 scaled units (den_geom.h KAPPA): s' = max(t,0) + log2(1 + 2^-|t|)
+// (for t > 20*log2(e) the log term is 0 in f32: torch's threshold branch).
+__device__ __forceinline__ float softplus2_scaled(float t) {
+  return fmaxf(t, 0.0f) + __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(-fabsf(t)));
+}
+// its derivative from the output: sigmoid(100 z) = 1 - 2^-s'
+__device__ __forceinline__ float dsoftplus2_scaled_from_out(float s) { return 1.0f - __builtin_amdgcn_exp2f(-s); }
+
+template <int MODE>
+__device__ __forceinline__ float hidden_act(float z) {
+  if constexpr (MODE == 0) return softplus_b100<true>(z);
+  else return softplus2_scaled(z);
+}
+template <int MODE>
+__device__ __forceinline__ float hidden_dact(float s) {
+  if constexpr (MODE == 0) return dsoftplus_b100_from_out<true>(s);
+  else return dsoftplus2_scaled_from_out(s);
+}
+
 __device__ __forceinline__ float softplus_b1(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
 
 // ------------------------------------------------------------------ exact f32 sampler math
@@ -217,30 +249,23 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // ------------------------------------------------------------------ weight chunk staging
-// A chunk (one packed TM-row tile of a layer, <= 20 KiB) is copied global ->
-// registers (issued before the MFMA block of the current chunk) -> LDS
-// (written after it), double-buffered, one barrier per chunk.
+// A chunk (one packed TM-row tile of a layer, <= 20 KiB, a multiple of 1 KiB)
+// is copied global -> LDS by LDS-DMA (global_load_lds_dwordx4: each wave moves
+// 1 KiB per instruction, lane-linear), issued before the MFMA block of the
+// current chunk into the other slot of a 2-slot ring; the barrier that ends
+// the chunk also drains the DMA (vmcnt(0)), one barrier per chunk.
 constexpr int WG_THREADS = 512;
 constexpr int CHUNK_MAX = 64 * 320;  // 20 KiB
-constexpr int STAGE_ROUNDS = (CHUNK_MAX + WG_THREADS * 16 - 1) / (WG_THREADS * 16);
 
-struct Stage {
-  uint4 v[STAGE_ROUNDS];
-};
-__device__ __forceinline__ void stage_load(Stage& st, const char* g, int bytes) {
-  const int t = threadIdx.x;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void dma_chunk(const char* g, char* lds_slot, int bytes) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int q = 0; q < STAGE_ROUNDS; ++q) {
-    int off = q * WG_THREADS * 16 + t * 16;
-    if (off < bytes) st.v[q] = *(const uint4*)(g + off);
-  }
-}
-__device__ __forceinline__ void stage_store(const Stage& st, char* lds, int bytes) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < STAGE_ROUNDS; ++q) {
-    int off = q * WG_THREADS * 16 + t * 16;
-    if (off < bytes) *(uint4*)(lds + off) = st.v[q];
+  for (int q = 0; q < (CHUNK_MAX + WG_THREADS * 16 - 1) / (WG_THREADS * 16); ++q) {
+    const int off = q * WG_THREADS * 16 + wave * 1024;  // wave-uniform
+    if (off < bytes)
+      __builtin_amdgcn_global_load_lds((const void*)(g + off + lane * 16), (lds_ptr_t)(lds_slot + off), 16, 0, 0);
   }
 }
 

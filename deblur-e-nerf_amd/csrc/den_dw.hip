@@ -197,7 +197,7 @@ __global__ void dw_reduce_kernel(DwReduceArgs R) {
   if (nt == R.NT) {  // ones tile -> bias gradient (column 0 only)
     if (col != 0) return;
     if (!ref_bias_coord(R.layer, o, R.rd, &t, &rr)) return;
-    R.grad[param_offset(R.rd, 2 * t + 1) + rr] = s;
+    R.grad[param_offset(R.rd, 2 * t + 1) + rr] = R.mode == 0 ? s : (float)((double)s * bias_scale(R.mode, R.layer));
     return;
   }
   const int n = 32 * nt + col;
@@ -208,7 +208,8 @@ __global__ void dw_reduce_kernel(DwReduceArgs R) {
     f = R.n1_feat + (n2 / TMc) * TMc + stored_to_row(R.mode, n2 % TMc);
   }
   if (!ref_coord(R.layer, o, f, R.rd, &t, &rr, &cc)) return;
-  R.grad[param_offset(R.rd, 2 * t) + (int64_t)rr * ref_in(t) + cc] = s;
+  R.grad[param_offset(R.rd, 2 * t) + (int64_t)rr * ref_in(t) + cc] =
+      R.mode == 0 ? s : (float)((double)s * col_scale(R.mode, R.layer, f));
 }
 
 template __global__ void dw_gemm_kernel<1, 8, 64, 0>(DwArgs);

@@ -162,6 +162,26 @@ DEN_HD bool ref_bias_coord(int l, int o, int rd, int* t, int* row) {
   return ref_coord(l, o, 0, rd, t, row, &dummy_col);
 }
 
+// ---------------------------------------------------------------- BF16 activation scaling
+// In BF16 mode softplus(beta=100) is evaluated in base 2 on t = K*z with
+// K = 100*log2(e):  s' = log2(1 + 2^t) = K * softplus_100(z).  K is folded into
+// the packed weights/biases (W' = col_scale * W, b' = bias_scale * b), so the
+// epilogue is v_exp + v_log + 3 VALU.  Activations kept for the backward are
+// in these scaled units; the weight-gradient reduction multiplies by the same
+// factors (dL/dW = col_scale * dL/dW').  F32 mode uses scale 1 (exact path).
+constexpr double KAPPA = 144.26950408889634;  // 100 / ln 2
+DEN_HD double col_scale(int mode, int l, int f) {
+  if (mode == 0) return 1.0;
+  if (l == 0) return KAPPA;                       // pe input
+  if (l < 8) return (l == 5 && f >= WIDTH) ? KAPPA : 1.0;
+  if (l == L_B || l == L_R) return 1.0 / KAPPA;   // consume K-scaled activations, identity / softplus(1) out
+  return KAPPA;                                   // L_G: [bottleneck, ve] raw inputs, softplus(100) out
+}
+DEN_HD double bias_scale(int mode, int l) {
+  if (mode == 0) return 1.0;
+  return (l == L_B || l == L_R) ? 1.0 : KAPPA;
+}
+
 // ---------------------------------------------------------------- workspace (render)
 // Activation tensors kept for the backward, each [n_samples][width] in the
 // operand dtype, stored order within tiles.

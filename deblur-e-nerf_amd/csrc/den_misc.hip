@@ -21,7 +21,8 @@ struct PackArgs {
 __device__ __forceinline__ float param_w(const PackArgs& P, int l, int o, int f) {
   int t, r, c;
   if (!ref_coord(l, o, f, P.rd, &t, &r, &c)) return 0.0f;
-  return P.params[param_offset(P.rd, 2 * t) + (int64_t)r * ref_in(t) + c];
+  const float w = P.params[param_offset(P.rd, 2 * t) + (int64_t)r * ref_in(t) + c];
+  return P.mode == 0 ? w : (float)((double)w * col_scale(P.mode, l, f));
 }
 
 __device__ __forceinline__ void decode_elem(int mode, int64_t e, int* kappa, int* lane, int* j) {
@@ -81,7 +82,9 @@ __global__ void pack_kernel(PackArgs P) {
     const int i = chunk - fwd_chunk_index(mode, l);
     const int o = TM * i + stored_to_row(mode, q);
     int t, r;
-    P.bias[e] = ref_bias_coord(l, o, P.rd, &t, &r) ? P.params[param_offset(P.rd, 2 * t + 1) + r] : 0.0f;
+    P.bias[e] = ref_bias_coord(l, o, P.rd, &t, &r)
+                    ? (float)((double)P.params[param_offset(P.rd, 2 * t + 1) + r] * bias_scale(mode, l))
+                    : 0.0f;
   }
 }
 

@@ -62,10 +62,8 @@ __device__ __forceinline__ char* act_ptr(const RenderArgs<MODE>& A, int a, int64
 template <typename Body>
 __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, int64_t next_off, int next_bytes,
                                            Body&& body) {
-  Stage st;
-  if (next_bytes > 0) stage_load(st, wbase + next_off, next_bytes);
+  if (next_bytes > 0) dma_chunk(wbase + next_off, lds + ((t + 1) & 1) * LDS_BUF, next_bytes);
   body(lds + (t & 1) * LDS_BUF);
-  if (next_bytes > 0) stage_store(st, lds + ((t + 1) & 1) * LDS_BUF, next_bytes);
   __syncthreads();
 }
 
@@ -89,16 +87,40 @@ __device__ __forceinline__ void bwd_next(int j, int i, int64_t* off, int* bytes)
 
 // ------------------------------------------------------------------ forward layer
 // Runs all row tiles of forward layer L with input fragments x1[0..KS1) ++ x2[0..KS2).
-// EPI: 0 = hidden softplus(100) -> xo (+store act OUTA), 1 = bottleneck/sigma, 2 = rgb.
+// EPI: 0 = hidden softplus(100) -> xo (+store act outA), 1 = bottleneck/sigma, 2 = rgb.
+// Software pipeline: the VALU epilogue of tile i-1 is issued in the same
+// basic block as the MFMA chain of tile i, so the two interleave.
+template <int MODE, int L, int EPI, typename Frag, typename Acc>
+__device__ __forceinline__ void fwd_epilogue(const RenderArgs<MODE>& A, int64_t sample, Acc& acc, int i, Frag* xo,
+                                             int outA, Acc* special) {
+  using T = Tr<MODE>;
+  constexpr int TM = T::TM, FPT = T::FPT;
+  if constexpr (EPI == 0) {
+#pragma unroll
+    for (int r = 0; r < T::REGS; ++r) acc[r] = hidden_act<MODE>(acc[r]);
+    acc_to_frags<MODE>(acc, xo + i * FPT);
+    if (A.train) store_tile_frags<MODE>(act_ptr(A, outA, sample, i), xo + i * FPT);
+  } else if constexpr (EPI == 1) {
+    if (i < WIDTH / TM) {
+      acc_to_frags<MODE>(acc, xo + i * FPT);
+      if (A.train) store_tile_frags<MODE>(act_ptr(A, A_BT, sample, i), xo + i * FPT);
+    } else if (i == WIDTH / TM) {
+      *special = acc;  // row 0 = sigma_raw (lane group 0, reg 0)
+    }
+  } else {
+    *special = acc;  // rows 0..rd-1 = rgb_raw (lane group 0, regs 0..rd-1)
+  }
+}
+
 template <int MODE, int L, int KS1, int KS2, int EPI, typename Frag, typename Acc>
 __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, int64_t sample, const Frag* x1,
                                           const Frag* x2, Frag* xo, int outA, Acc* special) {
   using T = Tr<MODE>;
-  constexpr int TM = T::TM, FPT = T::FPT;
+  constexpr int TM = T::TM;
   constexpr int NT = fwd_tiles(MODE, L);
-  constexpr bool EXACT = MODE == 0;
   constexpr int CB = fwd_chunk_index(MODE, L);
   const int lane = threadIdx.x & 63, grp = lane / TM;
+  Acc prev;
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     int64_t noff;
@@ -106,28 +128,16 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
     fwd_next<MODE>(L, i, &noff, &nbytes);
     chunk_step(lds, A.w, CB + i, noff, nbytes, [&](const char* chunk) {
       Acc acc;
-      const float* bias = A.bias + (int64_t)(CB + i) * TM + grp * T::REGS;
+      const float* bias = (const float*)(lds + 2 * LDS_BUF) + (CB + i) * TM + grp * T::REGS;
 #pragma unroll
       for (int r = 0; r < T::REGS; ++r) acc[r] = bias[r];
       mfma_chunk<MODE, KS1>(chunk, x1, acc);
       if constexpr (KS2 > 0) mfma_chunk<MODE, KS2>(chunk + KS1 * TM * T::KI * es_of(MODE), x2, acc);
-      if constexpr (EPI == 0) {
-#pragma unroll
-        for (int r = 0; r < T::REGS; ++r) acc[r] = softplus_b100<EXACT>(acc[r]);
-        if (A.train) store_tile_vals<MODE>(act_ptr(A, outA, sample, i), acc);
-        acc_to_frags<MODE>(acc, xo + i * FPT);
-      } else if constexpr (EPI == 1) {
-        if (i < WIDTH / TM) {
-          if (A.train) store_tile_vals<MODE>(act_ptr(A, A_BT, sample, i), acc);
-          acc_to_frags<MODE>(acc, xo + i * FPT);
-        } else if (i == WIDTH / TM) {
-          *special = acc;  // row 0 = sigma_raw (lane group 0, reg 0)
-        }
-      } else {
-        *special = acc;  // rows 0..rd-1 = rgb_raw (lane group 0, regs 0..rd-1)
-      }
+      if (i > 0) fwd_epilogue<MODE, L, EPI>(A, sample, prev, i - 1, xo, outA, special);
+      prev = acc;
     });
   }
+  fwd_epilogue<MODE, L, EPI>(A, sample, prev, NT - 1, xo, outA, special);
 }
 
 // ------------------------------------------------------------------ forward kernel
@@ -139,8 +149,10 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
   constexpr int TM = T::TM, FPT = T::FPT, REGS = T::REGS;
   constexpr bool EXACT = MODE == 0;
   constexpr int WGS = wg_samples(MODE);
-  __shared__ __attribute__((aligned(16))) char lds[2 * LDS_BUF + WGS * 16];
-  float* rec_lds = (float*)(lds + 2 * LDS_BUF);
+  constexpr int NBIAS = (int)bias_floats(MODE);
+  __shared__ __attribute__((aligned(16))) char lds[2 * LDS_BUF + NBIAS * 4 + WGS * 16];
+  float* bias_lds = (float*)(lds + 2 * LDS_BUF);
+  float* rec_lds = bias_lds + NBIAS;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane % TM, grp = lane / TM;
@@ -148,12 +160,9 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
   const int64_t ray = sample / A.n_samples;
   const int k = (int)(sample - ray * A.n_samples);
 
-  // prologue: chunk 0 -> slot 0
-  {
-    Stage st;
-    stage_load(st, A.w, chunk_bytes_K(fwd_K(MODE, 0)));
-    stage_store(st, lds, chunk_bytes_K(fwd_K(MODE, 0)));
-  }
+  // prologue: whole bias table -> LDS, chunk 0 -> slot 0
+  for (int q = threadIdx.x; q < NBIAS; q += WG_THREADS) bias_lds[q] = A.bias[q];
+  dma_chunk(A.w, lds, chunk_bytes_K(fwd_K(MODE, 0)));
 
   float o[3], d[3], xc[3], sel;
   if (A.points) {
@@ -234,7 +243,9 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
     if (A.train) *(f32x4*)(A.rec + sample * 4) = v;
     if (A.points) {
       A.out_opacity[sample] = sigma;
-      for (int ch = 0; ch < A.rd; ++ch) A.out_rgb[sample * A.rd + ch] = v[1 + ch];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+        if (ch < A.rd) A.out_rgb[sample * A.rd + ch] = v[1 + ch];
     }
   }
   if (A.points) return;
@@ -292,7 +303,9 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) cs[ch] = wave_sum(cs[ch]);
     if (lane == 0) {
-      for (int ch = 0; ch < A.rd; ++ch) {
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        if (ch >= A.rd) break;
         float v = cs[ch];
         if (A.has_bkgd) v = v + A.bkgd[ch] * (1.0f - op);
         A.out_rgb[r * A.rd + ch] = v;
@@ -308,6 +321,8 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
 // layer's chain inputs; epilogue multiplies by the activation derivative read
 // from the stored forward activation (act index SA) and stores dz (index DZ).
 // DER: 0 = softplus(100) derivative from stored output, 1 = identity.
+// The stored activation of tile i is loaded before tile i's MFMA chain and
+// consumed by its epilogue one tile later (software pipeline, as forward).
 template <int MODE, int J, int KS, int DER, typename Frag>
 __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* lds, int64_t sample, const Frag* x,
                                               Frag* xo, int SA, int DZ) {
@@ -315,26 +330,32 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
   using Acc = typename T::Acc;
   constexpr int NT = bwd_tiles(MODE, J);
   constexpr int FPT = T::FPT;
-  constexpr bool EXACT = MODE == 0;
   int cb = 0;
   for (int jj = 0; jj < J; ++jj) cb += bwd_tiles(MODE, jj);
+  Acc prev, s_prev, s_cur;
+  auto epilogue = [&](Acc& acc, const Acc& sv, int i) {
+    if constexpr (DER == 0) {
+#pragma unroll
+      for (int r = 0; r < T::REGS; ++r) acc[r] = acc[r] * hidden_dact<MODE>(sv[r]);
+    }
+    acc_to_frags<MODE>(acc, xo + i * FPT);
+    store_tile_frags<MODE>(act_ptr(A, DZ, sample, i), xo + i * FPT);
+  };
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     int64_t noff;
     int nbytes;
     bwd_next<MODE>(J, i, &noff, &nbytes);
+    if constexpr (DER == 0) s_cur = load_tile_vals<MODE>(act_ptr(A, SA, sample, i));
     chunk_step(lds, A.w, cb + i, noff, nbytes, [&](const char* chunk) {
       Acc acc = acc_zero<MODE>();
       mfma_chunk<MODE, KS>(chunk, x, acc);
-      if constexpr (DER == 0) {
-        Acc s = load_tile_vals<MODE>(act_ptr(A, SA, sample, i));
-#pragma unroll
-        for (int r = 0; r < T::REGS; ++r) acc[r] = acc[r] * dsoftplus_b100_from_out<EXACT>(s[r]);
-      }
-      store_tile_vals<MODE>(act_ptr(A, DZ, sample, i), acc);
-      acc_to_frags<MODE>(acc, xo + i * FPT);
+      if (i > 0) epilogue(prev, s_prev, i - 1);
+      prev = acc;
     });
+    s_prev = s_cur;
   }
+  epilogue(prev, s_prev, NT - 1);
 }
 
 template <int MODE>
@@ -351,11 +372,7 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
   const int c = lane % TM, grp = lane / TM;
   const int64_t sample = (int64_t)blockIdx.x * WGS + wave * TM + c;
 
-  {
-    Stage st;
-    stage_load(st, A.w, chunk_bytes_K(bwd_K(MODE, 0)));
-    stage_store(st, lds, chunk_bytes_K(bwd_K(MODE, 0)));
-  }
+  dma_chunk(A.w, lds, chunk_bytes_K(bwd_K(MODE, 0)));
 
   // ---- compositing adjoint, one wave per ray
   const int rays_per_wg = WGS / A.n_samples;
@@ -365,7 +382,9 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
       f32x4 rv = *(const f32x4*)(A.rec + sample * 4);
       float dsig = A.d_opacity ? A.d_opacity[sample] : 0.0f;
       float g3[3] = {0.f, 0.f, 0.f};
-      for (int ch = 0; ch < A.rd; ++ch) g3[ch] = A.d_rgb[sample * A.rd + ch];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+        if (ch < A.rd) g3[ch] = A.d_rgb[sample * A.rd + ch];
       f32x4 o4 = {dsig * fminf(rv[0], 3269017.5f), g3[0] * (-expm1f(-rv[1])), g3[1] * (-expm1f(-rv[2])),
                   g3[2] * (-expm1f(-rv[3]))};
       *(f32x4*)(rec_lds + (wave * TM + c) * 4) = o4;
@@ -382,12 +401,16 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
     const float ru = A.jitter[r];
     const int spl = A.n_samples / 64;
     float dC[3] = {0.f, 0.f, 0.f};
-    for (int ch = 0; ch < A.rd; ++ch) dC[ch] = A.d_rgb[r * A.rd + ch];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+      if (ch < A.rd) dC[ch] = A.d_rgb[r * A.rd + ch];
     float dO = A.d_opacity ? A.d_opacity[r] : 0.0f;
     const float dD = A.d_depth ? A.d_depth[r] : 0.0f;
     float bk_dot = 0.0f;
     if (A.has_bkgd)
-      for (int ch = 0; ch < A.rd; ++ch) bk_dot += dC[ch] * A.bkgd[ch];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+        if (ch < A.rd) bk_dot += dC[ch] * A.bkgd[ch];
     float tau[4], tmid[4], dlt[4], loc[4], sg4[4], rc4[4][3];
     float run = 0.0f;
     
