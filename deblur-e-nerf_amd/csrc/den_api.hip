@@ -111,12 +111,16 @@ RenderArgs<MODE> make_args(const den_render_desc* d, const den_render_io* io, co
   return A;
 }
 
+// Split-K weight-gradient GEMM of one layer + its reduction into the flat gradient.
+// red_n1 < 0: columns [0, N1) are the first input segment; red_n1 = 0 maps every column to the
+// second segment at chain feature n1_feat (the pe columns of L5).  bias = 0 skips the bias.
 template <int MODE, int MT, int N1, int N2>
 int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, int a_dz, int a_x1, int a_x2,
-              int n1_feat, float* grad, hipStream_t s, int m_off = 0) {
+              int n1_feat, float* grad, hipStream_t s, int m_off = 0, int red_n1 = -1, int bias = 1) {
   DwArgs P{};
-  P.A = ws + L.act[a_dz] + (size_t)m_off * es_of(MODE);
-  P.lda = act_width(MODE, a_dz);
+  P.A = ws + L.act[a_dz];
+  P.a_tiles = act_width(MODE, a_dz) / tm_of(MODE);
+  P.a_t0 = m_off / tm_of(MODE);
   P.B1 = ws + L.act[a_x1];
   P.B2 = a_x2 >= 0 ? ws + L.act[a_x2] : nullptr;
   P.n = (int64_t)d->n_rays * d->n_samples;
@@ -133,8 +137,9 @@ int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, 
   R.layer = layer;
   R.mode = MODE;
   R.rd = d->radiance_dim;
-  R.n1 = N1;
+  R.n1 = red_n1 < 0 ? N1 : red_n1;
   R.n1_feat = n1_feat;
+  R.bias = bias;
   R.grad = grad;
   const int64_t per = (int64_t)MT * (R.NT + 1) * 1024;
   hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);

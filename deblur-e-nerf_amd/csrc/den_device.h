@@ -65,22 +65,28 @@ __device__ __forceinline__ typename Tr<MODE>::Acc acc_zero() {
   return a;
 }
 
+// Activation tensors in HBM are wave-block major (den_geom.h): the TM x TN tile of one wave is
+// one contiguous block -- [frag f][lane][16 B] in BF16 (2 KiB), [lane][16 B] in F32 (1 KiB) --
+// so every store / load instruction of a wave moves 1 KiB of consecutive bytes.
+// `tile` is the (wave-uniform) base of the tile; each lane adds its own offset.
+
 // Store a lane's operand fragments of one tile (stored order: regs 0..REGS-1).
 template <int MODE>
-__device__ __forceinline__ void store_tile_frags(void* row_base_bytes, const typename Tr<MODE>::Frag* f) {
+__device__ __forceinline__ void store_tile_frags(void* tile, const typename Tr<MODE>::Frag* f) {
+  char* p = (char*)tile + (threadIdx.x & 63) * 16;
   if constexpr (MODE == 1) {
-    bf16x8* p = (bf16x8*)row_base_bytes;
-    p[0] = f[0];
-    p[1] = f[1];
+    *(bf16x8*)p = f[0];
+    *(bf16x8*)(p + 1024) = f[1];
   } else {
     f32x4 v = {f[0], f[1], f[2], f[3]};
-    *(f32x4*)row_base_bytes = v;
+    *(f32x4*)p = v;
   }
 }
 
 // Store a lane's REGS accumulator values (stored order) as operand dtype.
 template <int MODE>
-__device__ __forceinline__ void store_tile_vals(void* row_base_bytes, const typename Tr<MODE>::Acc& a) {
+__device__ __forceinline__ void store_tile_vals(void* tile, const typename Tr<MODE>::Acc& a) {
+  char* p = (char*)tile + (threadIdx.x & 63) * 16;
   if constexpr (MODE == 1) {
     uint32_t w[8];
 #pragma unroll
@@ -88,20 +94,19 @@ __device__ __forceinline__ void store_tile_vals(void* row_base_bytes, const type
       __bf16 lo = (__bf16)a[2 * q], hi = (__bf16)a[2 * q + 1];
       w[q] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
     }
-    uint4* p = (uint4*)row_base_bytes;
-    p[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    p[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+    *(uint4*)(p + 1024) = make_uint4(w[4], w[5], w[6], w[7]);
   } else {
-    *(f32x4*)row_base_bytes = a;
+    *(f32x4*)p = a;
   }
 }
 
 template <int MODE>
-__device__ __forceinline__ typename Tr<MODE>::Acc load_tile_vals(const void* row_base_bytes) {
+__device__ __forceinline__ typename Tr<MODE>::Acc load_tile_vals(const void* tile) {
   typename Tr<MODE>::Acc a;
+  const char* p = (const char*)tile + (threadIdx.x & 63) * 16;
   if constexpr (MODE == 1) {
-    const uint4* p = (const uint4*)row_base_bytes;
-    uint4 u0 = p[0], u1 = p[1];
+    uint4 u0 = *(const uint4*)p, u1 = *(const uint4*)(p + 1024);
     uint32_t w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -109,7 +114,7 @@ __device__ __forceinline__ typename Tr<MODE>::Acc load_tile_vals(const void* row
       a[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
     }
   } else {
-    a = *(const f32x4*)row_base_bytes;
+    a = *(const f32x4*)p;
   }
   return a;
 }

@@ -18,15 +18,39 @@ namespace den {
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 
+// Operands are wave-block-major activation tensors (den_geom.h): [n / TN][tiles][TM x TN tile],
+// BF16 tile = [frag f][lane c + 32h][8] (stored positions 16h + 8f + j), F32 tile = [lane c + 16g][4].
 struct DwArgs {
-  const char* A;       // dz  [n][lda] (stored order; the GEMM uses columns [0, M))
-  int lda;             // row pitch of A in elements
-  const char* B1;      // x   [n][N1]
-  const char* B2;      // x'  [n][N2] (second input segment, may be null when N2 = 0)
+  const char* A;       // dz tensor; the GEMM uses its tiles [a_t0, a_t0 + M / TM)
+  int a_tiles;         // tiles per wave block of the dz tensor
+  int a_t0;
+  const char* B1;      // x  (N1 / TM tiles per wave block)
+  const char* B2;      // x' (N2 / TM tiles, second input segment; null when N2 = 0)
   int64_t n;           // samples
   int64_t per_split;   // samples per split (multiple of 32)
   float* partial;      // [splits][MT][NT+1][64 lanes][16]
 };
+
+// 16-byte unit v (memory order) of the DW_BK-sample chunk starting at sample k0 of a tensor with
+// `tiles` tiles per wave block, restricted to tiles [t0, t0 + nt): source byte offset and the
+// (row = sample in chunk, column = stored feature) it lands at in the row-major LDS image.
+template <int MODE, int DW_BK>
+__device__ __forceinline__ int64_t dw_unit(int v, int nt, int tiles, int t0, int64_t k0, int* row, int* col) {
+  if constexpr (MODE == 1) {
+    const int t = v / (4 * DW_BK), r = v % (4 * DW_BK);
+    const int f = r / (2 * DW_BK), r2 = r % (2 * DW_BK);
+    const int h = r2 / DW_BK, cl = r2 % DW_BK;
+    *row = cl;
+    *col = 32 * t + 16 * h + 8 * f;
+    return ((k0 / 32) * tiles + t0 + t) * 2048 + f * 1024 + ((int)(k0 % 32) + cl + 32 * h) * 16;
+  } else {
+    const int jb = v / (nt * 64), r = v % (nt * 64);
+    const int t = r / 64, ln = r % 64;
+    *row = 16 * jb + (ln & 15);
+    *col = 16 * t + 4 * (ln >> 4);
+    return ((k0 / 16 + jb) * tiles + t0 + t) * 1024 + ln * 16;
+  }
+}
 
 constexpr int DW_BK_MAX = 32;  // samples per LDS stage (16 for register-heavy shapes)
 
@@ -45,8 +69,11 @@ __global__ __launch_bounds__(64 * MT) void dw_gemm_kernel(DwArgs P) {
   constexpr int PA = M * ES + dw_pad_bytes<MODE>(M), PB = N * ES + dw_pad_bytes<MODE>(N);
   constexpr int IMG = DW_BK * (PA + PB);
   constexpr int THREADS = 64 * MT;
-  constexpr int UA = M * ES / 16, UB1 = N1 * ES / 16, UB2 = N2 * ES / 16, UB = UB1 + UB2;  // 16-B units per row
-  constexpr int UNITS = DW_BK * (UA + UB);
+  constexpr int TMm = tm_of(MODE);
+  constexpr int NTA = M / TMm, NT1 = N1 / TMm, NT2 = N2 / TMm;  // tiles per segment
+  // 16-B units of a chunk per segment (4 per sample and tile in both modes), in memory order
+  constexpr int SA = DW_BK * NTA * 4, SB1 = DW_BK * NT1 * 4, SB2 = DW_BK * NT2 * 4;
+  constexpr int UNITS = SA + SB1 + SB2;
   constexpr int UPT = (UNITS + THREADS - 1) / THREADS;
   __shared__ __attribute__((aligned(16))) char lds[2 * IMG];
 
@@ -61,6 +88,22 @@ __global__ __launch_bounds__(64 * MT) void dw_gemm_kernel(DwArgs P) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
 
+  // unit u of a chunk -> global source and LDS destination (consecutive threads read consecutive
+  // 16 B of the wave-block-major tensors; the LDS image stays row-major [sample][stored feature])
+  auto unit = [&](int u, int64_t k0, const char** src, char** dst, char* img) {
+    int row, col;
+    if (u < SA) {
+      *src = P.A + dw_unit<MODE, DW_BK>(u, NTA, P.a_tiles, P.a_t0, k0, &row, &col);
+      *dst = img + row * PA + col * ES;
+    } else if (u < SA + SB1) {
+      *src = P.B1 + dw_unit<MODE, DW_BK>(u - SA, NT1, NT1, 0, k0, &row, &col);
+      *dst = img + DW_BK * PA + row * PB + col * ES;
+    } else {
+      *src = P.B2 + dw_unit<MODE, DW_BK>(u - SA - SB1, NT2, NT2, 0, k0, &row, &col);
+      *dst = img + DW_BK * PA + row * PB + (N1 + col) * ES;
+    }
+    return row;
+  };
   uint4 st[UPT];
   auto load = [&](int ch) {
     const int64_t k0 = k_begin + (int64_t)ch * DW_BK;
@@ -69,15 +112,10 @@ __global__ __launch_bounds__(64 * MT) void dw_gemm_kernel(DwArgs P) {
       int u = q * THREADS + threadIdx.x;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (u < UNITS) {
-        int row = u / (UA + UB), cu = u % (UA + UB);
-        int64_t kr = k0 + row;
-        if (kr < k_end) {
-          const char* src;
-          if (cu < UA) src = P.A + kr * ((int64_t)P.lda * ES) + cu * 16;
-          else if (cu < UA + UB1) src = P.B1 + kr * (N1 * ES) + (cu - UA) * 16;
-          else src = P.B2 + kr * (N2 * ES) + (cu - UA - UB1) * 16;
-          v = *(const uint4*)src;
-        }
+        const char* src;
+        char* dst;
+        const int row = unit(u, k0, &src, &dst, lds);
+        if (k0 + row < k_end) v = *(const uint4*)src;
       }
       st[q] = v;
     }
@@ -88,8 +126,9 @@ __global__ __launch_bounds__(64 * MT) void dw_gemm_kernel(DwArgs P) {
     for (int q = 0; q < UPT; ++q) {
       int u = q * THREADS + threadIdx.x;
       if (u < UNITS) {
-        int row = u / (UA + UB), cu = u % (UA + UB);
-        char* dst = cu < UA ? img + row * PA + cu * 16 : img + DW_BK * PA + row * PB + (cu - UA) * 16;
+        const char* src;
+        char* dst;
+        unit(u, 0, &src, &dst, img);
         *(uint4*)dst = st[q];
       }
     }
@@ -176,6 +215,7 @@ struct DwReduceArgs {
   int rd;
   int n1;          // width of the first input segment (features of x before the second segment)
   int n1_feat;     // chain-feature offset of the second segment (e.g. 256 for [h4, pe])
+  int bias;        // 0: skip the ones tile (the bias gradient is written by another launch)
   float* grad;     // flat params layout
 };
 
@@ -195,7 +235,7 @@ __global__ void dw_reduce_kernel(DwReduceArgs R) {
   const int o = (m / TMc) * TMc + stored_to_row(R.mode, m % TMc);
   int t, rr, cc;
   if (nt == R.NT) {  // ones tile -> bias gradient (column 0 only)
-    if (col != 0) return;
+    if (col != 0 || !R.bias) return;
     if (!ref_bias_coord(R.layer, o, R.rd, &t, &rr)) return;
     R.grad[param_offset(R.rd, 2 * t + 1) + rr] = R.mode == 0 ? s : (float)((double)s * bias_scale(R.mode, R.layer));
     return;

@@ -50,11 +50,13 @@ struct RenderArgs {
 
 // ------------------------------------------------------------------ helpers
 
+// Base of tile `tile` of activation tensor `a` for the wave that owns `sample` (wave-block major
+// layout, den_geom.h); the per-lane offset is added by store_tile_* / load_tile_vals.
 template <int MODE>
 __device__ __forceinline__ char* act_ptr(const RenderArgs<MODE>& A, int a, int64_t sample, int tile) {
-  constexpr int TM = Tr<MODE>::TM, REGS = Tr<MODE>::REGS, ES = es_of(MODE);
-  const int grp = (threadIdx.x & 63) / TM;
-  return A.act[a] + (sample * act_width(MODE, a) + tile * TM + grp * REGS) * ES;
+  constexpr int TM = Tr<MODE>::TM, ES = es_of(MODE);
+  const int64_t wb = __builtin_amdgcn_readfirstlane((int)(sample / TM));  // uniform across the wave
+  return A.act[a] + (wb * (act_width(MODE, a) / TM) + tile) * (int64_t)(TM * TM * ES);
 }
 
 // One chunk step of the pipeline: prefetch chunk (t+1), run `body` on chunk t,
@@ -99,16 +101,30 @@ __device__ __forceinline__ void fwd_epilogue(const RenderArgs<MODE>& A, int64_t 
 #pragma unroll
     for (int r = 0; r < T::REGS; ++r) acc[r] = hidden_act<MODE>(acc[r]);
     acc_to_frags<MODE>(acc, xo + i * FPT);
-    if (A.train) store_tile_frags<MODE>(act_ptr(A, outA, sample, i), xo + i * FPT);
   } else if constexpr (EPI == 1) {
     if (i < WIDTH / TM) {
       acc_to_frags<MODE>(acc, xo + i * FPT);
-      if (A.train) store_tile_frags<MODE>(act_ptr(A, A_BT, sample, i), xo + i * FPT);
     } else if (i == WIDTH / TM) {
       *special = acc;  // row 0 = sigma_raw (lane group 0, reg 0)
     }
   } else {
     *special = acc;  // rows 0..rd-1 = rgb_raw (lane group 0, regs 0..rd-1)
+  }
+}
+
+// HBM store of forward tile i (train mode), issued at the START of the chunk interval after
+// the one that computed it: the barrier closing an interval drains vmcnt(0) (it must wait for
+// the weight DMA), so a store issued there has a whole interval to complete instead of
+// stalling that barrier.
+template <int MODE, int EPI, typename Frag>
+__device__ __forceinline__ void fwd_store(const RenderArgs<MODE>& A, int64_t sample, int i, const Frag* xo,
+                                          int outA) {
+  constexpr int TM = Tr<MODE>::TM, FPT = Tr<MODE>::FPT;
+  if (!A.train) return;
+  if constexpr (EPI == 0) {
+    store_tile_frags<MODE>(act_ptr(A, outA, sample, i), xo + i * FPT);
+  } else if constexpr (EPI == 1) {
+    if (i < WIDTH / TM) store_tile_frags<MODE>(act_ptr(A, A_BT, sample, i), xo + i * FPT);
   }
 }
 
@@ -127,6 +143,7 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
     int nbytes;
     fwd_next<MODE>(L, i, &noff, &nbytes);
     chunk_step(lds, A.w, CB + i, noff, nbytes, [&](const char* chunk) {
+      if (i >= 2) fwd_store<MODE, EPI>(A, sample, i - 2, xo, outA);
       Acc acc;
       const float* bias = (const float*)(lds + 2 * LDS_BUF) + (CB + i) * TM + grp * T::REGS;
 #pragma unroll
@@ -138,6 +155,8 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
     });
   }
   fwd_epilogue<MODE, L, EPI>(A, sample, prev, NT - 1, xo, outA, special);
+  if constexpr (NT >= 2) fwd_store<MODE, EPI>(A, sample, NT - 2, xo, outA);
+  fwd_store<MODE, EPI>(A, sample, NT - 1, xo, outA);
 }
 
 // ------------------------------------------------------------------ forward kernel
@@ -339,8 +358,9 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
       for (int r = 0; r < T::REGS; ++r) acc[r] = acc[r] * hidden_dact<MODE>(sv[r]);
     }
     acc_to_frags<MODE>(acc, xo + i * FPT);
-    store_tile_frags<MODE>(act_ptr(A, DZ, sample, i), xo + i * FPT);
   };
+  // dz stores deferred to the start of the next chunk interval (see fwd_store)
+  auto store = [&](int i) { store_tile_frags<MODE>(act_ptr(A, DZ, sample, i), xo + i * FPT); };
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     int64_t noff;
@@ -348,6 +368,7 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
     bwd_next<MODE>(J, i, &noff, &nbytes);
     if constexpr (DER == 0) s_cur = load_tile_vals<MODE>(act_ptr(A, SA, sample, i));
     chunk_step(lds, A.w, cb + i, noff, nbytes, [&](const char* chunk) {
+      if (i >= 2) store(i - 2);
       Acc acc = acc_zero<MODE>();
       mfma_chunk<MODE, KS>(chunk, x, acc);
       if (i > 0) epilogue(prev, s_prev, i - 1);
@@ -356,6 +377,8 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
     s_prev = s_cur;
   }
   epilogue(prev, s_prev, NT - 1);
+  if constexpr (NT >= 2) store(NT - 2);
+  store(NT - 1);
 }
 
 template <int MODE>
