@@ -4,12 +4,14 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
 
 #include "../../include/den_api.h"
 #include "den_dw.hip"
+#include "den_hidden.hip"
 #include "den_misc.hip"
 #include "den_pixbw.hip"
 #include "den_render.hip"
@@ -45,6 +47,17 @@ struct WsLayout {
 
 constexpr int64_t DW_BLOCK_MAX = 8LL * 11 * 1024;  // floats per split for the largest layer (L5: MT 8, NT+1 11)
 
+// persistent workgroups of the layer-major hidden backward: one per CU, at most one per wave block
+inline int64_t hidden_grid(int64_t n_samples) { return std::min<int64_t>(HB_GRID_MAX, std::max<int64_t>(1, n_samples / 32)); }
+
+// BF16 backward: layer-major hidden layers (den_hidden.hip) unless DEN_BWD=sample selects the
+// sample-major chain + split-K GEMMs of the F32 mode (A/B comparisons).
+inline bool use_hidden_path(int mode) {
+  if (mode != DEN_MODE_BF16) return false;
+  const char* e = std::getenv("DEN_BWD");
+  return !(e && std::strcmp(e, "sample") == 0);
+}
+
 WsLayout ws_layout(const den_render_desc* d) {
   WsLayout L{};
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
@@ -66,7 +79,9 @@ WsLayout ws_layout(const den_render_desc* d) {
   L.splits = (int)splits;
   L.per_split = per;
   L.dw_partial = off;
-  if (d->train) off += align256((size_t)splits * DW_BLOCK_MAX * 4);
+  // shared by the split-K GEMMs and the layer-major hidden backward (den_hidden.hip)
+  const size_t hidden = (size_t)hidden_grid(n) * 8 * 9 * 1024;
+  if (d->train) off += align256(std::max((size_t)splits * DW_BLOCK_MAX, hidden) * 4);
   L.total = off;
   return L;
 }
@@ -147,6 +162,40 @@ int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, 
   return DEN_OK;
 }
 
+// Layer-major backward of hidden layer l (den_hidden.hip) + reduction of its weight/bias gradient.
+int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLayout& L, char* ws, int l, float* grad,
+                  hipStream_t s) {
+  const int64_t n = (int64_t)d->n_rays * d->n_samples;
+  HiddenArgs H{};
+  H.w = (const char*)io->w_bwd + bwd_layer_offset(DEN_MODE_BF16, 10 - l);
+  H.dz_in = ws + L.act[D_Z0 + l];
+  H.s_in = ws + L.act[A_S0 + l - 1];
+  H.dz_out = ws + L.act[D_Z0 + l - 1];
+  H.partial = (float*)(ws + L.dw_partial);
+  H.n_blocks = n / 32;
+  const int64_t grid = hidden_grid(n);
+  H.per_wg = (H.n_blocks + grid - 1) / grid;
+  hipLaunchKernelGGL(hidden_bwd_kernel, dim3((unsigned)grid), dim3(HB_THREADS), 0, s, H);
+  DEN_LAUNCHED();
+  DwReduceArgs R{};
+  R.partial = H.partial;
+  R.splits = (int)grid;
+  R.MT = 8;
+  R.NT = 8;
+  R.m_off = 0;
+  R.layer = l;
+  R.mode = DEN_MODE_BF16;
+  R.rd = d->radiance_dim;
+  R.n1 = WIDTH;
+  R.n1_feat = 0;
+  R.bias = 1;
+  R.grad = grad;
+  const int64_t per = 8LL * 9 * 1024;
+  hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
 template <int MODE>
 int render_fwd_impl(const den_render_desc* d, const den_render_io* io, hipStream_t s) {
   WsLayout L = ws_layout(d);
@@ -168,22 +217,40 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
   A.d_opacity = g->d_opacity;
   A.d_depth = g->d_depth;
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
-  if (parts & 1) {
-    hipLaunchKernelGGL(render_bwd_kernel<MODE>, dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s, A);
-    DEN_LAUNCHED();
-  }
-  if (!(parts & 2)) return DEN_OK;
   char* ws = (char*)io->workspace;
   float* G = g->grad_params;
+  const bool hidden = use_hidden_path(MODE);
   int rc;
+  if (parts & 1) {
+    if constexpr (MODE == DEN_MODE_BF16) {
+      if (hidden) {
+        // head (compositing adjoint, Lr^T, Lg^T, Lb^T) sample-major, then L7..L1 layer-major
+        hipLaunchKernelGGL((render_bwd_kernel<MODE, 2>), dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s, A);
+        DEN_LAUNCHED();
+        for (int l = 7; l >= 1; --l)
+          if ((rc = launch_hidden(d, io, L, ws, l, G, s)) != DEN_OK) return rc;
+      }
+    }
+    if (!hidden) {
+      hipLaunchKernelGGL((render_bwd_kernel<MODE, NBL - 1>), dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s,
+                         A);
+      DEN_LAUNCHED();
+    }
+  }
+  if (!(parts & 2)) return DEN_OK;
   if ((rc = launch_dw<MODE, 8, 64, 0>(d, L, ws, 0, D_Z0 + 0, A_PE, -1, 0, G, s)) != DEN_OK) return rc;
-  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 1, D_Z0 + 1, A_S0 + 0, -1, 0, G, s)) != DEN_OK) return rc;
-  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 2, D_Z0 + 2, A_S0 + 1, -1, 0, G, s)) != DEN_OK) return rc;
-  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 3, D_Z0 + 3, A_S0 + 2, -1, 0, G, s)) != DEN_OK) return rc;
-  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 4, D_Z0 + 4, A_S0 + 3, -1, 0, G, s)) != DEN_OK) return rc;
-  if ((rc = launch_dw<MODE, 8, 256, 64>(d, L, ws, 5, D_Z0 + 5, A_S0 + 4, A_PE, WIDTH, G, s)) != DEN_OK) return rc;
-  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 6, D_Z0 + 6, A_S0 + 5, -1, 0, G, s)) != DEN_OK) return rc;
-  if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 7, D_Z0 + 7, A_S0 + 6, -1, 0, G, s)) != DEN_OK) return rc;
+  if (hidden) {
+    // pe columns of L5 (the S4 columns and the bias come from the hidden launch of layer 5)
+    if ((rc = launch_dw<MODE, 8, 64, 0>(d, L, ws, 5, D_Z0 + 5, A_PE, -1, WIDTH, G, s, 0, 0, 0)) != DEN_OK) return rc;
+  } else {
+    if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 1, D_Z0 + 1, A_S0 + 0, -1, 0, G, s)) != DEN_OK) return rc;
+    if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 2, D_Z0 + 2, A_S0 + 1, -1, 0, G, s)) != DEN_OK) return rc;
+    if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 3, D_Z0 + 3, A_S0 + 2, -1, 0, G, s)) != DEN_OK) return rc;
+    if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 4, D_Z0 + 4, A_S0 + 3, -1, 0, G, s)) != DEN_OK) return rc;
+    if ((rc = launch_dw<MODE, 8, 256, 64>(d, L, ws, 5, D_Z0 + 5, A_S0 + 4, A_PE, WIDTH, G, s)) != DEN_OK) return rc;
+    if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 6, D_Z0 + 6, A_S0 + 5, -1, 0, G, s)) != DEN_OK) return rc;
+    if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 7, D_Z0 + 7, A_S0 + 6, -1, 0, G, s)) != DEN_OK) return rc;
+  }
   // [bottleneck | sigma]: the 256 bottleneck rows, then the sigma tile (row 256)
   if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, L_B, D_ZB, A_S0 + 7, -1, 0, G, s)) != DEN_OK) return rc;
   if ((rc = launch_dw<MODE, 1, 256, 0>(d, L, ws, L_B, D_ZB, A_S0 + 7, -1, 0, G, s, WIDTH)) != DEN_OK) return rc;

@@ -1,0 +1,189 @@
+// den_hidden.hip -- layer-major backward of the hidden layers L7..L1 (BF16 mode).
+//
+// One launch per hidden layer l (transposed layer j = 10 - l), one persistent workgroup per CU
+// sweeping a contiguous range of 32-sample wave blocks of the wave-block-major activation tensors
+// (den_geom.h).  Per block, wave w of 4 (one per SIMD, 512 VGPRs) owns rows [64w, 64w + 64):
+//   chain : dS_{l-1} = W_l^T dz_l                (A = W_l^T row tiles 2w, 2w+1 held in VGPRs for
+//           dz_{l-1} = dS_{l-1} * (1 - 2^-S'_{l-1})   the whole launch, B = dz_l fragments from LDS)
+//   dW    : dW_l[rows 64w..][all 256] += dz_l (x) S'_{l-1},  db_l += dz_l
+//           (k = samples: both operands by ds_read_b64_tr_b16 from the same LDS blocks; the bias from
+//           VALU sums of the dz operand), accumulated in registers over the whole range, written once as a
+//           split-K partial for dw_reduce_kernel (den_dw.hip layout, MT = NT = 8).
+// dz_l and S'_{l-1} (16 KiB per block each) arrive by LDS-DMA one block ahead.  Per sample and layer
+// this moves 1.5 KiB of HBM (read dz_l and S'_{l-1}, write dz_{l-1}) where the sample-major chain
+// plus the split-K GEMM (den_render.hip + den_dw.hip; kept for the F32 parity mode) move 3 KiB.
+//
+// Reference: the nn.Linear backward of base.hidden_layers.{1..7} with softplus(beta=100)
+// (external/mlp.py:99-113, models/nerf.py:18), in the scaled base-2 units of den_geom.h.
+#include "den_device.h"
+
+namespace den {
+
+constexpr int HB_WAVES = 4;
+constexpr int HB_THREADS = 64 * HB_WAVES;
+constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
+constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
+constexpr int HB_SLOT = 2 * HB_BLOCK;  // LDS ring slot: [dz_l block | S'_{l-1} block]
+constexpr int HB_GRID_MAX = 256;
+
+typedef short hb_v4i16 __attribute__((ext_vector_type(4)));
+
+struct HiddenArgs {
+  const char* w;      // packed transposed weights of the layer (bwd chunk 0 of layer j, 16 KiB per row tile)
+  const char* dz_in;  // dz_l
+  const char* s_in;   // S'_{l-1}
+  char* dz_out;       // dz_{l-1}
+  float* partial;     // [gridDim.x][8][9][64][16]
+  int64_t n_blocks;   // 32-sample wave blocks
+  int64_t per_wg;     // blocks per workgroup
+};
+
+// 16-byte LDS slot that holds tile lane `lane`'s fragment f inside a 1 KiB piece:
+// lane c + 32h -> 32h + (c ^ 4(2h + f)).  An involution for each (h, f); it spreads the
+// 4-sample x 16-feature blocks of the transposed reads over all 64 banks, while the plain
+// per-lane fragment reads stay a permutation of one 1 KiB piece (conflict-free either way).
+__device__ __forceinline__ int hb_slot(int lane, int f) {
+  const int h = lane >> 5;
+  return 32 * h + ((lane & 31) ^ (4 * (2 * h + f)));
+}
+
+// LDS-DMA of one 16 KiB block (pieces pc = 2t + f of 1 KiB): the destination of an LDS-DMA
+// instruction is linear, so lane p fetches the tile lane whose fragment belongs in slot p.
+__device__ __forceinline__ void hb_dma(const char* src, char* dst) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < 16 / HB_WAVES; ++q) {
+    const int pc = q * HB_WAVES + wave;  // wave-uniform
+    __builtin_amdgcn_global_load_lds((const void*)(src + pc * 1024 + hb_slot(lane, pc & 1) * 16),
+                                     (lds_ptr_t)(dst + pc * 1024), 16, 0, 0);
+  }
+}
+
+// This lane's own fragment f of a tile in LDS (the chain's B operand / the stored activation).
+__device__ __forceinline__ bf16x8 hb_frag(const char* tile, int f) {
+  return *(const bf16x8*)(tile + f * 1024 + hb_slot(threadIdx.x & 63, f) * 16);
+}
+
+// Operand with k = samples: row (A) / column (B) index = feature (stored position) l & 31 of the
+// tile, k-slot 8(l >> 5) + j = sample 16 kk + 8(l >> 5) + j of the block; two transposed reads of
+// 4 samples x 16 features per 16-lane group.
+__device__ __forceinline__ bf16x8 hb_tr_frag(const char* tile, int kk) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const int hq = g & 1, p = i & 3, f = p >> 1;
+  bf16x8 out;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int c = 16 * kk + 8 * (g >> 1) + 4 * r + (i >> 2);
+    const char* a = tile + f * 1024 + hb_slot(c + 32 * hq, f) * 16 + (p & 1) * 8;
+    const hb_v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) hb_v4i16*)a);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[4 * r + e] = __builtin_bit_cast(__bf16, (short)v[e]);
+  }
+  return out;
+}
+
+__global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * HB_SLOT];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t b0 = (int64_t)blockIdx.x * P.per_wg;
+  const int64_t b1 = b0 + P.per_wg < P.n_blocks ? b0 + P.per_wg : P.n_blocks;
+
+  if (b0 < b1) {
+    hb_dma(P.dz_in + b0 * HB_BLOCK, lds);
+    hb_dma(P.s_in + b0 * HB_BLOCK, lds + HB_BLOCK);
+  }
+  // W_l^T row tiles 2w, 2w+1: packed [row tile][kappa][lane][8] = the chain's A fragments
+  bf16x8 wt[2][16];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      wt[t][k] = *(const bf16x8*)(P.w + (int64_t)(2 * wave + t) * 16384 + k * 1024 + lane * 16);
+  f32x16 dw[2][8];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dw[t][n][r] = 0.0f;
+  float db[2] = {0.0f, 0.0f};  // bias partial: feature (lane & 31) of row tile 2w + t, this lane's samples
+  __syncthreads();
+
+  for (int64_t b = b0; b < b1; ++b) {
+    const char* cur = lds + (int)((b - b0) & 1) * HB_SLOT;
+    char* nxt = lds + (int)((b - b0 + 1) & 1) * HB_SLOT;
+    if (b + 1 < b1) {
+      hb_dma(P.dz_in + (b + 1) * HB_BLOCK, nxt);
+      hb_dma(P.s_in + (b + 1) * HB_BLOCK, nxt + HB_BLOCK);
+    }
+    const char* dzb = cur;
+    const char* sb = cur + HB_BLOCK;
+    // chain: two row tiles, K = 256 (16 k-steps); then the activation derivative
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[t][k], hb_frag(dzb + (k >> 1) * HB_TILE, k & 1), acc, 0,
+                                                       0, 0);
+      const char* st = sb + (2 * wave + t) * HB_TILE;
+      const bf16x8 s0 = hb_frag(st, 0), s1 = hb_frag(st, 1);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float sv = (float)(r < 8 ? s0[r] : s1[r - 8]);
+        acc[r] = acc[r] * dsoftplus2_scaled_from_out(sv);
+      }
+      // dz_{l-1} tile: stored now, the weight-gradient MFMAs below cover its write latency
+      bf16x8 of[2];
+      acc_to_frags<1>(acc, of);
+      char* d = P.dz_out + (b * 8 + 2 * wave + t) * HB_TILE + lane * 16;
+      *(bf16x8*)d = of[0];
+      *(bf16x8*)(d + 1024) = of[1];
+    }
+    // weight / bias gradients over the block's 32 samples (two k-steps of 16)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 a0 = hb_tr_frag(dzb + (2 * wave) * HB_TILE, kk);
+      const bf16x8 a1 = hb_tr_frag(dzb + (2 * wave + 1) * HB_TILE, kk);
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        const bf16x8 bb = hb_tr_frag(sb + n * HB_TILE, kk);
+        dw[0][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bb, dw[0][n], 0, 0, 0);
+        dw[1][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bb, dw[1][n], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        db[0] += (float)a0[j];
+        db[1] += (float)a1[j];
+      }
+    }
+    __syncthreads();
+  }
+  // split-K partial of this workgroup (dw_gemm_kernel layout: [wg][mt][nt][lane][16]); the bias
+  // goes where that layout's ones tile (nt = 8) keeps it: column 0 = lanes 0 and 32, row m in
+  // register (m & 3) + 4 (m >> 3) of lane 32 ((m >> 2) & 1)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const float bsum = db[t] + __shfl_xor(db[t], 32, 64);
+    if (lane < 32) {
+      const int m = lane;
+      float* o = P.partial + (((int64_t)blockIdx.x * 8 + 2 * wave + t) * 9 + 8) * 1024;
+      o[(32 * ((m >> 2) & 1)) * 16 + (m & 3) + 4 * (m >> 3)] = bsum;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      float* o = P.partial + (((int64_t)blockIdx.x * 8 + 2 * wave + t) * 9 + n) * 1024 + lane * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4 v = {dw[t][n][4 * q], dw[t][n][4 * q + 1], dw[t][n][4 * q + 2], dw[t][n][4 * q + 3]};
+        *(f32x4*)(o + 4 * q) = v;
+      }
+    }
+}
+
+}  // namespace den

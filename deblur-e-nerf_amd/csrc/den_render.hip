@@ -78,11 +78,11 @@ __device__ __forceinline__ void fwd_next(int l, int i, int64_t* off, int* bytes)
   *bytes = chunk_bytes_K(fwd_K(MODE, nl));
   *off = fwd_layer_offset(MODE, nl) + (int64_t)ni * *bytes;
 }
-template <int MODE>
+template <int MODE, int LAST_J>
 __device__ __forceinline__ void bwd_next(int j, int i, int64_t* off, int* bytes) {
   int nj = j, ni = i + 1;
   if (ni >= bwd_tiles(MODE, j)) { nj = j + 1; ni = 0; }
-  if (nj >= NBL) { *off = 0; *bytes = 0; return; }
+  if (nj > LAST_J) { *off = 0; *bytes = 0; return; }
   *bytes = chunk_bytes_K(bwd_K(MODE, nj));
   *off = bwd_layer_offset(MODE, nj) + (int64_t)ni * *bytes;
 }
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
 // DER: 0 = softplus(100) derivative from stored output, 1 = identity.
 // The stored activation of tile i is loaded before tile i's MFMA chain and
 // consumed by its epilogue one tile later (software pipeline, as forward).
-template <int MODE, int J, int KS, int DER, typename Frag>
+template <int MODE, int LAST_J, int J, int KS, int DER, typename Frag>
 __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* lds, int64_t sample, const Frag* x,
                                               Frag* xo, int SA, int DZ) {
   using T = Tr<MODE>;
@@ -365,7 +365,7 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
   for (int i = 0; i < NT; ++i) {
     int64_t noff;
     int nbytes;
-    bwd_next<MODE>(J, i, &noff, &nbytes);
+    bwd_next<MODE, LAST_J>(J, i, &noff, &nbytes);
     if constexpr (DER == 0) s_cur = load_tile_vals<MODE>(act_ptr(A, SA, sample, i));
     chunk_step(lds, A.w, cb + i, noff, nbytes, [&](const char* chunk) {
       if (i >= 2) store(i - 2);
@@ -381,7 +381,9 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
   store(NT - 1);
 }
 
-template <int MODE>
+// LAST_J = NBL - 1: the whole chain (F32 parity mode).  LAST_J = 2: stop after Lb^T (writes
+// dz_7); the hidden layers then run layer-major in den_hidden.hip (BF16 mode).
+template <int MODE, int LAST_J>
 __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) {
   using T = Tr<MODE>;
   using Frag = typename T::Frag;
@@ -525,9 +527,9 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
   acc_to_frags<MODE>(dzr, fr);
   Frag xa[KS + 2 * FPT], xb[KS + 2 * FPT];
   // j=0 Lr^T: dz_r -> dG * softplus'(G) -> DZG (128 rows)
-  bwd_layer_run<MODE, 0, FPT, 0>(A, lds, sample, fr, xa, A_G, D_ZG);
+  bwd_layer_run<MODE, LAST_J, 0, FPT, 0>(A, lds, sample, fr, xa, A_G, D_ZG);
   // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles 0..
-  bwd_layer_run<MODE, 1, WIDTH_COND / T::KI, 1>(A, lds, sample, xa, xb, 0, D_ZB);
+  bwd_layer_run<MODE, LAST_J, 1, WIDTH_COND / T::KI, 1>(A, lds, sample, xa, xb, 0, D_ZB);
   // sigma head row(s) of Lb as extra fake tile(s) appended to the DZB fragments
   {
     constexpr int EXTRA_T = (DZB_W - WIDTH) / TM;  // sigma tile + zero padding
@@ -539,20 +541,23 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
     }
   }
   // j=2 Lb^T: dz_b (K = fwd_M(Lb)) -> dS7 * softplus'(S7) -> DZ7
-  bwd_layer_run<MODE, 2, fwd_M(MODE, L_B) / T::KI, 0>(A, lds, sample, xb, xa, A_S0 + 7, D_Z0 + 7);
-  // j=3.. L7^T..L1^T
-  bwd_layer_run<MODE, 3, KS, 0>(A, lds, sample, xa, xb, A_S0 + 6, D_Z0 + 6);
-  bwd_layer_run<MODE, 4, KS, 0>(A, lds, sample, xb, xa, A_S0 + 5, D_Z0 + 5);
-  bwd_layer_run<MODE, 5, KS, 0>(A, lds, sample, xa, xb, A_S0 + 4, D_Z0 + 4);
-  bwd_layer_run<MODE, 6, KS, 0>(A, lds, sample, xb, xa, A_S0 + 3, D_Z0 + 3);
-  bwd_layer_run<MODE, 7, KS, 0>(A, lds, sample, xa, xb, A_S0 + 2, D_Z0 + 2);
-  bwd_layer_run<MODE, 8, KS, 0>(A, lds, sample, xb, xa, A_S0 + 1, D_Z0 + 1);
-  bwd_layer_run<MODE, 9, KS, 0>(A, lds, sample, xa, xb, A_S0 + 0, D_Z0 + 0);
+  bwd_layer_run<MODE, LAST_J, 2, fwd_M(MODE, L_B) / T::KI, 0>(A, lds, sample, xb, xa, A_S0 + 7, D_Z0 + 7);
+  if constexpr (LAST_J > 2) {
+    // j=3.. L7^T..L1^T
+    bwd_layer_run<MODE, LAST_J, 3, KS, 0>(A, lds, sample, xa, xb, A_S0 + 6, D_Z0 + 6);
+    bwd_layer_run<MODE, LAST_J, 4, KS, 0>(A, lds, sample, xb, xa, A_S0 + 5, D_Z0 + 5);
+    bwd_layer_run<MODE, LAST_J, 5, KS, 0>(A, lds, sample, xa, xb, A_S0 + 4, D_Z0 + 4);
+    bwd_layer_run<MODE, LAST_J, 6, KS, 0>(A, lds, sample, xb, xa, A_S0 + 3, D_Z0 + 3);
+    bwd_layer_run<MODE, LAST_J, 7, KS, 0>(A, lds, sample, xa, xb, A_S0 + 2, D_Z0 + 2);
+    bwd_layer_run<MODE, LAST_J, 8, KS, 0>(A, lds, sample, xb, xa, A_S0 + 1, D_Z0 + 1);
+    bwd_layer_run<MODE, LAST_J, 9, KS, 0>(A, lds, sample, xa, xb, A_S0 + 0, D_Z0 + 0);
+  }
 }
 
 template __global__ void render_fwd_kernel<0>(RenderArgs<0>);
 template __global__ void render_fwd_kernel<1>(RenderArgs<1>);
-template __global__ void render_bwd_kernel<0>(RenderArgs<0>);
-template __global__ void render_bwd_kernel<1>(RenderArgs<1>);
+template __global__ void render_bwd_kernel<0, NBL - 1>(RenderArgs<0>);
+template __global__ void render_bwd_kernel<1, NBL - 1>(RenderArgs<1>);
+template __global__ void render_bwd_kernel<1, 2>(RenderArgs<1>);
 
 }  // namespace den

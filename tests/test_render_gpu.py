@@ -111,6 +111,68 @@ def test_render_matches_oracle(mode, n_samples, rd, bk):
     print(f"[{mode} S={n_samples} rd={rd}] worst grad err {worst:.2e}")
 
 
+def _render_grads(mode, rd, R, n_samples, seed, env=None):
+    nat = _nat()
+    o, d, u = synthetic_rays(R, seed=seed)
+    p = onerf.build_params(rd, 1)
+    flat = flat_from_params(p, rd).to(DEV).requires_grad_(True)
+    packed = nat.PackedWeights(mode, rd, DEV)
+    packed.pack(flat.detach())
+    bk = torch.tensor([0.9, 0.8, 0.7][:rd], device=DEV, requires_grad=True)
+    old = os.environ.get("DEN_BWD")
+    if env is not None:
+        os.environ["DEN_BWD"] = env
+    try:
+        c, op, dp = nat.render(o.to(DEV), d.to(DEV), u.to(DEV), bk, flat, _cfg(mode, rd), packed, n_samples)
+        g = torch.Generator().manual_seed(seed + 1)
+        gc = torch.randn(c.shape, generator=g).to(DEV)
+        go = torch.randn(op.shape, generator=g).to(DEV)
+        ((c * gc).sum() + (op * go).sum()).backward()
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            os.environ.pop("DEN_BWD", None)
+        else:
+            os.environ["DEN_BWD"] = old
+    return c.detach(), flat.grad.detach().clone(), bk.grad.detach().clone(), p
+
+
+@pytest.mark.parametrize("rd", [1, 3])
+def test_hidden_layer_major_backward_matches_sample_major(rd):
+    """BF16: the layer-major hidden backward (den_hidden.hip, several 32-sample blocks per
+    persistent workgroup) against the sample-major chain + split-K GEMM path on the same
+    bf16 operands -- only f32 summation order differs."""
+    R = 1024  # 131072 samples = 4096 wave blocks = 16 per workgroup
+    c1, g1, b1, _ = _render_grads("bf16", rd, R, 128, seed=21)
+    c2, g2, b2, _ = _render_grads("bf16", rd, R, 128, seed=21, env="sample")
+    assert torch.equal(c1, c2)
+    gf1, gf2 = unflat(g1.cpu(), rd), unflat(g2.cpu(), rd)
+    worst = max(norm_rel(gf1[k], gf2[k]) for k in gf2)
+    print(f"[rd={rd}] layer-major vs sample-major worst grad rel diff {worst:.2e}")
+    assert worst <= 1e-3
+    assert norm_rel(b1.cpu(), b2.cpu()) <= 1e-5
+
+
+def test_render_bf16_many_blocks_matches_oracle():
+    """BF16 gradients vs the oracle on a batch where each hidden-backward workgroup sweeps
+    more than one wave block (128 rays x 128 samples = 512 blocks over <= 256 workgroups)."""
+    rd, R = 1, 128
+    c, g, bk, p = _render_grads("bf16", rd, R, 128, seed=33)
+    o, d, u = synthetic_rays(R, seed=33)
+    for k in p:
+        p[k].requires_grad_(True)
+    bkgd = torch.tensor([0.9], requires_grad=True)
+    col, op, dep, _ = onerf.render_rays(p, o, d, u, n_samples=128, bkgd=bkgd)
+    gen = torch.Generator().manual_seed(34)
+    gc, go = torch.randn(col.shape, generator=gen), torch.randn(op.shape, generator=gen)
+    ((col * gc).sum() + (op * go).sum()).backward()
+    assert rel_err(c, col) <= 0.12
+    gf = unflat(g.cpu(), rd)
+    worst = max(norm_rel(gf[k], v.grad) for k, v in p.items())
+    print(f"bf16 many-block worst grad err {worst:.2e}")
+    assert worst <= 6e-2
+
+
 def test_render_rejects_bad_shapes():
     nat = _nat()
     flat = torch.zeros(nat.param_count(3), device=DEV)
