@@ -356,6 +356,81 @@ int den_adam_step(int64_t n, float* p, const float* g, float* m, float* v, float
   return DEN_OK;
 }
 
+// ------------------------------------------------------------------ pixel bandwidth
+int den_pixbw_blocks(int32_t N) { return N > 0 ? (N + PIXBW_BLOCK - 1) / PIXBW_BLOCK : 0; }
+
+size_t den_pixbw_workspace_bytes(int32_t S, int32_t N) {
+  if (S < 2 || N <= 0) return 0;
+  return ((size_t)(S - 1) * PIXBW_SEG_F + (size_t)S * 8) * (size_t)N * sizeof(double);
+}
+
+int den_pixbw_sample_ts(int32_t S, int32_t N, const double* gen, const double* out_ts, double omega_c_min,
+                        double max_cumprob, double* ts, void* stream) {
+  if (S < 2 || N <= 0 || !out_ts || !ts || (S > 2 && !gen)) return fail(DEN_EINVAL, "bad arguments");
+  if (!(omega_c_min > 0.0) || !(max_cumprob > 0.0 && max_cumprob < 1.0))
+    return fail(DEN_EINVAL, "omega_c_min must be > 0 and max_cumprob in (0, 1)");
+  // torch.distributions.Exponential keeps the Python-float rate as an f32 tensor and the target
+  // cumulative probability is an f32 buffer (pixel_bandwidth.py:81-83, 344-350)
+  const float rate = (float)(1e-9 * omega_c_min), cum = (float)max_cumprob;
+  const int64_t tot = (int64_t)S * N;
+  hipLaunchKernelGGL(pixbw_sample_ts_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     S, N, gen, out_ts, rate, cum, ts);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+static int pixbw_args(int32_t S, int32_t N, int32_t reset, const float* it, const double* ts, const double* out_ts,
+                      const float* prm, const float* delta_in, const double* reset_ts, PixArgs* A) {
+  if (S < 2 || N <= 0 || !it || !ts || !out_ts || !prm) return fail(DEN_EINVAL, "bad arguments");
+  if (!reset && (!delta_in || !reset_ts))
+    return fail(DEN_EINVAL, "a non-reset call needs delta_in and reset_ts of a preceding reset call");
+  *A = PixArgs{};
+  A->S = S;
+  A->N = N;
+  A->reset = reset ? 1 : 0;
+  A->it = it;
+  A->ts = ts;
+  A->out_ts = out_ts;
+  A->prm = prm;
+  A->delta_in = delta_in;
+  A->reset_ts = reset_ts;
+  return DEN_OK;
+}
+
+int den_pixbw_fwd(int32_t S, int32_t N, int32_t reset, const float* it, const double* ts, const double* out_ts,
+                  const float* prm, const float* delta_in, const double* reset_ts, float* out, float* delta_out,
+                  void* stream) {
+  PixArgs A;
+  int rc = pixbw_args(S, N, reset, it, ts, out_ts, prm, delta_in, reset_ts, &A);
+  if (rc) return rc;
+  if (!out || (reset && !delta_out)) return fail(DEN_EINVAL, "out (and delta_out for a reset call) are required");
+  A.out = out;
+  A.delta_out = delta_out;
+  hipLaunchKernelGGL(pixbw_fwd_kernel, dim3((unsigned)den_pixbw_blocks(N)), dim3(PIXBW_BLOCK), 0, (hipStream_t)stream, A);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_pixbw_bwd(int32_t S, int32_t N, int32_t reset, const float* it, const double* ts, const double* out_ts,
+                  const float* prm, const float* delta_in, const double* reset_ts, const float* d_out,
+                  const float* d_delta_out, void* workspace, float* d_it, float* d_delta_in, float* d_prm,
+                  void* stream) {
+  PixArgs A;
+  int rc = pixbw_args(S, N, reset, it, ts, out_ts, prm, delta_in, reset_ts, &A);
+  if (rc) return rc;
+  if (!d_out || !workspace || !d_it || !d_prm || (!reset && !d_delta_in))
+    return fail(DEN_EINVAL, "d_out, workspace, d_intensity, d_params_partial (and d_delta_in) are required");
+  A.d_out = d_out;
+  A.d_delta_out = reset ? d_delta_out : nullptr;
+  A.ws = (double*)workspace;
+  A.d_it = d_it;
+  A.d_delta_in = d_delta_in;
+  A.d_prm = d_prm;
+  hipLaunchKernelGGL(pixbw_bwd_kernel, dim3((unsigned)den_pixbw_blocks(N)), dim3(PIXBW_BLOCK), 0, (hipStream_t)stream, A);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
 size_t den_event_loss_workspace_bytes(int32_t N) {
   const int nb = (N + LOSS_BLOCK - 1) / LOSS_BLOCK;
   return (size_t)(2 * nb + 2 + nb) * 4;

@@ -69,9 +69,10 @@ _SIGS = {
     "den_event_step_bwd": (ctypes.c_int, [ctypes.c_int32] * 5 + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 8),
     "den_pixbw_sample_ts": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]),
-    "den_pixbw_fwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 10),
+    "den_pixbw_fwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 9),
     "den_pixbw_blocks": (ctypes.c_int, [ctypes.c_int32]),
-    "den_pixbw_bwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 14),
+    "den_pixbw_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
+    "den_pixbw_bwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 13),
 }
 
 
@@ -290,3 +291,80 @@ def event_target(ts_diff, lid, end_ts, start_ts, c):
                                   _ptr(end_ts.long().contiguous()), _ptr(start_ts.double().contiguous()),
                                   _ptr(c.float().reshape(1).contiguous()), _ptr(out), _stream(lid.device)))
     return out
+
+
+# ----------------------------------------------------------------------------- pixel bandwidth
+PIXBW_NPARAM = 7
+
+
+def pixbw_sample_ts(gen, output_ts, omega_c_min, max_cumprob):
+    """den_pixbw_sample_ts: (S-1, ...) f64 interval generators and (...) f64 output
+    timestamps (ns) -> (S, ...) f64 sample timestamps (pixel_bandwidth.py:311-360,
+    before the clamp to min_ts)."""
+    _require_device(gen, output_ts)
+    S = gen.shape[0] + 1
+    batch = output_ts.shape
+    N = output_ts.numel()
+    g = gen.reshape(S - 1, N).to(torch.float64).contiguous()
+    o = output_ts.reshape(N).to(torch.float64).contiguous()
+    ts = torch.empty(S, N, dtype=torch.float64, device=gen.device)
+    _check(lib().den_pixbw_sample_ts(S, N, _ptr(g), _ptr(o), float(omega_c_min), float(max_cumprob), _ptr(ts),
+                                     _stream(gen.device)))
+    return ts.reshape(S, *batch)
+
+
+class PixelBandwidthFunction(torch.autograd.Function):
+    """One PixelBandwidth call after intensity sampling (pixel_bandwidth.py:369-448).
+
+    intensity (S, ...) and params (7) = [tau_in_it_eff_prod, tau_mil_it_eff_prod, A_amp_inv,
+    A_loop_inv, tau_out, tau_sf, tau_diff] (post-parametrisation) -> (out, delta_out), both (...).
+    reset=True resets the differencing amplifier (delta_out = its offset, the reference's
+    ``reset_delta_log_it``); otherwise delta_in / reset_ts of the preceding reset call decay the
+    offset and delta_out is zeros."""
+
+    @staticmethod
+    def forward(ctx, intensity, params, delta_in, sample_ts, output_ts, reset_ts, reset):
+        _require_device(intensity, params, delta_in, sample_ts, output_ts, reset_ts)
+        S = intensity.shape[0]
+        N = intensity[0].numel()
+        dev = intensity.device
+        it = intensity.reshape(S, N).to(torch.float32).contiguous()
+        ts = sample_ts.reshape(S, N).to(torch.float64).contiguous()
+        ots = output_ts.reshape(N).to(torch.float64).contiguous()
+        prm = params.to(torch.float32).contiguous()
+        din = None if reset else delta_in.reshape(N).to(torch.float32).contiguous()
+        rts = None if reset else reset_ts.reshape(N).to(torch.float64).contiguous()
+        out = torch.empty(N, dtype=torch.float32, device=dev)
+        delta_out = torch.empty(N, dtype=torch.float32, device=dev) if reset else torch.zeros(
+            N, dtype=torch.float32, device=dev)
+        _check(lib().den_pixbw_fwd(S, N, int(reset), _ptr(it), _ptr(ts), _ptr(ots), _ptr(prm), _ptr(din), _ptr(rts),
+                                   _ptr(out), _ptr(delta_out) if reset else None, _stream(dev)))
+        ctx.save_for_backward(it, ts, ots, prm, din, rts)
+        ctx.reset = bool(reset)
+        ctx.in_dtype, ctx.in_shape, ctx.p_dtype = intensity.dtype, intensity.shape, params.dtype
+        ctx.din_shape = None if reset else delta_in.shape
+        if not reset:
+            ctx.mark_non_differentiable(delta_out)
+        batch = intensity.shape[1:]
+        return out.reshape(batch), delta_out.reshape(batch)
+
+    @staticmethod
+    def backward(ctx, d_out, d_delta):
+        it, ts, ots, prm, din, rts = ctx.saved_tensors
+        S, N = it.shape
+        dev = it.device
+        L = lib()
+        g = torch.zeros(N, dtype=torch.float32, device=dev) if d_out is None else \
+            d_out.reshape(N).to(torch.float32).contiguous()
+        dd = d_delta.reshape(N).to(torch.float32).contiguous() if (ctx.reset and d_delta is not None) else None
+        ws = torch.empty(L.den_pixbw_workspace_bytes(S, N), dtype=torch.uint8, device=dev)
+        nb = L.den_pixbw_blocks(N)
+        d_it = torch.empty(S, N, dtype=torch.float32, device=dev)
+        d_din = None if ctx.reset else torch.empty(N, dtype=torch.float32, device=dev)
+        part = torch.empty(PIXBW_NPARAM * nb, dtype=torch.float32, device=dev)
+        _check(L.den_pixbw_bwd(S, N, int(ctx.reset), _ptr(it), _ptr(ts), _ptr(ots), _ptr(prm), _ptr(din), _ptr(rts),
+                               _ptr(g), _ptr(dd), _ptr(ws), _ptr(d_it), _ptr(d_din), _ptr(part), _stream(dev)))
+        d_prm = torch.empty(PIXBW_NPARAM, dtype=torch.float32, device=dev)
+        sum_partials(part, PIXBW_NPARAM, nb, d_prm)
+        return (d_it.reshape(ctx.in_shape).to(ctx.in_dtype), d_prm.to(ctx.p_dtype),
+                None if d_din is None else d_din.reshape(ctx.din_shape), None, None, None, None)

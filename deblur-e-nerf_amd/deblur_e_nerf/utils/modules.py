@@ -18,8 +18,9 @@ class Softplus(torch.nn.Module):
         return torch.nn.functional.softplus(x, self.beta, self.threshold)
 
     def right_inverse(self, y):
-        # inverse softplus, linear above the threshold
-        return torch.where(y * self.beta > self.threshold, y, torch.log(torch.expm1(self.beta * y)) / self.beta)
+        # inverse softplus, linear above the threshold -- the reference's exact expression
+        # (utils/modules.py:67-75), so parametrised originals match it bit for bit
+        return torch.where(y * self.beta > self.threshold, y, torch.log(torch.exp(self.beta * y) - 1) / self.beta)
 
 
 class ScaledShiftedSigmoid(torch.nn.Module):

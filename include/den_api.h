@@ -166,12 +166,15 @@ int den_pixbw_fwd(int32_t S, int32_t N, int32_t reset, const float* intensity,
 /* Backward.  d_out (N), d_delta_out (N, reset only, may be NULL) ->
  * d_intensity (S,N) (overwrite), d_delta_in (N, non-reset only; overwrite),
  * d_params_partial (DEN_PIXBW_NPARAM x n_blocks f32 partial sums; the caller
- * sums them with den_sum_partials).  n_blocks = den_pixbw_blocks(N). */
+ * sums them with den_sum_partials).  n_blocks = den_pixbw_blocks(N).
+ * workspace: den_pixbw_workspace_bytes(S, N) bytes (f64 Phi / Bd / Btd of every
+ * segment and the running row vectors of the weight recurrence). */
 int den_pixbw_blocks(int32_t N);
+size_t den_pixbw_workspace_bytes(int32_t S, int32_t N);
 int den_pixbw_bwd(int32_t S, int32_t N, int32_t reset, const float* intensity,
                   const double* sample_ts, const double* output_ts, const float* params,
                   const float* delta_in, const double* reset_ts, const float* d_out,
-                  const float* d_delta_out, float* d_intensity, float* d_delta_in,
+                  const float* d_delta_out, void* workspace, float* d_intensity, float* d_delta_in,
                   float* d_params_partial, void* stream);
 
 /* ---------------------------------------------------------------- event loss

@@ -91,9 +91,11 @@ def foh_discretise(A, B, dt):
     return Phi, G1 - G2, G2
 
 
-def weights(I, sample_ts, prm, with_sf):
-    """I (S, N), sample_ts (S, N) f64 ns -> unnormalised weights (S, N, o)."""
-    dt = NS_TO_S * torch.diff(sample_ts, dim=0).to(I.dtype)
+def weights(I, sample_ts, prm, with_sf, dt_dtype=None):
+    """I (S, N), sample_ts (S, N) f64 ns -> unnormalised weights (S, N, o).
+    dt_dtype: dtype the f64 timestamp differences are cast to (the reference casts
+    them to the intensity dtype, pixel_bandwidth.py:486; f32 in its training runs)."""
+    dt = NS_TO_S * torch.diff(sample_ts, dim=0).to(dt_dtype or I.dtype).to(I.dtype)
     A, B, C = _system(I[1:], prm, with_sf)
     Ad, Bd, Btd = foh_discretise(A, B, dt)
     S = I.shape[0]
@@ -111,8 +113,9 @@ def weights(I, sample_ts, prm, with_sf):
 class PixelBandwidthOracle:
     """Stateful wrapper mirroring PixelBandwidth.forward's reset semantics."""
 
-    def __init__(self, prm, min_ts, f_c_dominant_min=21.0, max_cumprob=0.95):
+    def __init__(self, prm, min_ts, f_c_dominant_min=21.0, max_cumprob=0.95, dt_dtype=None):
         self.prm = prm
+        self.dt_dtype = dt_dtype
         self.min_ts = min_ts
         self.omega_c_min = 2 * math.pi * f_c_dominant_min
         self.max_cumprob = max_cumprob
@@ -123,13 +126,13 @@ class PixelBandwidthOracle:
         with torch.no_grad():
             sts = sample_timestamps(gen, output_ts, self.omega_c_min, self.max_cumprob)
         I = intensity_fn(torch.clamp(sts, min=float(self.min_ts)))
-        w = weights(I, sts, self.prm, with_sf=reset_diff)
+        w = weights(I, sts, self.prm, with_sf=reset_diff, dt_dtype=self.dt_dtype)
         wn = w / w.sum(dim=0, keepdim=True)
         y = (wn * torch.log(I)[..., None]).sum(dim=0)
         if reset_diff:
             self.reset_delta_log_it = y[..., 1] - y[..., 0]
             self.reset_ts = output_ts
             return y[..., 0]
-        dt = (output_ts - self.reset_ts).to(y.dtype)
+        dt = (output_ts - self.reset_ts).to(self.dt_dtype or y.dtype).to(y.dtype)
         assert torch.all(dt >= 0)
         return y[..., 0] - self.reset_delta_log_it * torch.exp(-(1 / self.prm["tau_diff"]) * (NS_TO_S * dt))
