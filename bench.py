@@ -44,7 +44,33 @@ def parse():
     return ap.parse_args()
 
 
-def phase_times(ts, reps=3):
+PHASE_REPS = 3
+# algorithmic HBM bytes per sample and STEP of each render-path kernel class, BF16 layout
+# (DESIGN.md section 4): hidden_bwd: 7 launches (L7..L1), each reading dz_l + a_(l-1) and writing
+# dz_(l-1), 256 bf16 each = 1536 B; render_fwd: the activations + record it stores for the
+# backward; render_bwd: head activations read + dz written; dw_gemm: the dz/x operand streams of the
+# split-K GEMMs of L0, L5-pe, Lb, sigma, Lg, Lr.  Per launch = per step / launches per step.
+BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "render_fwd_kernel": 5072, "render_bwd_kernel": 2192,
+                    "dw_gemm_kernel": 4032}
+
+
+def pmc_traffic(kernel, a):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc pass
+    (profiles/pmc_traffic.json, FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE),
+    only when it was taken on this exact workload; else None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        w = t["workload"]
+        if (w["rays"], w["samples"], w["mode"], w["rd"]) != (a.rays, a.samples, a.mode, a.rd):
+            return None
+        return t["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def phase_times(ts, reps=PHASE_REPS):
     """Average duration of each phase, measured with HIP events on the stream
     the kernels are launched on (torch's current stream)."""
     import ctypes
@@ -85,8 +111,8 @@ def cpu_baseline(n_rays, n_samples, rd, threads):
     """The oracle (PyTorch-CPU restatement of the reference path) timed on a
     bounded sample: n_rays rays through render fwd + event loss + backward +
     Adam (the same step as the GPU line, fewer rays)."""
-    from oracle import loss as oloss
     from oracle import nerf as onerf
+    from oracle.train import step_loss
     from deblur_e_nerf.train import synthetic_batch
     torch.set_num_threads(threads)
     N = n_rays // 4
@@ -97,21 +123,16 @@ def cpu_baseline(n_rays, n_samples, rd, threads):
         t.requires_grad_(True)
     bk = torch.tensor([0.5413] * rd, requires_grad=True)
     opt = torch.optim.Adam([{"params": params, "weight_decay": 1e-6}, {"params": [bk]}], lr=0.01)
-    c = torch.tensor(0.25)
 
     def step():
         opt.zero_grad()
-        bkgd = torch.nn.functional.softplus(bk)
-        col, op, _, _ = onerf.render_rays(p, b["rays_o"], b["rays_d"], b["jitter"], n_samples=n_samples, bkgd=bkgd)
-        y = torch.log(col[:, 0] + 1e-3).view(4, N)
-        Ld, Lt = oloss.event_loss(b["lid"], b["end_ts"], b["start_ts"], y[1] - y[0], b["ts_diff"],
-                                  torch.ones(N, dtype=torch.bool), y[3] - y[2], torch.ones(N, dtype=torch.bool), c)
-        (Ld + 1e-3 * Lt).backward()
+        total, _, _ = step_loss(p, torch.nn.functional.softplus(bk), b, n_samples)
+        total.backward()
         opt.step()
 
     step()  # warm-up
     t0 = time.perf_counter()
-    reps = 2
+    reps = 4
     for _ in range(reps):
         step()
     dt = (time.perf_counter() - t0) / reps
@@ -131,6 +152,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    from deblur_e_nerf import _native as nat
     from deblur_e_nerf.train import TrainStep, synthetic_batch
 
     assert a.rays % (4 * world) == 0
@@ -159,19 +181,38 @@ def main():
     rays_per_step = a.rays
     value = rays_per_step * a.steps / elapsed
 
+    nat.timing_enable(True)
     phases = phase_times(ts)
+    nat.timing_enable(False)
+    kt = nat.timing_collect()
     n_local = ts.R * ts.S
-    flop_fwd = 2.0 * MAC_PER_SAMPLE[a.rd] * n_local
-    fwd_ms = phases["render_fwd"]
-    achieved = flop_fwd / (fwd_ms * 1e-3) / 1e12
-    step_flop = 3.0 * flop_fwd
-    roofline = {"bound": "mfma", "kernel": "render_fwd_kernel (fused sampler+encoding+MLP fwd+compositing)",
-                "achieved": round(achieved, 2), "peak": PEAK_TFLOPS[a.mode], "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_TFLOPS[a.mode], 4), "traffic": None,
-                "flop_per_launch": flop_fwd, "kernel_ms": round(fwd_ms, 3),
-                # whole train step (fwd + 2x bwd algorithmic FLOPs of this rank) vs the peak of one GPU
-                "step_frac": round(step_flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.mode], 4),
-                "phases_ms": {k: round(v, 3) for k, v in phases.items()}}
+    kernels = {}
+    for k, (tot, cnt) in kt.items():
+        if cnt == 0:
+            continue
+        avg = tot / cnt
+        e = {"launches_per_step": cnt // PHASE_REPS, "avg_ms": round(avg, 4),
+             "step_ms": round(tot / PHASE_REPS, 3)}
+        if k in BYTES_PER_SAMPLE and a.mode == "bf16":
+            b = BYTES_PER_SAMPLE[k] * n_local * PHASE_REPS / cnt  # algorithmic bytes per launch
+            e.update(bytes_per_launch=b, gbs=round(b / (avg * 1e-3) / 1e9, 1))
+        if k == "render_fwd_kernel":
+            f = 2.0 * MAC_PER_SAMPLE[a.rd] * n_local
+            e.update(flop_per_launch=f, tflops=round(f / (avg * 1e-3) / 1e12, 1))
+        kernels[k] = e
+    dom = max(kernels, key=lambda k: kernels[k]["step_ms"])  # the kernel that takes most of the step
+    de = kernels[dom]
+    if dom == "render_fwd_kernel":
+        roofline = {"bound": "mfma", "achieved": de["tflops"], "peak": PEAK_TFLOPS[a.mode], "unit": "TFLOP/s"}
+    else:
+        roofline = {"bound": "hbm", "achieved": de["gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s"}
+    roofline["frac"] = round(roofline["achieved"] / roofline["peak"], 4)
+    roofline["traffic"] = pmc_traffic(dom, a)
+    roofline.update(kernel=dom, avg_launch_ms=de["avg_ms"], timing="hipEvents on the launch stream (den_timing_*)")
+    step_flop = 3.0 * 2.0 * MAC_PER_SAMPLE[a.rd] * n_local
+    roofline["step_mfma_frac"] = round(step_flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.mode], 4)
+    roofline["kernels"] = kernels
+    roofline["phases_ms"] = {k: round(v, 3) for k, v in phases.items()}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

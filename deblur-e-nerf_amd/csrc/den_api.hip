@@ -7,7 +7,9 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/den_api.h"
 #include "den_dw.hip"
@@ -35,6 +37,36 @@ int fail(int code, const std::string& msg) {
     hipError_t e_ = hipGetLastError();                                                    \
     if (e_ != hipSuccess) return fail(DEN_EHIP, std::string("launch: ") + hipGetErrorString(e_)); \
   } while (0)
+
+// ---- kernel timing (measurement only; bench.py).  When enabled, each render-path launch is
+// bracketed by a pair of hipEvents recorded on the launch stream itself.
+enum { T_RENDER_FWD = 0, T_RENDER_BWD = 1, T_HIDDEN_BWD = 2, T_DW_GEMM = 3, T_DW_REDUCE = 4, T_NCLASS = 5 };
+struct TimingRec {
+  int cls;
+  hipEvent_t a, b;
+};
+bool g_timing = false;
+std::mutex g_timing_mu;
+std::vector<TimingRec> g_timing_recs;
+
+struct TimedLaunch {
+  TimingRec r{};
+  hipStream_t s;
+  bool on;
+  TimedLaunch(int cls, hipStream_t st) : s(st), on(g_timing) {
+    if (!on) return;
+    r.cls = cls;
+    on = hipEventCreate(&r.a) == hipSuccess && hipEventCreate(&r.b) == hipSuccess &&
+         hipEventRecord(r.a, s) == hipSuccess;
+  }
+  ~TimedLaunch() {
+    if (!on) return;
+    (void)hipEventRecord(r.b, s);
+    std::lock_guard<std::mutex> g(g_timing_mu);
+    g_timing_recs.push_back(r);
+  }
+};
+#define DEN_TIMED(cls, s) TimedLaunch timed_##cls##_(cls, s)
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -141,7 +173,10 @@ int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, 
   P.n = (int64_t)d->n_rays * d->n_samples;
   P.per_split = L.per_split;
   P.partial = (float*)(ws + L.dw_partial);
-  hipLaunchKernelGGL((dw_gemm_kernel<MODE, MT, N1, N2>), dim3(L.splits), dim3(64 * MT), 0, s, P);
+  {
+    DEN_TIMED(T_DW_GEMM, s);
+    hipLaunchKernelGGL((dw_gemm_kernel<MODE, MT, N1, N2>), dim3(L.splits), dim3(64 * MT), 0, s, P);
+  }
   DEN_LAUNCHED();
   DwReduceArgs R{};
   R.partial = P.partial;
@@ -157,7 +192,10 @@ int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, 
   R.bias = bias;
   R.grad = grad;
   const int64_t per = (int64_t)MT * (R.NT + 1) * 1024;
-  hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
+  {
+    DEN_TIMED(T_DW_REDUCE, s);
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
+  }
   DEN_LAUNCHED();
   return DEN_OK;
 }
@@ -175,7 +213,10 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   H.n_blocks = n / 32;
   const int64_t grid = hidden_grid(n);
   H.per_wg = (H.n_blocks + grid - 1) / grid;
-  hipLaunchKernelGGL(hidden_bwd_kernel, dim3((unsigned)grid), dim3(HB_THREADS), 0, s, H);
+  {
+    DEN_TIMED(T_HIDDEN_BWD, s);
+    hipLaunchKernelGGL(hidden_bwd_kernel, dim3((unsigned)grid), dim3(HB_THREADS), 0, s, H);
+  }
   DEN_LAUNCHED();
   DwReduceArgs R{};
   R.partial = H.partial;
@@ -191,7 +232,10 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   R.bias = 1;
   R.grad = grad;
   const int64_t per = 8LL * 9 * 1024;
-  hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
+  {
+    DEN_TIMED(T_DW_REDUCE, s);
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
+  }
   DEN_LAUNCHED();
   return DEN_OK;
 }
@@ -202,7 +246,10 @@ int render_fwd_impl(const den_render_desc* d, const den_render_io* io, hipStream
   RenderArgs<MODE> A = make_args<MODE>(d, io, L);
   A.w = (const char*)io->w_fwd;
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
-  hipLaunchKernelGGL(render_fwd_kernel<MODE>, dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s, A);
+  {
+    DEN_TIMED(T_RENDER_FWD, s);
+    hipLaunchKernelGGL(render_fwd_kernel<MODE>, dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s, A);
+  }
   DEN_LAUNCHED();
   return DEN_OK;
 }
@@ -225,13 +272,18 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
     if constexpr (MODE == DEN_MODE_BF16) {
       if (hidden) {
         // head (compositing adjoint, Lr^T, Lg^T, Lb^T) sample-major, then L7..L1 layer-major
-        hipLaunchKernelGGL((render_bwd_kernel<MODE, 2>), dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s, A);
+        {
+          DEN_TIMED(T_RENDER_BWD, s);
+          hipLaunchKernelGGL((render_bwd_kernel<MODE, 2>), dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s,
+                             A);
+        }
         DEN_LAUNCHED();
         for (int l = 7; l >= 1; --l)
           if ((rc = launch_hidden(d, io, L, ws, l, G, s)) != DEN_OK) return rc;
       }
     }
     if (!hidden) {
+      DEN_TIMED(T_RENDER_BWD, s);
       hipLaunchKernelGGL((render_bwd_kernel<MODE, NBL - 1>), dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s,
                          A);
       DEN_LAUNCHED();
@@ -269,6 +321,33 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
 extern "C" {
 
 int den_version(void) { return DEN_VERSION; }
+
+int den_timing_enable(int32_t on) {
+  std::lock_guard<std::mutex> g(g_timing_mu);
+  g_timing = on != 0;
+  return DEN_OK;
+}
+
+int den_timing_collect(int32_t n_classes, double* total_ms, int64_t* launches) {
+  if (n_classes < 0 || (n_classes > 0 && (!total_ms || !launches))) return fail(DEN_EINVAL, "bad timing buffers");
+  std::vector<TimingRec> recs;
+  {
+    std::lock_guard<std::mutex> g(g_timing_mu);
+    recs.swap(g_timing_recs);
+  }
+  for (int c = 0; c < n_classes; ++c) total_ms[c] = 0.0, launches[c] = 0;
+  int rc = DEN_OK;
+  for (auto& r : recs) {
+    float ms = 0.f;
+    if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess)
+      rc = fail(DEN_EHIP, "timing event failed");
+    else if (r.cls < n_classes)
+      total_ms[r.cls] += ms, launches[r.cls] += 1;
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  return rc;
+}
 const char* den_last_error(void) { return g_err.c_str(); }
 
 int64_t den_param_count(int32_t rd) { return (rd == 1 || rd == 3) ? param_count(rd) : -1; }

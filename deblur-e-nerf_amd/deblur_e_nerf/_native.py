@@ -44,6 +44,8 @@ _lib = None
 _SIGS = {
     "den_version": (ctypes.c_int, []),
     "den_last_error": (ctypes.c_char_p, []),
+    "den_timing_enable": (ctypes.c_int, [ctypes.c_int32]),
+    "den_timing_collect": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     "den_param_count": (ctypes.c_int64, [ctypes.c_int32]),
     "den_param_offset": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     "den_packed_fwd_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
@@ -94,6 +96,23 @@ def lib():
 
 def exported_symbols():
     return sorted(_SIGS)
+
+
+TIMING_CLASSES = ("render_fwd_kernel", "render_bwd_kernel", "hidden_bwd_kernel", "dw_gemm_kernel",
+                  "dw_reduce_kernel")
+
+
+def timing_enable(on=True):
+    _check(lib().den_timing_enable(int(on)))
+
+
+def timing_collect():
+    """-> {kernel: (total_ms, launches)} since the last collect (den_timing_collect)."""
+    n = len(TIMING_CLASSES)
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_int64 * n)()
+    _check(lib().den_timing_collect(n, ms, cnt))
+    return {k: (ms[i], cnt[i]) for i, k in enumerate(TIMING_CLASSES)}
 
 
 def _check(rc):

@@ -26,6 +26,16 @@ from .external import mlp, ngp
 ERR = nat.ERROR_FNS
 
 
+def allreduce_mean(buf):
+    """DDP gradient semantics (scripts/run.py:84-89): the mean over ranks of the
+    per-rank gradients, one collective on one flat buffer (RCCL on the GPU box,
+    gloo in the CPU tests).  No-op for a single process."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+        buf.div_(dist.get_world_size())
+    return buf
+
+
 class TrainStep:
     def __init__(self, n_events, n_samples=128, radiance_dim=1, mode="bf16", seed=0, device="cuda",
                  aabb=(-1.5, -1.5, -1.5, 1.5, 1.5, 1.5), near=1.43, far=6.63, lr=0.01, weight_decay=1e-6,
@@ -109,9 +119,7 @@ class TrainStep:
         nat._check(nat.lib().den_render_bwd(ctypes.byref(self.desc), ctypes.byref(self.io), ctypes.byref(gr), st))
 
     def allreduce(self):
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_reduce(self.gbuf, op=dist.ReduceOp.SUM)
-            self.gbuf.div_(dist.get_world_size())
+        allreduce_mean(self.gbuf)
 
     def optimizer_step(self):
         self.t += 1

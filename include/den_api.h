@@ -111,6 +111,15 @@ typedef struct den_render_grad {
 int den_version(void);
 const char* den_last_error(void);
 
+/* Kernel timing, for measurement only (bench.py's roofline).  While enabled,
+ * every render-path launch is bracketed by two hipEvents recorded on its own
+ * stream.  den_timing_collect waits for them and returns, per kernel class
+ * (0 render_fwd_kernel, 1 render_bwd_kernel, 2 hidden_bwd_kernel,
+ * 3 dw_gemm_kernel, 4 dw_reduce_kernel), the summed duration in ms and the
+ * launch count since the last collect.  No reference counterpart. */
+int den_timing_enable(int32_t on);
+int den_timing_collect(int32_t n_classes, double* total_ms, int64_t* launches);
+
 /* Number of f32 parameters of the MLP (595,844 for rd=3) and the offset of the
  * tensor `idx` in the flat buffer, in the reference's named_parameters() order:
  * base.hidden_layers.{0..7}.{weight,bias}, sigma_layer.output_layer.{w,b},

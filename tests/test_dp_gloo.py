@@ -1,0 +1,93 @@
+"""Data-parallel semantics of the train step, world_size 2 over gloo on CPU.
+
+The GPU path shards the events of one step over the ranks
+(`synthetic_batch(rank, world)`), computes per-rank gradients and averages them
+with ONE all-reduce of the flat gradient buffer (`train.allreduce_mean`, RCCL
+on the GPU box).  Here the per-rank gradient comes from the CPU oracle; the
+collective and the sharding are the product's own code.  With every event valid
+(render background parameter on), the mean of the per-shard means equals the
+full-batch gradient (the reference's DDP semantics, scripts/run.py:84-89).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from _util import unflat
+
+RD, S, N_PER_RANK, WORLD = 1, 32, 6, 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _params():
+    from oracle import nerf as onerf
+    return onerf.build_params(RD, 0, dtype=torch.float64)
+
+
+def _f64(b):
+    # f64 end to end, so the identity is checked to rounding (1e-12), not to f32 noise
+    return {k: (v.double() if v.is_floating_point() else v) for k, v in b.items()}
+
+
+def _worker(rank, world, port, out):
+    import sys
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deblur_e_nerf.train import allreduce_mean, synthetic_batch
+    from oracle.train import flat_grad
+    b = _f64(synthetic_batch(N_PER_RANK, rank=rank, world=world))
+    g, losses = flat_grad(_params(), torch.zeros(RD, dtype=torch.float64), b, S, RD)
+    allreduce_mean(g)
+    out[rank] = (g, torch.tensor(losses, dtype=torch.float64), b["end_ts"].clone())
+    dist.destroy_process_group()
+
+
+def test_sharding_partitions_the_global_batch():
+    from deblur_e_nerf.train import synthetic_batch
+    full = synthetic_batch(N_PER_RANK * WORLD)
+    parts = [synthetic_batch(N_PER_RANK, rank=r, world=WORLD) for r in range(WORLD)]
+    N = N_PER_RANK * WORLD
+    for k in ("lid", "end_ts", "start_ts", "ts_diff"):
+        assert torch.equal(torch.cat([p[k] for p in parts]), full[k])
+    for k in ("rays_o", "rays_d", "jitter"):
+        f = full[k].reshape(4, N, -1)
+        cat = torch.cat([p[k].reshape(4, N_PER_RANK, -1) for p in parts], dim=1)
+        assert torch.equal(cat, f), k
+
+
+@pytest.mark.timeout(300)
+def test_allreduce_mean_equals_full_batch_gradient():
+    from deblur_e_nerf.train import synthetic_batch
+    from oracle.train import flat_grad
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(WORLD, port, out), nprocs=WORLD, join=True)
+    g0, l0, e0 = out[0]
+    g1, l1, e1 = out[1]
+    assert not torch.equal(e0, e1)           # ranks saw different events
+    assert torch.equal(g0, g1)               # identical averaged gradient on every rank
+    full = _f64(synthetic_batch(N_PER_RANK * WORLD))
+    g_full, losses = flat_grad(_params(), torch.zeros(RD, dtype=torch.float64), full, S, RD)
+    rel = float((g0 - g_full).norm() / g_full.norm())
+    assert rel < 1e-12, rel
+    # per-layer check too (the small heads must not be swamped by the trunk)
+    a, b = unflat(g0[:-RD], RD), unflat(g_full[:-RD], RD)
+    for k in a:
+        assert float((a[k] - b[k]).norm()) <= 1e-11 * float(b[k].norm()) + 1e-20, k
+    assert torch.allclose(g0[-RD:], g_full[-RD:], rtol=1e-11, atol=1e-20)
+    # the mean of the per-rank losses is the full-batch loss
+    assert torch.allclose((l0 + l1) / 2, torch.tensor(losses, dtype=torch.float64), rtol=1e-12)
