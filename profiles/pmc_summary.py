@@ -1,0 +1,80 @@
+"""Summarise rocprofv3 output of profiles/gpu_round.sh into committed evidence.
+
+    python profiles/pmc_summary.py gpurun_out <round tag>
+
+* profiles/pmc_traffic.json -- HBM bytes per launch of each render-path kernel
+  from the separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes, corrected
+  as MI355X_MICROARCH.md prescribes for gfx950 (FETCH_SIZE counts half the
+  bytes of wide coalesced streaming reads: x2; both counters are in KiB).
+  bench.py reads it for `roofline.traffic` when the workload matches.
+* profiles/<tag>_kernel_stats.md -- the `--kernel-trace --stats` table.
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNELS = ("render_fwd_kernel", "render_bwd_kernel", "hidden_bwd_kernel", "dw_gemm_kernel", "dw_reduce_kernel",
+           "pack_kernel", "adam_kernel")
+
+
+def short(name):
+    for k in KERNELS:
+        if k in name:
+            return k
+    return None
+
+
+def per_launch(path, counter):
+    acc = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != counter:
+                continue
+            k = short(row["Kernel_Name"])
+            if k:
+                acc[k].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main(out_dir, tag):
+    here = os.path.dirname(os.path.abspath(__file__))
+    fetch = per_launch(os.path.join(out_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_launch(os.path.join(out_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    kern = {}
+    for k in sorted(set(fetch) & set(write)):
+        rd, wr = 2.0 * fetch[k] * 1024, write[k] * 1024
+        kern[k] = {"fetch_size_kib": round(fetch[k], 1), "write_size_kib": round(write[k], 1),
+                   "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                   "hbm_bytes_per_launch": rd + wr}
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes ({tag}); "
+                     "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes",
+           "command": "bench.py --steps 1 --warmup 1 --no-cpu-baseline (profiles/gpu_round.sh)",
+           "workload": {"rays": 131072, "samples": 128, "mode": "bf16", "rd": 1},
+           "kernels": kern}
+    with open(os.path.join(here, "pmc_traffic.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    rows = []
+    with open(os.path.join(out_dir, "prof", "run_kernel_stats.csv")) as f:
+        for r in csv.DictReader(f):
+            rows.append(r)
+    lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
+             "Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python bench.py --steps 5 --warmup 2 "
+             "--no-cpu-baseline` (profiles/gpu_round.sh); 7 train steps + 3 phase-timing reps per kernel.", "",
+             "| kernel | calls | avg ms | total % |", "|---|---|---|---|"]
+    for r in rows[:20]:
+        lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | "
+                     f"{float(r['Percentage']):.2f} |")
+    lines += ["", "HBM traffic per launch (separate PMC passes, profiles/pmc_traffic.json):", "",
+              "| kernel | read GB | write GB | total GB |", "|---|---|---|---|"]
+    for k, v in kern.items():
+        lines.append(f"| `{k}` | {v['hbm_read_bytes_per_launch'] / 1e9:.2f} | "
+                     f"{v['hbm_write_bytes_per_launch'] / 1e9:.2f} | {v['hbm_bytes_per_launch'] / 1e9:.2f} |")
+    with open(os.path.join(here, f"{tag}_kernel_stats.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print(json.dumps(kern, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
