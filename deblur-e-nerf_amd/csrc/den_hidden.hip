@@ -9,7 +9,7 @@
 //           (k = samples: both operands by ds_read_b64_tr_b16 from the same LDS blocks; the bias from
 //           VALU sums of the dz operand), accumulated in registers over the whole range, written once as a
 //           split-K partial for dw_reduce_kernel (den_dw.hip layout, MT = NT = 8).
-// dz_l and S'_{l-1} (16 KiB per block each) arrive by LDS-DMA one block ahead.  Per sample and layer
+// dz_l and S'_{l-1} (16 KiB per block each) arrive by LDS-DMA HB_DEPTH = 3 blocks ahead (96 KiB in flight per CU).  Per sample and layer
 // this moves 1.5 KiB of HBM (read dz_l and S'_{l-1}, write dz_{l-1}) where the sample-major chain
 // plus the split-K GEMM (den_render.hip + den_dw.hip; kept for the F32 parity mode) move 3 KiB.
 //
@@ -25,6 +25,15 @@ constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
 constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
 constexpr int HB_SLOT = 2 * HB_BLOCK;  // LDS ring slot: [dz_l block | S'_{l-1} block]
 constexpr int HB_GRID_MAX = 256;
+constexpr int HB_DEPTH = 3;                              // blocks in flight ahead of the computed one
+constexpr int HB_RING = HB_DEPTH + 1;                    // LDS slots (4 x 32 KiB)
+static_assert((HB_RING & (HB_RING - 1)) == 0, "ring index by mask");
+constexpr int HB_DMA_OPS = 2 * (16 / 4);                 // LDS-DMA instructions per wave per block
+constexpr int HB_STORE_OPS = 4;                          // dz_{l-1} stores per wave per block
+// vector-memory ops a wave issues after its DMA of block b+1 by the end of block b (issue order:
+// stores(b-2), DMA(b+2), stores(b-1), DMA(b+3), stores(b)); the asm DMAs clobber "memory", so the
+// stores keep their program order around them
+constexpr int HB_YOUNGER = HB_STORE_OPS + (HB_DEPTH - 1) * (HB_DMA_OPS + HB_STORE_OPS);
 
 typedef short hb_v4i16 __attribute__((ext_vector_type(4)));
 
@@ -59,6 +68,26 @@ __device__ __forceinline__ void hb_dma(const char* src, char* dst) {
   }
 }
 
+// The same DMA issued through inline asm: the compiler then does not track it, so it does not make
+// every LDS read wait vmcnt(0) for the prefetches in flight (it cannot tell the ring slots apart);
+// hidden_bwd_kernel waits for them explicitly (hb_wait_vm_lgkm0 + barrier).  The "memory" clobber
+// keeps LDS reads and global stores in program order around it.
+__device__ __forceinline__ void hb_dma_untracked(const char* src, char* dst) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // per-lane 32-bit offsets (two: the slot permutation depends on the fragment parity); the 64-bit
+  // base stays in SGPRs (saddr form), so the ring needs no per-instruction VGPR address pairs
+  const uint32_t off0 = (uint32_t)hb_slot(lane, 0) * 16, off1 = (uint32_t)hb_slot(lane, 1) * 16;
+#pragma unroll
+  for (int q = 0; q < 16 / HB_WAVES; ++q) {
+    // wave-uniform piece index (readfirstlane is 32-bit: never pass it a 64-bit pointer)
+    const int pc = __builtin_amdgcn_readfirstlane(q * HB_WAVES + wave);
+    const char* base = src + pc * 1024;
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(dst + pc * 1024));
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"((pc & 1) ? off1 : off0),
+                 "s"(base), "s"(m0) : "memory", "m0");
+  }
+}
+
 // This lane's own fragment f of a tile in LDS (the chain's B operand / the stored activation).
 __device__ __forceinline__ bf16x8 hb_frag(const char* tile, int f) {
   return *(const bf16x8*)(tile + f * 1024 + hb_slot(threadIdx.x & 63, f) * 16);
@@ -82,16 +111,82 @@ __device__ __forceinline__ bf16x8 hb_tr_frag(const char* tile, int kk) {
   return out;
 }
 
+// s_waitcnt vmcnt(VM) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14;
+// expcnt left at its maximum).
+template <int VM>
+__device__ __forceinline__ void hb_wait_vm_lgkm0() {
+  static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | ((VM >> 4) << 14));
+}
+
+// One 32-sample block from its LDS slot: the chain (dz_{l-1} stored), then the dW / db accumulation.
+__device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, int64_t b, const bf16x8 (&wt)[2][16],
+                                         f32x16 (&dw)[2][8], float (&db)[2]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const char* dzb = cur;
+  const char* sb = cur + HB_BLOCK;
+  // chain: two row tiles, K = 256 (16 k-steps); then the activation derivative
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[t][k], hb_frag(dzb + (k >> 1) * HB_TILE, k & 1), acc, 0, 0,
+                                                     0);
+    const char* st = sb + (2 * wave + t) * HB_TILE;
+    const bf16x8 s0 = hb_frag(st, 0), s1 = hb_frag(st, 1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float sv = (float)(r < 8 ? s0[r] : s1[r - 8]);
+      acc[r] = acc[r] * dsoftplus2_scaled_from_out(sv);
+    }
+    // dz_{l-1} tile: stored now, the weight-gradient MFMAs below cover its write latency
+    bf16x8 of[2];
+    acc_to_frags<1>(acc, of);
+    char* d = P.dz_out + (b * 8 + 2 * wave + t) * HB_TILE + lane * 16;
+    *(bf16x8*)d = of[0];
+    *(bf16x8*)(d + 1024) = of[1];
+    // keep the scheduler from hoisting the next phase's LDS reads here (register pressure: W^T lives
+    // in 128 VGPRs and dW in all 256 AGPRs for the whole launch)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // weight / bias gradients over the block's 32 samples (two k-steps of 16)
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const bf16x8 a0 = hb_tr_frag(dzb + (2 * wave) * HB_TILE, kk);
+    const bf16x8 a1 = hb_tr_frag(dzb + (2 * wave + 1) * HB_TILE, kk);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const bf16x8 bb = hb_tr_frag(sb + n * HB_TILE, kk);
+      dw[0][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bb, dw[0][n], 0, 0, 0);
+      dw[1][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bb, dw[1][n], 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      db[0] += (float)a0[j];
+      db[1] += (float)a1[j];
+    }
+  }
+}
+
 __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * HB_SLOT];
+  // HB_RING LDS slots of [dz_l block | S'_{l-1} block]; HB_DEPTH blocks in flight ahead of the one
+  // being computed.  Each wave waits for its own part of block b+1 at the end of block b (vmcnt; the
+  // younger prefetches and stores stay in flight), then the workgroup barrier publishes every part.
+  __shared__ __attribute__((aligned(16))) char lds[HB_RING * HB_SLOT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t b0 = (int64_t)blockIdx.x * P.per_wg;
   const int64_t b1 = b0 + P.per_wg < P.n_blocks ? b0 + P.per_wg : P.n_blocks;
+  auto fetch = [&](int64_t b, char* dst) {
+    hb_dma_untracked(P.dz_in + b * HB_BLOCK, dst);
+    hb_dma_untracked(P.s_in + b * HB_BLOCK, dst + HB_BLOCK);
+  };
+#pragma unroll
+  for (int u = 0; u < HB_DEPTH; ++u)
+    if (b0 + u < b1) fetch(b0 + u, lds + u * HB_SLOT);
 
-  if (b0 < b1) {
-    hb_dma(P.dz_in + b0 * HB_BLOCK, lds);
-    hb_dma(P.s_in + b0 * HB_BLOCK, lds + HB_BLOCK);
-  }
   // W_l^T row tiles 2w, 2w+1: packed [row tile][kappa][lane][8] = the chain's A fragments
   bf16x8 wt[2][16];
 #pragma unroll
@@ -107,59 +202,21 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dw[t][n][r] = 0.0f;
   float db[2] = {0.0f, 0.0f};  // bias partial: feature (lane & 31) of row tile 2w + t, this lane's samples
-  __syncthreads();
+  hb_wait_vm_lgkm0<0>();       // block b0 (and the prologue prefetches) landed
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 
   for (int64_t b = b0; b < b1; ++b) {
-    const char* cur = lds + (int)((b - b0) & 1) * HB_SLOT;
-    char* nxt = lds + (int)((b - b0 + 1) & 1) * HB_SLOT;
-    if (b + 1 < b1) {
-      hb_dma(P.dz_in + (b + 1) * HB_BLOCK, nxt);
-      hb_dma(P.s_in + (b + 1) * HB_BLOCK, nxt + HB_BLOCK);
-    }
-    const char* dzb = cur;
-    const char* sb = cur + HB_BLOCK;
-    // chain: two row tiles, K = 256 (16 k-steps); then the activation derivative
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[t][k], hb_frag(dzb + (k >> 1) * HB_TILE, k & 1), acc, 0,
-                                                       0, 0);
-      const char* st = sb + (2 * wave + t) * HB_TILE;
-      const bf16x8 s0 = hb_frag(st, 0), s1 = hb_frag(st, 1);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float sv = (float)(r < 8 ? s0[r] : s1[r - 8]);
-        acc[r] = acc[r] * dsoftplus2_scaled_from_out(sv);
-      }
-      // dz_{l-1} tile: stored now, the weight-gradient MFMAs below cover its write latency
-      bf16x8 of[2];
-      acc_to_frags<1>(acc, of);
-      char* d = P.dz_out + (b * 8 + 2 * wave + t) * HB_TILE + lane * 16;
-      *(bf16x8*)d = of[0];
-      *(bf16x8*)(d + 1024) = of[1];
-    }
-    // weight / bias gradients over the block's 32 samples (two k-steps of 16)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 a0 = hb_tr_frag(dzb + (2 * wave) * HB_TILE, kk);
-      const bf16x8 a1 = hb_tr_frag(dzb + (2 * wave + 1) * HB_TILE, kk);
-#pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        const bf16x8 bb = hb_tr_frag(sb + n * HB_TILE, kk);
-        dw[0][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bb, dw[0][n], 0, 0, 0);
-        dw[1][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bb, dw[1][n], 0, 0, 0);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        db[0] += (float)a0[j];
-        db[1] += (float)a1[j];
-      }
-    }
-    __syncthreads();
+    const int u = (int)((b - b0) & (HB_RING - 1));
+    // prefetch block b + HB_DEPTH into the slot block b - 1 used (free since the last barrier)
+    if (b + HB_DEPTH < b1) fetch(b + HB_DEPTH, lds + ((u + HB_DEPTH) & (HB_RING - 1)) * HB_SLOT);
+    hb_block(P, lds + u * HB_SLOT, b, wt, dw, db);
+    if (b + HB_DEPTH < b1) hb_wait_vm_lgkm0<HB_YOUNGER>();
+    else hb_wait_vm_lgkm0<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
   // split-K partial of this workgroup (dw_gemm_kernel layout: [wg][mt][nt][lane][16]); the bias
   // goes where that layout's ones tile (nt = 8) keeps it: column 0 = lanes 0 and 32, row m in
