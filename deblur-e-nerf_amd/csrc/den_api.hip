@@ -77,7 +77,7 @@ struct WsLayout {
   int64_t per_split;
 };
 
-constexpr int64_t DW_BLOCK_MAX = 8LL * 11 * 1024;  // floats per split for the largest layer (L5: MT 8, NT+1 11)
+constexpr int64_t DW_BLOCK_MAX = 9LL * 11 * 1024;  // floats per split, bound over the shapes (L5: MT 8, NT+1 11; Lb: MT 9, NT+1 9)
 
 // persistent workgroups of the layer-major hidden backward: one per CU, at most one per wave block
 inline int64_t hidden_grid(int64_t n_samples) { return std::min<int64_t>(HB_GRID_MAX, std::max<int64_t>(1, n_samples / 32)); }
@@ -161,7 +161,7 @@ RenderArgs<MODE> make_args(const den_render_desc* d, const den_render_io* io, co
 // Split-K weight-gradient GEMM of one layer + its reduction into the flat gradient.
 // red_n1 < 0: columns [0, N1) are the first input segment; red_n1 = 0 maps every column to the
 // second segment at chain feature n1_feat (the pe columns of L5).  bias = 0 skips the bias.
-template <int MODE, int MT, int N1, int N2>
+template <int MODE, int MT, int N1, int N2, int WN = 1>
 int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, int a_dz, int a_x1, int a_x2,
               int n1_feat, float* grad, hipStream_t s, int m_off = 0, int red_n1 = -1, int bias = 1) {
   DwArgs P{};
@@ -175,7 +175,7 @@ int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, 
   P.partial = (float*)(ws + L.dw_partial);
   {
     DEN_TIMED(T_DW_GEMM, s);
-    hipLaunchKernelGGL((dw_gemm_kernel<MODE, MT, N1, N2>), dim3(L.splits), dim3(64 * MT), 0, s, P);
+    hipLaunchKernelGGL((dw_gemm_kernel<MODE, MT, N1, N2, WN>), dim3(L.splits), dim3(64 * MT * WN), 0, s, P);
   }
   DEN_LAUNCHED();
   DwReduceArgs R{};
@@ -303,11 +303,13 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
     if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 6, D_Z0 + 6, A_S0 + 5, -1, 0, G, s)) != DEN_OK) return rc;
     if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, 7, D_Z0 + 7, A_S0 + 6, -1, 0, G, s)) != DEN_OK) return rc;
   }
-  // [bottleneck | sigma]: the 256 bottleneck rows, then the sigma tile (row 256)
+  // [bottleneck | sigma]: the 256 bottleneck rows, then the sigma tile (row 256) with 4 waves splitting
+  // its 8 column tiles (one 9-wave launch would spill: 9 accumulator tiles at 3 waves per SIMD)
   if ((rc = launch_dw<MODE, 8, 256, 0>(d, L, ws, L_B, D_ZB, A_S0 + 7, -1, 0, G, s)) != DEN_OK) return rc;
-  if ((rc = launch_dw<MODE, 1, 256, 0>(d, L, ws, L_B, D_ZB, A_S0 + 7, -1, 0, G, s, WIDTH)) != DEN_OK) return rc;
+  if ((rc = launch_dw<MODE, 1, 256, 0, 4>(d, L, ws, L_B, D_ZB, A_S0 + 7, -1, 0, G, s, WIDTH)) != DEN_OK) return rc;
   if ((rc = launch_dw<MODE, 4, 256, 32>(d, L, ws, L_G, D_ZG, A_BT, A_VE, WIDTH, G, s)) != DEN_OK) return rc;
-  if ((rc = launch_dw<MODE, 1, 128, 0>(d, L, ws, L_R, D_ZR, A_G, -1, 0, G, s)) != DEN_OK) return rc;
+  // rgb output (M = 32): 4 waves split the 4 column tiles
+  if ((rc = launch_dw<MODE, 1, 128, 0, 4>(d, L, ws, L_R, D_ZR, A_G, -1, 0, G, s)) != DEN_OK) return rc;
   if (g->grad_bkgd) {
     hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(256), 0, s, d->radiance_dim, d->n_rays,
                        (const float*)(ws + L.bkgd_partial), g->grad_bkgd);

@@ -136,8 +136,11 @@ __device__ __forceinline__ float dsoftplus_b100_from_out(float s) {
 }
 // BF16 path, base-2 scaled units (den_geom.h KAPPA): s' = max(t,0) + log2(1 + 2^-|t|)
 // (for t > 20*log2(e) the log term is 0 in f32: torch's threshold branch).
+// max(t, 0) as v_med3_f32(t, 0, FLT_MAX): fmaxf lowers to maxnum, which makes the compiler
+// canonicalize an MFMA result first (a second v_max_f32 per element in the forward epilogue).
 __device__ __forceinline__ float softplus2_scaled(float t) {
-  return fmaxf(t, 0.0f) + __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(-fabsf(t)));
+  return __builtin_amdgcn_fmed3f(t, 0.0f, 3.4028235e38f) +
+         __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(-fabsf(t)));
 }
 // its derivative from the output: sigmoid(100 z) = 1 - 2^-s'
 __device__ __forceinline__ float dsoftplus2_scaled_from_out(float s) { return 1.0f - __builtin_amdgcn_exp2f(-s); }

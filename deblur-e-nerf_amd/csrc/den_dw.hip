@@ -61,14 +61,17 @@ DEN_HD constexpr int dw_pad_bytes(int W) {
   return MODE == 1 ? 4 * (((16 - (W / 2)) % 64 + 64) % 64) : 16;
 }
 
-template <int MODE, int MT, int N1, int N2>
-__global__ __launch_bounds__(64 * MT) void dw_gemm_kernel(DwArgs P) {
+// WN waves per 32-row tile of dz split its N/32 column tiles (narrow layers: rgb output, M = 32).
+template <int MODE, int MT, int N1, int N2, int WN>
+__global__ __launch_bounds__(64 * MT * WN) void dw_gemm_kernel(DwArgs P) {
   constexpr int M = 32 * MT, N = N1 + N2, NT = N / 32;
+  static_assert(NT % WN == 0, "column tiles split evenly over the waves of a row tile");
+  constexpr int NTG = NT / WN;  // column tiles per wave
   constexpr int DW_BK = (NT + 1) * 16 > 160 ? 16 : 32;
   constexpr int ES = es_of(MODE);
   constexpr int PA = M * ES + dw_pad_bytes<MODE>(M), PB = N * ES + dw_pad_bytes<MODE>(N);
   constexpr int IMG = DW_BK * (PA + PB);
-  constexpr int THREADS = 64 * MT;
+  constexpr int THREADS = 64 * MT * WN;
   constexpr int TMm = tm_of(MODE);
   constexpr int NTA = M / TMm, NT1 = N1 / TMm, NT2 = N2 / TMm;  // tiles per segment
   // 16-B units of a chunk per segment (4 per sample and tile in both modes), in memory order
@@ -78,13 +81,14 @@ __global__ __launch_bounds__(64 * MT) void dw_gemm_kernel(DwArgs P) {
   __shared__ __attribute__((aligned(16))) char lds[2 * IMG];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int mt = wave % MT, cg = wave / MT;  // row tile, column group
   const int64_t k_begin = (int64_t)blockIdx.x * P.per_split;
   const int64_t k_end = min(P.n, k_begin + P.per_split);
   const int nchunks = (int)((k_end - k_begin + DW_BK - 1) / DW_BK);
 
-  f32x16 acc[NT + 1];
+  f32x16 acc[NTG + 1];
 #pragma unroll
-  for (int t = 0; t <= NT; ++t)
+  for (int t = 0; t <= NTG; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
 
@@ -166,36 +170,37 @@ __global__ __launch_bounds__(64 * MT) void dw_gemm_kernel(DwArgs P) {
           }
           return f;
         };
-        bf16x8 a = tr_frag(imgA, PA, 32 * wave);
+        bf16x8 a = tr_frag(imgA, PA, 32 * mt);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          bf16x8 b = tr_frag(imgB, PB, 32 * t);
+        for (int t = 0; t < NTG; ++t) {
+          bf16x8 b = tr_frag(imgB, PB, 32 * (cg * NTG + t));
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[t], 0, 0, 0);
         }
-        acc[NT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, ones, acc[NT], 0, 0, 0);
+        acc[NTG] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, ones, acc[NTG], 0, 0, 0);
       }
     } else {
       const int c = lane & 31, h = lane >> 5;
 #pragma unroll 4
       for (int kk = 0; kk < DW_BK / 2; ++kk) {
         const int row = 2 * kk + h;
-        float a = *(const float*)(imgA + row * PA + (32 * wave + c) * 4);
+        float a = *(const float*)(imgA + row * PA + (32 * mt + c) * 4);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          float b = *(const float*)(imgB + row * PB + (32 * t + c) * 4);
+        for (int t = 0; t < NTG; ++t) {
+          float b = *(const float*)(imgB + row * PB + (32 * (cg * NTG + t) + c) * 4);
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
         }
-        acc[NT] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, 1.0f, acc[NT], 0, 0, 0);
+        acc[NTG] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, 1.0f, acc[NTG], 0, 0, 0);
       }
     }
     if (more) store((ch + 1) & 1);
     __syncthreads();
   }
 
-  float* out = P.partial + (((int64_t)blockIdx.x * MT + wave) * (NT + 1)) * 1024;
+  float* out = P.partial + (((int64_t)blockIdx.x * MT + mt) * (NT + 1)) * 1024;
 #pragma unroll
-  for (int t = 0; t <= NT; ++t) {
-    f32x4* o4 = (f32x4*)(out + t * 1024 + lane * 16);
+  for (int t = 0; t <= NTG; ++t) {
+    if (t == NTG && cg != 0) break;  // the ones (bias) tile is column group 0's
+    f32x4* o4 = (f32x4*)(out + (t == NTG ? NT : cg * NTG + t) * 1024 + lane * 16);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       f32x4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
@@ -252,17 +257,17 @@ __global__ void dw_reduce_kernel(DwReduceArgs R) {
       R.mode == 0 ? s : (float)((double)s * col_scale(R.mode, R.layer, f));
 }
 
-template __global__ void dw_gemm_kernel<1, 8, 64, 0>(DwArgs);
-template __global__ void dw_gemm_kernel<1, 8, 256, 0>(DwArgs);
-template __global__ void dw_gemm_kernel<1, 8, 256, 64>(DwArgs);
-template __global__ void dw_gemm_kernel<1, 4, 256, 32>(DwArgs);
-template __global__ void dw_gemm_kernel<1, 1, 128, 0>(DwArgs);
-template __global__ void dw_gemm_kernel<1, 1, 256, 0>(DwArgs);
-template __global__ void dw_gemm_kernel<0, 8, 64, 0>(DwArgs);
-template __global__ void dw_gemm_kernel<0, 8, 256, 0>(DwArgs);
-template __global__ void dw_gemm_kernel<0, 8, 256, 64>(DwArgs);
-template __global__ void dw_gemm_kernel<0, 1, 256, 0>(DwArgs);
-template __global__ void dw_gemm_kernel<0, 4, 256, 32>(DwArgs);
-template __global__ void dw_gemm_kernel<0, 1, 128, 0>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 8, 64, 0, 1>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 8, 256, 0, 1>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 8, 256, 64, 1>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 1, 256, 0, 4>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 4, 256, 32, 1>(DwArgs);
+template __global__ void dw_gemm_kernel<1, 1, 128, 0, 4>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 8, 64, 0, 1>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 8, 256, 0, 1>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 8, 256, 64, 1>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 1, 256, 0, 4>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 4, 256, 32, 1>(DwArgs);
+template __global__ void dw_gemm_kernel<0, 1, 128, 0, 4>(DwArgs);
 
 }  // namespace den
