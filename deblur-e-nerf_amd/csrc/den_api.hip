@@ -13,6 +13,7 @@
 
 #include "../../include/den_api.h"
 #include "den_dw.hip"
+#include "den_events.hip"
 #include "den_hidden.hip"
 #include "den_misc.hip"
 #include "den_pixbw.hip"
@@ -597,6 +598,32 @@ int den_event_step_bwd(int32_t N, int32_t rd, int32_t fn_d, int32_t fn_t, int32_
   EventStepArgs E = make_event_args(N, rd, fn_d, fn_t, has_bkgd, min_int, w_d, w_t, radiance, opacity, channel,
                                     target, c, ws, nullptr, d_radiance);
   hipLaunchKernelGGL(event_step_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, E);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_event_prep(int32_t N, int32_t has_diff, int32_t has_tv, const int64_t* num_pos, const int64_t* num_neg,
+                   const int64_t* end_ts, const int64_t* start_ts, const double* norm, const float* ct,
+                   const double* refractory, const float* norm_c, float* lid, double* start_out, double* render_ts,
+                   double* ts_diff, double* ts_subdiff, float* target, void* stream) {
+  if (N <= 0 || !num_pos || !num_neg || !end_ts || !start_ts || !norm || !ct || !refractory || !lid || !start_out ||
+      !render_ts || (target && (!norm_c || !has_diff)))
+    return fail(DEN_EINVAL, "bad arguments");
+  EventPrepArgs E{N, has_diff ? 1 : 0, has_tv ? 1 : 0, num_pos, num_neg, end_ts, start_ts, norm, ct, refractory,
+                  norm_c, lid, start_out, render_ts, ts_diff, ts_subdiff, target};
+  hipLaunchKernelGGL(event_prep_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, E);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_pixel_rays(int32_t M, int32_t N, const float* k_inv, const float* pixel, const float* t_pos,
+                   const float* t_rot, float* ray_o, float* ray_d, void* stream) {
+  if (M <= 0 || N <= 0 || (int64_t)M * N > (int64_t)INT32_MAX * 64 || !k_inv || !pixel || !t_pos || !t_rot ||
+      !ray_o || !ray_d)
+    return fail(DEN_EINVAL, "bad arguments");
+  const int64_t n = (int64_t)M * N;
+  hipLaunchKernelGGL(pixel_rays_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, M, N,
+                     k_inv, pixel, t_pos, t_rot, ray_o, ray_d);
   DEN_LAUNCHED();
   return DEN_OK;
 }

@@ -69,6 +69,8 @@ _SIGS = {
     "den_event_step_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
     "den_event_step_fwd": (ctypes.c_int, [ctypes.c_int32] * 5 + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 8),
     "den_event_step_bwd": (ctypes.c_int, [ctypes.c_int32] * 5 + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 8),
+    "den_event_prep": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 15),
+    "den_pixel_rays": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 7),
     "den_pixbw_sample_ts": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]),
     "den_pixbw_fwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 9),
@@ -387,3 +389,57 @@ class PixelBandwidthFunction(torch.autograd.Function):
         sum_partials(part, PIXBW_NPARAM, nb, d_prm)
         return (d_it.reshape(ctx.in_shape).to(ctx.in_dtype), d_prm.to(ctx.p_dtype),
                 None if d_din is None else d_din.reshape(ctx.din_shape), None, None, None, None)
+
+
+# ----------------------------------------------------------------------------- event preparation
+def event_prep(num_pos, num_neg, end_ts, start_ts, normalized, ct, refractory, norm_c=None, has_diff=True,
+               has_tv=True, out=None):
+    """den_event_prep: ContrastThreshold + RefractoryPeriod forward and the diff /
+    subdiff timestamps of DeblurENeRF.training_step (deblur_e_nerf.py:414-455).
+
+    num_pos, num_neg, end_ts, start_ts (N) i64; normalized (4,N) f64 [ts_diff,
+    diff_start_ts, ts_subdiff, subdiff_start_ts]; ct (2) f32 [C+, C-]; refractory
+    (1) f64 (ns).  -> dict(lid (N) f32, start_ts (N) f64, render_ts (4,N) f64,
+    ts_diff (N) f64, ts_subdiff (N) f64, target (N) f32 if norm_c is given)."""
+    _require_device(num_pos, num_neg, end_ts, start_ts, normalized, ct, refractory, norm_c)
+    for t, dt in ((num_pos, torch.int64), (num_neg, torch.int64), (end_ts, torch.int64), (start_ts, torch.int64),
+                  (normalized, torch.float64), (ct, torch.float32), (refractory, torch.float64)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise DenError(f"event_prep: expected contiguous {dt}, got {t.dtype}")
+    N = end_ts.numel()
+    if normalized.shape != (4, N) or ct.numel() != 2 or refractory.numel() != 1:
+        raise DenError("event_prep: bad shapes")
+    dev = end_ts.device
+    if out is None:
+        out = dict(lid=torch.empty(N, device=dev), start_ts=torch.empty(N, dtype=torch.float64, device=dev),
+                   render_ts=torch.zeros(4, N, dtype=torch.float64, device=dev),
+                   ts_diff=torch.zeros(N, dtype=torch.float64, device=dev),
+                   ts_subdiff=torch.zeros(N, dtype=torch.float64, device=dev),
+                   target=torch.empty(N, device=dev) if norm_c is not None else None)
+    _check(lib().den_event_prep(N, int(has_diff), int(has_tv), _ptr(num_pos), _ptr(num_neg), _ptr(end_ts),
+                                _ptr(start_ts), _ptr(normalized), _ptr(ct), _ptr(refractory), _ptr(norm_c),
+                                _ptr(out["lid"]), _ptr(out["start_ts"]), _ptr(out["render_ts"]),
+                                _ptr(out["ts_diff"]), _ptr(out["ts_subdiff"]), _ptr(out["target"]), _stream(dev)))
+    return out
+
+
+def pixel_rays(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation, out=None):
+    """den_pixel_rays (NeRF.pixel_params_to_ray, nerf.py:206-228): K^-1 (3,3),
+    pixels (N,2), poses ([M,] N, 3) / ([M,] N, 3, 3) -> origins, unit directions
+    ([M,] N, 3) f32.  Pixels broadcast over the leading render-group dim M."""
+    _require_device(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
+    ts = (intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
+    if any(t.dtype != torch.float32 or not t.is_contiguous() for t in ts):
+        raise DenError("pixel_rays: expected contiguous f32 tensors")
+    N = pixel_position.shape[0]
+    lead = T_wc_position.shape[:-1]
+    M = T_wc_position.numel() // (3 * N) if N else 0
+    if (intrinsics_inverse.shape != (3, 3) or pixel_position.shape != (N, 2) or lead[-1:] != (N,)
+            or T_wc_orientation.shape != (*lead, 3, 3) or M * N * 3 != T_wc_position.numel()):
+        raise DenError("pixel_rays: bad shapes")
+    if out is None:
+        out = (torch.empty_like(T_wc_position), torch.empty_like(T_wc_position))
+    _check(lib().den_pixel_rays(M, N, _ptr(intrinsics_inverse), _ptr(pixel_position), _ptr(T_wc_position),
+                                _ptr(T_wc_orientation), _ptr(out[0]), _ptr(out[1]),
+                                _stream(pixel_position.device)))
+    return out

@@ -97,7 +97,11 @@ class NeRF(torch.nn.Module):
 
     @staticmethod
     def pixel_params_to_ray(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation):
-        raise NotImplementedError("trajectory / ray generation is the next row of SURVEY.md 8(f) (#2)")
+        """nerf.py:206-228 on the device (den_pixel_rays): (3,3), (N,2), ([M,] N, 3),
+        ([M,] N, 3, 3) -> ray origins, unit directions ([M,] N, 3).  Forward only:
+        pose refinement (gradients into the trajectory) is out of scope."""
+        return _native.pixel_rays(intrinsics_inverse.float().contiguous(), pixel_position.float().contiguous(),
+                                  T_wc_position.float().contiguous(), T_wc_orientation.float().contiguous())
 
     def forward(self, ray_origin, ray_direction):
         shape = ray_origin.shape[:-1]

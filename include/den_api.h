@@ -28,6 +28,11 @@
  *   den_pixbw_*      <- deblur_e_nerf/models/pixel_bandwidth.py:298-494
  *                       PixelBandwidth.sample_intensity / forward and
  *                       utils/control.py:29-123 foh_cont2discrete
+ *   den_event_prep   <- deblur_e_nerf/models/event_generation_params.py:106-118
+ *                       ContrastThreshold.forward, :230-237 RefractoryPeriod.forward
+ *                       and the timestamp derivation of
+ *                       deblur_e_nerf/models/deblur_e_nerf.py:418-455 training_step
+ *   den_pixel_rays   <- deblur_e_nerf/models/nerf.py:206-228 NeRF.pixel_params_to_ray
  *   den_event_loss_* <- deblur_e_nerf/loss_metric/loss.py:34-96 Loss.compute
  *   den_event_target
  *   den_adam_step    <- torch.optim.Adam as configured by
@@ -225,6 +230,34 @@ int den_event_step_fwd(int32_t N, int32_t rd, int32_t fn_d, int32_t fn_t, int32_
 int den_event_step_bwd(int32_t N, int32_t rd, int32_t fn_d, int32_t fn_t, int32_t has_bkgd, float min_int,
                        float w_d, float w_t, const float* radiance, const float* opacity, const int64_t* channel,
                        const float* target, const float* norm_c, void* workspace, float* d_radiance, void* stream);
+
+/* ---------------------------------------------------------------- event preparation
+ * The event corrections and supervision timestamps of DeblurENeRF.training_step,
+ * one thread per event:
+ *   lid       = f32(num_pos) * C+ - f32(num_neg) * C-         (ContrastThreshold.forward)
+ *   start_out = f64(start_ts) + tau_r                          (RefractoryPeriod.forward)
+ *   has_diff: dt = (end - start_out) * norm[0]; s = lerp(start_out, max(end - dt, start_out), norm[1]);
+ *             e = min(s + dt, end); render_ts[0] = s, render_ts[1] = e, ts_diff = dt,
+ *             target = f32(dt * (lid / (end - start_out)) / norm_c)  (loss.py:74-77; needs norm_c)
+ *   has_tv:   the same on [s, e] (or [start_out, end] without has_diff) with norm[2], norm[3]
+ *             -> render_ts[2], render_ts[3], ts_subdiff
+ * norm (4,N) f64 = the datamodule's normalized ts_diff, diff_start_ts, ts_subdiff,
+ * subdiff_start_ts samples; ct (2) f32 = C+, C- and refractory (1) f64 = tau_r ns are
+ * the modules' post-parametrisation values (device scalars).  render_ts (4,N) f64 is
+ * the [diff start, diff end, tv start, tv end] timestamp grid the renders consume.
+ * ts_diff, ts_subdiff, target may be NULL.  Forward only: the synthetic
+ * configuration freezes C+/C-/tau_r (configs/train/synthetic.yaml:29-40). */
+int den_event_prep(int32_t N, int32_t has_diff, int32_t has_tv, const int64_t* num_pos, const int64_t* num_neg,
+                   const int64_t* end_ts, const int64_t* start_ts, const double* norm, const float* ct,
+                   const double* refractory, const float* norm_c, float* lid, double* start_out, double* render_ts,
+                   double* ts_diff, double* ts_subdiff, float* target, void* stream);
+
+/* Rays of M render groups x N pixels (NeRF.pixel_params_to_ray):
+ *   ray_d[m,n] = normalize(t_rot[m,n] @ (k_inv @ [pixel[n], 1])),  ray_o[m,n] = t_pos[m,n]
+ * k_inv (3,3) row-major, pixel (N,2), t_pos (M,N,3), t_rot (M,N,3,3) row-major, f32.
+ * ray_o, ray_d (M,N,3): exactly the (R,3) ray layout den_render_fwd reads, R = M*N. */
+int den_pixel_rays(int32_t M, int32_t N, const float* k_inv, const float* pixel, const float* t_pos,
+                   const float* t_rot, float* ray_o, float* ray_d, void* stream);
 
 /* ---------------------------------------------------------------- reductions / optimizer */
 /* out[j] = sum_b partial[j*n_blocks + b] for j < n (deterministic order). */

@@ -24,6 +24,16 @@ enum/tinycudann).  What each fixture pins:
                            normalized, masked means) + gradients.
 * ``ct.npz``            -- models/event_generation_params.py ContrastThreshold
                            forward (counts -> delta log I).
+* ``events.npz``        -- the event preparation of DeblurENeRF.training_step:
+                           ContrastThreshold + RefractoryPeriod forward (modules
+                           run as-is), then the diff / subdiff timestamp derivation
+                           of deblur_e_nerf.py:418-455, executed from the reference
+                           file's own text (located by its comment markers at
+                           generation time; nothing of it is stored), for the three
+                           loss-weight cases (both terms, diff only, TV only).
+* ``rays.npz``          -- models/nerf.py NeRF.pixel_params_to_ray (pixel + pose ->
+                           ray origin / unit direction), with and without the
+                           leading render-group dimension.
 """
 import os
 import sys
@@ -290,7 +300,89 @@ def gen_ct():
          mean_ct=ct.mean_contrast_threshold.detach().numpy())
 
 
-if __name__ == "__main__":
+def _training_step_ts_code():
+    """The timestamp-derivation block of DeblurENeRF.training_step, read from the
+    reference file (deblur_e_nerf.py:418-455) between its own comment markers."""
+    src = open(os.path.join(_refload.REF_ROOT, "deblur_e_nerf/models/deblur_e_nerf.py")).read().splitlines()
+    a = next(i for i, l in enumerate(src) if "# derive the ts. for log-intensity supervision" in l)
+    b = next(i for i in range(a, len(src)) if src[i].strip() == "batch.subdiff = None")
+    import textwrap
+    return textwrap.dedent("\n".join(src[a:b + 1]))
+
+
+def gen_events():
+    egp = _refload.load("models.event_generation_params")
+    ED = sys.modules["easydict"].EasyDict
+    d = _calib_dir(EDS)
+    cal = dict(np.load(os.path.join(d, "camera_calibration.npz")))
+    cal["refractory_period"] = np.array(250000)            # ns, i64 like the calibration files
+    np.savez(os.path.join(d, "camera_calibration.npz"), **cal)
+    torch.save(torch.tensor(1000000), os.path.join(d, "max_refractory_period.pt"))
+    ct = egp.ContrastThreshold(d, parameterize_mean_ct=True)
+    rp = egp.RefractoryPeriod(d)
+    with torch.no_grad():  # move off the calibrated values so the parametrisations matter
+        ct.parametrizations.p2n_contrast_threshold_ratio.original.add_(0.07)
+        ct.parametrizations.mean_contrast_threshold.original.sub_(0.03)
+        rp.parametrizations._refractory_period.original.add_(12345.678)
+    code = compile(_training_step_ts_code(), "deblur_e_nerf.py:418-455", "exec")
+    g = torch.Generator().manual_seed(21)
+    N = 512
+    num_pos = torch.randint(0, 3, (N,), generator=g)
+    num_neg = torch.randint(0, 3, (N,), generator=g)
+    num_pos[:128] = (torch.rand(128, generator=g) < 0.5).long()      # queued events: one per interval
+    num_neg[:128] = 1 - num_pos[:128]
+    end_ts = (torch.rand(N, generator=g, dtype=torch.float64) * 9e8 + 1e8).floor().long()
+    start_ts = end_ts - (torch.rand(N, generator=g, dtype=torch.float64) * 3e6 + 3e5).floor().long()
+    norm = torch.rand(4, N, generator=g, dtype=torch.float64)
+    norm[0, :256] = 1.0                                                # Dirac(1) interval sampler
+    norm[1, :8] = torch.tensor([0.0, 0.5, 1.0, 0.25, 0.75, 1e-9, 1 - 1e-9, 0.5 - 1e-12], dtype=torch.float64)
+    norm[3, :8] = norm[1, :8]
+    out = dict(num_pos=num_pos.numpy(), num_neg=num_neg.numpy(), end_ts=end_ts.numpy(), start_ts=start_ts.numpy(),
+               norm=norm.numpy(), pos_ct=ct.pos_contrast_threshold.detach().numpy(),
+               neg_ct=ct.neg_contrast_threshold.detach().numpy(),
+               mean_ct=ct.mean_contrast_threshold.detach().numpy(),
+               refractory_period=rp.refractory_period.detach().numpy())
+    for tag, wd, wt in (("both", 1.0, 1e-3), ("diff", 1.0, 0.0), ("tv", 0.0, 1e-3)):
+        ev = ED(num_pos=num_pos.clone(), num_neg=num_neg.clone(), end_ts=end_ts.clone(), start_ts=start_ts.clone())
+        batch = ED(event=ev, normalized=ED(ts_diff=norm[0], diff_start_ts=norm[1], ts_subdiff=norm[2],
+                                           subdiff_start_ts=norm[3]))
+        with torch.no_grad():
+            batch.event = ct(batch.event)
+            batch.event = rp(batch.event)
+            self_ = types.SimpleNamespace(hparams=ED(loss=ED(weight=ED(log_intensity_diff=wd, log_intensity_tv=wt))))
+            exec(code, {"torch": torch}, {"batch": batch, "self": self_})
+        out[f"{tag}:lid"] = batch.event.log_intensity_diff.numpy()
+        out[f"{tag}:start_ts"] = batch.event.start_ts.numpy()
+        for grp in ("diff", "subdiff"):
+            if batch[grp] is not None:
+                for k in ("ts_diff", "start_ts", "end_ts"):
+                    out[f"{tag}:{grp}.{k}"] = batch[grp][k].numpy()
+    save("events.npz", **out)
+
+
+def gen_rays():
+    nerfm = _refload.load("models.nerf")
+    g = torch.Generator().manual_seed(23)
+    N, M = 400, 4
+    K = torch.tensor([[1111.0, 0.0, 400.0], [0.0, 1111.0, 400.0], [0.0, 0.0, 1.0]])
+    K_inv = torch.linalg.inv(K)
+    pixel = torch.rand(N, 2, generator=g) * 800
+    pixel[:4] = torch.tensor([[0.0, 0.0], [799.5, 799.5], [400.0, 400.0], [0.5, 799.0]])
+    q, _ = torch.linalg.qr(torch.randn(M, N, 3, 3, generator=g, dtype=torch.float64))
+    rot = (q * torch.sign(torch.linalg.det(q))[..., None, None]).float()      # proper rotations
+    pos = torch.randn(M, N, 3, generator=g) * 4
+    o, dr = nerfm.NeRF.pixel_params_to_ray(K_inv, pixel, pos, rot)          # (N,2) pixels broadcast over M
+    o1, d1 = nerfm.NeRF.pixel_params_to_ray(K_inv, pixel, pos[0], rot[0])
+    save("rays.npz", K_inv=K_inv.numpy(), pixel=pixel.numpy(), T_wc_position=pos.numpy(),
+         T_wc_orientation=rot.numpy(), ray_origin=o.numpy(), ray_direction=dr.numpy(),
+         ray_origin_1=o1.numpy(), ray_direction_1=d1.numpy())
+
+
+if __name__ == "__main__" and len(sys.argv) > 1:
+    torch.set_num_threads(8)
+    for name in sys.argv[1:]:
+        globals()["gen_" + name]()
+elif __name__ == "__main__":
     torch.set_num_threads(8)
     gen_mlp(3, seed=0)
     gen_mlp(1, seed=1)
@@ -300,3 +392,5 @@ if __name__ == "__main__":
     gen_pixbw(16, PERTURBED, "pert")
     gen_loss()
     gen_ct()
+    gen_events()
+    gen_rays()

@@ -183,3 +183,36 @@ def test_contrast_threshold_matches_reference(golden_dir):
     lid = oloss.contrast_log_intensity_diff(torch.from_numpy(z["num_pos"]), torch.from_numpy(z["num_neg"]),
                                             torch.from_numpy(z["pos_ct"]), torch.from_numpy(z["neg_ct"]))
     assert np.array_equal(lid.numpy(), z["lid"])
+
+
+# --------------------------------------------------------------------------- event preparation / pixel rays
+@pytest.mark.parametrize("tag,has_diff,has_tv", [("both", True, True), ("diff", True, False), ("tv", False, True)])
+def test_event_prep_matches_reference(golden_dir, tag, has_diff, has_tv):
+    """events.npz = the reference's ContrastThreshold / RefractoryPeriod modules
+    and its training_step timestamp block, run here: the oracle is bit-exact."""
+    from oracle import events as oev
+    z = _load(golden_dir, "events.npz")
+    t = {k: torch.from_numpy(z[k]) for k in ("num_pos", "num_neg", "end_ts", "start_ts", "norm", "pos_ct", "neg_ct",
+                                               "refractory_period")}
+    o = oev.event_prep(t["num_pos"], t["num_neg"], t["end_ts"], t["start_ts"], t["norm"], t["pos_ct"], t["neg_ct"],
+                       t["refractory_period"], has_diff, has_tv)
+    assert o["lid"].dtype == torch.float32 and o["start_ts"].dtype == torch.float64
+    assert np.array_equal(o["lid"].numpy(), z[f"{tag}:lid"])
+    assert np.array_equal(o["start_ts"].numpy(), z[f"{tag}:start_ts"])
+    for grp, have in (("diff", has_diff), ("subdiff", has_tv)):
+        assert (o[grp] is not None) == have
+        if have:
+            for i, k in enumerate(("ts_diff", "start_ts", "end_ts")):
+                assert np.array_equal(o[grp][i].numpy(), z[f"{tag}:{grp}.{k}"]), (grp, k)
+
+
+def test_pixel_rays_match_reference(golden_dir):
+    from oracle import events as oev
+    z = _load(golden_dir, "rays.npz")
+    K, px, pos, rot = (torch.from_numpy(z[k]) for k in ("K_inv", "pixel", "T_wc_position", "T_wc_orientation"))
+    o, d = oev.pixel_params_to_ray(K, px, pos, rot)
+    assert np.array_equal(o.numpy(), z["ray_origin"])
+    assert rel_err(d, z["ray_direction"]) < 1e-7
+    o1, d1 = oev.pixel_params_to_ray(K, px, pos[0], rot[0])
+    assert rel_err(d1, z["ray_direction_1"]) < 1e-7
+    assert np.allclose(np.linalg.norm(z["ray_direction"], axis=-1), 1.0, atol=1e-6)
