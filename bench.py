@@ -1,9 +1,13 @@
 """Train-step throughput of the Deblur e-NeRF render + event-measurement hot path.
 
 Workload (BASELINE.json configs[1]): chair-like synthetic scene, 2^17 rays x 128
-samples per step through the 8x256 `mlp` NeRF, pixel-bandwidth model off, rays
-= 4 render groups (diff start/end, TV start/end) x 32768 events, Huber diff +
-1e-3 L1 TV loss, backward, all-reduce, Adam.  Strong scaling: the 2^17-ray step
+samples per step through the 8x256 `mlp` NeRF, pixel-bandwidth model off.  Each
+step starts from the raw events (32768: counts, i64 timestamps, normalized
+samples, pixels, camera poses at the 4 render timestamps) resident in HBM:
+event preparation (contrast threshold, refractory delay, diff/subdiff
+timestamps, target) and pixel rays on the device, then 4 render groups (diff
+start/end, TV start/end) x 32768 events, Huber diff + 1e-3 L1 TV loss,
+backward, all-reduce, Adam.  Strong scaling: the 2^17-ray step
 is split over the ranks (reference DDP semantics: per-GPU batch = eff // gpus).
 
     python bench.py [--gpus N --steps K --warmup W]     (N > 1 via torch.distributed.run)
@@ -82,6 +86,7 @@ def phase_times(ts, reps=PHASE_REPS):
     for _ in range(reps):
         e = [ev() for _ in range(6)]
         e[0].record()
+        ts.prepare()
         ts.bkgd = torch.nn.functional.softplus(ts.bkgd_orig)
         ts.io.bkgd = nat._ptr(ts.bkgd)
         nat._check(L.den_render_fwd(ctypes.byref(ts.desc), ctypes.byref(ts.io), st))
@@ -112,11 +117,11 @@ def cpu_baseline(n_rays, n_samples, rd, threads):
     bounded sample: n_rays rays through render fwd + event loss + backward +
     Adam (the same step as the GPU line, fewer rays)."""
     from oracle import nerf as onerf
-    from oracle.train import step_loss
-    from deblur_e_nerf.train import synthetic_batch
+    from oracle.train import prepare_batch, step_loss
+    from deblur_e_nerf.train import synthetic_events
     torch.set_num_threads(threads)
     N = n_rays // 4
-    b = synthetic_batch(N, seed=99)
+    raw = synthetic_events(N, seed=99)
     p = onerf.build_params(rd, 0)
     params = list(p.values())
     for t in params:
@@ -126,6 +131,7 @@ def cpu_baseline(n_rays, n_samples, rd, threads):
 
     def step():
         opt.zero_grad()
+        b = prepare_batch(raw)
         total, _, _ = step_loss(p, torch.nn.functional.softplus(bk), b, n_samples)
         total.backward()
         opt.step()
@@ -138,7 +144,7 @@ def cpu_baseline(n_rays, n_samples, rd, threads):
     dt = (time.perf_counter() - t0) / reps
     return dict(value=round(n_rays / dt, 2), unit="rays/s", cores=threads, kind="port",
                 sample=f"oracle (PyTorch CPU) train step on {n_rays} rays x {n_samples} samples "
-                       f"(render fwd + event loss + backward + Adam), {reps} timed reps after 1 warm-up, "
+                       f"(event prep + rays + render fwd + event loss + backward + Adam), {reps} timed reps after 1 warm-up, "
                        f"{dt:.2f} s/step")
 
 
@@ -153,12 +159,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     from deblur_e_nerf import _native as nat
-    from deblur_e_nerf.train import TrainStep, synthetic_batch
+    from deblur_e_nerf.train import TrainStep, synthetic_events
 
     assert a.rays % (4 * world) == 0
     n_events = a.rays // 4 // world
     ts = TrainStep(n_events, n_samples=a.samples, radiance_dim=a.rd, mode=a.mode, device=dev)
-    ts.load_batch(**synthetic_batch(n_events, rank=rank, world=world, device="cpu"))
+    ts.load_events(**synthetic_events(n_events, rank=rank, world=world))
     for _ in range(a.warmup):
         ts.step()
     torch.cuda.synchronize()
@@ -226,9 +232,9 @@ def main():
             "metric": "train-step rays/sec at 131072 rays x 128 samples",
             "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": a.mode, "data": "synthetic (chair-like rays/events, PyTorch default-init weights)",
+            "dtype": a.mode, "data": "synthetic (chair-like raw events + camera poses, PyTorch default-init weights)",
             "config": {"workload": f"chair synthetic, pixel-bandwidth off, {a.rays} rays x {a.samples} samples, "
-                                   f"mlp 8x256 rd={a.rd}, fwd+bwd+allreduce+Adam",
+                                   f"mlp 8x256 rd={a.rd}, event prep+rays+fwd+bwd+allreduce+Adam",
                        "rays_per_step": a.rays, "samples_per_ray": a.samples, "events_per_step": a.rays // 4,
                        "parallelism": f"ray-dp{world}"},
             "loss": [round(x, 6) for x in loss],

@@ -179,9 +179,15 @@ __device__ __forceinline__ RayGeom ray_geom(const float* o, const float* d, cons
   }
   if (near_p >= 0.0f) tmn = fmaxf(tmn, near_p);
   if (far_p >= 0.0f) tmx = fminf(tmx, far_p);
+  // A ray that misses AABB n [near, far] gets zero-length samples at its origin:
+  // nerfacc would return no samples at all (C = bkgd, O = D = 0, no gradient),
+  // which zero-length samples reproduce, and the MLP never sees the far-away
+  // points of a clipped slab intersection (whose raw coordinates enter the
+  // positional encoding unbounded).
   RayGeom g;
-  g.tmin = tmn;
-  g.span = (tmx > tmn) ? (tmx - tmn) : 0.0f;
+  const bool hit = tmx > tmn;
+  g.tmin = hit ? tmn : 0.0f;
+  g.span = hit ? (tmx - tmn) : 0.0f;
   return g;
 }
 

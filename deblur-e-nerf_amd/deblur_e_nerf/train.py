@@ -5,7 +5,8 @@
 for the synthetic configuration of BASELINE.json (chair, pixel-bandwidth model
 off, mlp arch), with every array operation in libden.so:
 
-  den_event_target -> den_render_fwd (4 render groups x N events in ONE launch)
+  [den_event_prep -> den_pixel_rays, when fed raw events (load_events)]
+  -> den_event_target (when fed prepared rays, load_batch) -> den_render_fwd (4 render groups x N events in ONE launch)
   -> den_event_step_fwd/bwd (log-intensity, Huber diff + L1 TV losses and their
   gradient) -> den_render_bwd (compositing adjoint, MLP backward, split-K weight
   gradients) -> RCCL all-reduce of one flat f32 gradient buffer (ranks > 1)
@@ -40,7 +41,8 @@ class TrainStep:
     def __init__(self, n_events, n_samples=128, radiance_dim=1, mode="bf16", seed=0, device="cuda",
                  aabb=(-1.5, -1.5, -1.5, 1.5, 1.5, 1.5), near=1.43, far=6.63, lr=0.01, weight_decay=1e-6,
                  loss_weight=(1.0, 1e-3), error_fn=("huber", "l1"), min_modeled_intensity=1e-3,
-                 mean_contrast_threshold=0.25, alpha_over_white_bg=True):
+                 mean_contrast_threshold=0.25, alpha_over_white_bg=True, contrast_thresholds=None,
+                 refractory_period=0.0):
         self.N, self.S, self.rd, self.mode = n_events, n_samples, radiance_dim, nat.mode_id(mode)
         self.dev = torch.device(device)
         self.R = 4 * n_events
@@ -68,6 +70,12 @@ class TrainStep:
         self.wl, self.fn = loss_weight, error_fn
         self.min_int = min_modeled_intensity
         self.c = torch.tensor([mean_contrast_threshold], device=self.dev)
+        # post-parametrisation C+, C- and tau_r (frozen in the synthetic configuration,
+        # configs/train/synthetic.yaml:29-40); C+ = C- = mean unless given
+        cp = contrast_thresholds or (mean_contrast_threshold, mean_contrast_threshold)
+        self.ct = torch.tensor(cp, dtype=torch.float32, device=self.dev)
+        self.tau = torch.tensor([refractory_period], dtype=torch.float64, device=self.dev)
+        self.raw = False
         self.cfg = dict(mode=self.mode, rd=radiance_dim, aabb=list(aabb), near=near, far=far)
         self.packed = nat.PackedWeights(self.mode, radiance_dim, self.dev)
         self.packed.pack(self.flat)
@@ -95,12 +103,57 @@ class TrainStep:
         self.ts_diff = ts_diff.to(d, torch.float64).contiguous()
         self.channel = None if channel is None else channel.to(d, torch.int64).contiguous()
 
+    def load_events(self, num_pos, num_neg, end_ts, start_ts, normalized, position, T_wc_position,
+                    T_wc_orientation, intrinsics_inverse, jitter, channel=None):
+        """Raw events as the datamodule hands them to training_step
+        (deblur_e_nerf.py:396-455): num_pos, num_neg, end_ts, start_ts (N) i64,
+        normalized (4,N) f64 [ts_diff, diff_start_ts, ts_subdiff, subdiff_start_ts],
+        pixel position (N,2) f32, and the camera poses at the 4 render timestamps
+        (4,N,3) / (4,N,3,3) f32 (the trajectory's output), K^-1 (3,3), per-ray
+        sampler jitter (4N).  Every step then derives the event corrections,
+        timestamps, target and rays on the device (den_event_prep, den_pixel_rays)."""
+        d = self.dev
+        i64 = lambda t: t.to(d, torch.int64).contiguous()
+        f32 = lambda t: t.to(d, torch.float32).contiguous()
+        self.ev = dict(num_pos=i64(num_pos), num_neg=i64(num_neg), end_ts=i64(end_ts), start_ts=i64(start_ts))
+        self.norm = normalized.to(d, torch.float64).contiguous()
+        self.position, self.T_pos, self.T_rot = f32(position), f32(T_wc_position), f32(T_wc_orientation)
+        self.K_inv = f32(intrinsics_inverse)
+        self.jitter = f32(jitter)
+        self.end_ts = self.ev["end_ts"]
+        self.channel = None if channel is None else i64(channel)
+        N = self.N
+        self.lid = torch.empty(N, device=d)
+        self.start_ts = torch.empty(N, dtype=torch.float64, device=d)
+        self.render_ts = torch.empty(4, N, dtype=torch.float64, device=d)
+        self.ts_diff = torch.empty(N, dtype=torch.float64, device=d)
+        self.ts_subdiff = torch.empty(N, dtype=torch.float64, device=d)
+        self.rays_o = torch.empty(4 * N, 3, device=d)
+        self.rays_d = torch.empty(4 * N, 3, device=d)
+        self.raw = True
+
     # ---------------------------------------------------------------- phases
+    def prepare(self):
+        """Raw events -> lid, refractory-shifted start, supervision timestamps,
+        diff target (den_event_prep) and the 4N rays (den_pixel_rays)."""
+        L, st = nat.lib(), nat._stream(self.dev)
+        e = self.ev
+        nat._check(L.den_event_prep(self.N, 1, 1, nat._ptr(e["num_pos"]), nat._ptr(e["num_neg"]),
+                                    nat._ptr(e["end_ts"]), nat._ptr(e["start_ts"]), nat._ptr(self.norm),
+                                    nat._ptr(self.ct), nat._ptr(self.tau), nat._ptr(self.c), nat._ptr(self.lid),
+                                    nat._ptr(self.start_ts), nat._ptr(self.render_ts), nat._ptr(self.ts_diff),
+                                    nat._ptr(self.ts_subdiff), nat._ptr(self.target), st))
+        nat._check(L.den_pixel_rays(4, self.N, nat._ptr(self.K_inv), nat._ptr(self.position), nat._ptr(self.T_pos),
+                                    nat._ptr(self.T_rot), nat._ptr(self.rays_o), nat._ptr(self.rays_d), st))
+
     def forward(self):
         L, st = nat.lib(), nat._stream(self.dev)
         self.bkgd = torch.nn.functional.softplus(self.bkgd_orig) if self.has_bkgd else None
-        nat._check(L.den_event_target(self.N, nat._ptr(self.ts_diff), nat._ptr(self.lid), nat._ptr(self.end_ts),
-                                      nat._ptr(self.start_ts), nat._ptr(self.c), nat._ptr(self.target), st))
+        if self.raw:
+            self.prepare()
+        else:
+            nat._check(L.den_event_target(self.N, nat._ptr(self.ts_diff), nat._ptr(self.lid), nat._ptr(self.end_ts),
+                                          nat._ptr(self.start_ts), nat._ptr(self.c), nat._ptr(self.target), st))
         self.io = nat.RenderIO(nat._ptr(self.rays_o), nat._ptr(self.rays_d), nat._ptr(self.jitter),
                                nat._ptr(self.packed.fwd), nat._ptr(self.packed.bwd), nat._ptr(self.packed.bias),
                                nat._ptr(self.bkgd), nat._ptr(self.ws), nat._ptr(self.rgb), nat._ptr(self.opacity),
@@ -163,3 +216,48 @@ def synthetic_batch(n_events, seed=1234, radius=4.03, device="cpu", rank=0, worl
     o4, d4, j4 = (t.reshape(4, N, *t.shape[1:])[:, sl].reshape(4 * n_events, *t.shape[1:]) for t in (o, d, jitter))
     return dict(rays_o=o4.to(device), rays_d=d4.to(device), jitter=j4.to(device), lid=lid[sl].to(device),
                 end_ts=end_ts[sl].to(device), start_ts=start_ts[sl].to(device), ts_diff=ts_diff[sl].to(device))
+
+
+def _look_at(centre, target_dir):
+    """Camera-to-world rotation whose z axis (principal axis) is target_dir
+    (x right, y down, as the reference's OpenCV-style intrinsics assume)."""
+    z = target_dir / target_dir.norm(dim=-1, keepdim=True)
+    up = torch.tensor([0.0, 0.0, 1.0]).expand_as(z)
+    x = torch.linalg.cross(z, up)
+    x = x / x.norm(dim=-1, keepdim=True).clamp_min(1e-6)
+    y = torch.linalg.cross(z, x)
+    return torch.stack([x, y, z], dim=-1)  # columns = camera axes in world coordinates
+
+
+def synthetic_events(n_events, seed=1234, radius=4.03, rank=0, world=1, img=800, focal=1111.0):
+    """Synthetic chair-like RAW event batch, the form
+    training_step receives: queued events (num_pos + num_neg = 1, polarity
+    Bernoulli(0.5)), end_ts ~ U[1e8, 1e9] ns, intervals ~ Exp(1 ms) + 1 us (i64),
+    the datamodule's normalized samples (ts_diff ~ Dirac(1), diff start ~ U,
+    ts_subdiff ~ Tri(0, 1, mode 0), subdiff start ~ U; datamodule.py:151-197),
+    pixel positions in an 800x800 image (f = 1111), and camera poses at the 4
+    render timestamps: centres on a sphere around the AABB looking at the origin
+    (+-0.3 rad), moving slightly between timestamps.  Rank r of `world` gets the
+    r-th contiguous shard of the events (all 4 renders of an event on one rank)."""
+    g = torch.Generator().manual_seed(seed)
+    N = n_events * world
+    v = torch.randn(N, 3, generator=g)
+    c0 = v / v.norm(dim=-1, keepdim=True) * radius
+    look = -c0 / c0.norm(dim=-1, keepdim=True) + (torch.rand(N, 3, generator=g) * 2 - 1) * math.sin(0.3)
+    rot = _look_at(c0, look)
+    motion = torch.randn(4, N, 3, generator=g) * 0.01
+    pos = c0[None] + motion
+    rot4 = rot[None].expand(4, N, 3, 3).contiguous()
+    pixel = torch.rand(N, 2, generator=g) * img
+    K = torch.tensor([[focal, 0.0, img / 2], [0.0, focal, img / 2], [0.0, 0.0, 1.0]])
+    jitter = torch.rand(4, N, generator=g)
+    num_pos = (torch.rand(N, generator=g) < 0.5).long()
+    end_ts = (torch.rand(N, generator=g, dtype=torch.float64) * 9e8 + 1e8).long()
+    start_ts = end_ts - (-torch.log(torch.rand(N, generator=g, dtype=torch.float64)) * 1e6 + 1e3).long()
+    u = torch.rand(3, N, generator=g, dtype=torch.float64)
+    norm = torch.stack([torch.ones(N, dtype=torch.float64), u[0], 1 - torch.sqrt(1 - u[1]), u[2]])
+    sl = slice(rank * n_events, (rank + 1) * n_events)
+    return dict(num_pos=num_pos[sl], num_neg=1 - num_pos[sl], end_ts=end_ts[sl], start_ts=start_ts[sl],
+                normalized=norm[:, sl].contiguous(), position=pixel[sl], T_wc_position=pos[:, sl].contiguous(),
+                T_wc_orientation=rot4[:, sl].contiguous(), intrinsics_inverse=torch.linalg.inv(K),
+                jitter=jitter[:, sl].reshape(-1).contiguous())

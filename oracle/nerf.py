@@ -137,6 +137,8 @@ def stratified_samples(o, d, u, aabb, near, far, n_samples):
     tmin, tmax = ray_aabb_tmin_tmax(o, d, aabb, near, far)
     hit = tmax > tmin
     span = torch.where(hit, tmax - tmin, torch.zeros_like(tmin))
+    # a missed ray: zero-length samples at its origin (nerfacc: no samples; same C, O, D, gradient)
+    tmin = torch.where(hit, tmin, torch.zeros_like(tmin))
     k = torch.arange(n_samples, dtype=o.dtype)
     s = (k[None, :] + u[:, None]) / n_samples
     mid = tmin[:, None] + s * span[:, None]

@@ -52,3 +52,17 @@ def flat_grad(p, bkgd_raw, batch, n_samples, rd, **kw):
     total.backward()
     g = torch.cat([t.grad.reshape(-1) for t in leaves] + [bk.grad.reshape(-1)])
     return g.detach(), (float(Ld.detach()), float(Lt.detach()), float(total.detach()))
+
+
+def prepare_batch(raw, contrast_thresholds=(0.25, 0.25), refractory_period=0.0):
+    """Raw event batch (deblur_e_nerf.train.synthetic_events layout) -> the
+    prepared layout step_loss consumes, through the oracle's event preparation
+    and pixel rays (oracle/events.py)."""
+    from . import events as oev
+    pc, nc = (torch.tensor(c, dtype=torch.float32) for c in contrast_thresholds)
+    o = oev.event_prep(raw["num_pos"], raw["num_neg"], raw["end_ts"], raw["start_ts"], raw["normalized"], pc, nc,
+                       torch.tensor(refractory_period, dtype=torch.float64))
+    ro, rdir = oev.pixel_params_to_ray(raw["intrinsics_inverse"], raw["position"], raw["T_wc_position"],
+                                       raw["T_wc_orientation"])
+    return dict(rays_o=ro.reshape(-1, 3), rays_d=rdir.reshape(-1, 3), jitter=raw["jitter"], lid=o["lid"],
+                end_ts=raw["end_ts"], start_ts=o["start_ts"], ts_diff=o["diff"][0])

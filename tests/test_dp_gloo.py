@@ -68,6 +68,20 @@ def test_sharding_partitions_the_global_batch():
         assert torch.equal(cat, f), k
 
 
+def test_raw_event_sharding_partitions_the_global_batch():
+    """synthetic_events shards whole events (all 4 renders of an event on one rank)."""
+    from deblur_e_nerf.train import synthetic_events
+    full = synthetic_events(N_PER_RANK * WORLD)
+    parts = [synthetic_events(N_PER_RANK, rank=r, world=WORLD) for r in range(WORLD)]
+    for k in ("num_pos", "num_neg", "end_ts", "start_ts", "position"):
+        assert torch.equal(torch.cat([p[k] for p in parts]), full[k]), k
+    for k in ("normalized", "T_wc_position", "T_wc_orientation"):
+        assert torch.equal(torch.cat([p[k] for p in parts], dim=1), full[k]), k
+    j = torch.cat([p["jitter"].reshape(4, N_PER_RANK) for p in parts], dim=1)
+    assert torch.equal(j, full["jitter"].reshape(4, -1))
+    assert torch.equal(parts[0]["intrinsics_inverse"], full["intrinsics_inverse"])
+
+
 @pytest.mark.timeout(300)
 def test_allreduce_mean_equals_full_batch_gradient():
     from deblur_e_nerf.train import synthetic_batch

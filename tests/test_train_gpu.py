@@ -65,6 +65,44 @@ def test_train_step_matches_oracle(mode, rd, tol_l, tol_g):
     assert e_bk <= max(tol_g, 4 * e_bk_cpu)
 
 
+@pytest.mark.parametrize("rd", [1, 3])
+def test_train_step_from_raw_events_matches_oracle(rd):
+    """TrainStep fed raw events (load_events: den_event_prep + den_pixel_rays on
+    the device every step) against the oracle's event preparation + rays + step,
+    F32 parity mode, with non-trivial C+/C- and refractory period."""
+    from deblur_e_nerf.train import TrainStep, synthetic_events
+    from oracle.train import flat_grad, prepare_batch
+    N, S = 64, 128
+    cts, tau = (0.27, 0.22), 1500.0
+    ts = TrainStep(N, n_samples=S, radiance_dim=rd, mode="f32", device=DEV, seed=7, contrast_thresholds=cts,
+                   refractory_period=tau, mean_contrast_threshold=0.245)
+    raw = synthetic_events(N, seed=8)
+    if rd == 3:
+        raw["channel"] = torch.randint(0, 3, (N,), generator=torch.Generator().manual_seed(8))
+    ts.load_events(**raw)
+    b = prepare_batch(raw, cts, tau)
+    if rd == 3:
+        b["channel"] = raw["channel"]
+    p32 = unflat(ts.flat.detach().cpu(), rd)
+    p64 = {k: v.double() for k, v in p32.items()}
+    b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in b.items()}
+    bk = ts.bkgd_orig.detach().cpu()
+    g32, (Ld, Lt, tot) = flat_grad({k: v.clone() for k, v in p32.items()}, bk, b, S, rd, mean_ct=0.245)
+    g64, _ = flat_grad(p64, bk.double(), b64, S, rd, mean_ct=0.245)
+    ts.forward()
+    ts.backward()
+    torch.cuda.synchronize()
+    # the device-derived inputs themselves
+    assert torch.equal(ts.lid.cpu(), b["lid"])
+    assert torch.equal(ts.start_ts.cpu(), b["start_ts"])
+    assert torch.allclose(ts.rays_d.cpu(), b["rays_d"], rtol=0, atol=1e-6)
+    loss = ts.loss[:3].cpu().tolist()
+    for a, r in zip(loss, (Ld, Lt, tot)):
+        assert abs(a - r) <= 1e-4 * max(abs(r), 1e-3), (loss, (Ld, Lt, tot))
+    g = ts.gbuf.detach().cpu().double()
+    assert norm_rel(g, g64) <= max(1e-4, 4 * norm_rel(g32.double(), g64))
+
+
 def test_adam_matches_torch():
     ts, _ = _setup("f32", 1)
     ts.forward()
@@ -96,3 +134,27 @@ def test_step_is_deterministic():
         torch.cuda.synchronize()
         out.append(ts.gbuf.detach().cpu().clone())
     assert torch.equal(out[0], out[1])
+
+
+def test_missed_rays_stay_finite_over_training():
+    """Rays that miss the AABB (here: near-axis directions passing beside the box)
+    render the background exactly, carry no gradient, and several Adam steps
+    stay finite (regression: their clipped slab points once fed unbounded
+    coordinates to the encoding)."""
+    from deblur_e_nerf.train import TrainStep, synthetic_events
+    N = 2048
+    ts = TrainStep(N, n_samples=128, radiance_dim=1, mode="bf16", device=DEV, seed=3)
+    raw = synthetic_events(N, seed=11)
+    # force a quarter of the events to look past the box along a near-axis direction
+    k = N // 4
+    raw["T_wc_position"][:, :k] = torch.tensor([-1.96, -3.49, -0.58])
+    raw["T_wc_orientation"][:, :k] = torch.eye(3)[[0, 2, 1]].T.contiguous()  # z axis ~ world y
+    raw["position"][:k] = torch.tensor([400.6, 400.0])
+    ts.load_events(**raw)
+    for _ in range(6):
+        ts.step()
+        assert torch.isfinite(ts.loss[:3]).all(), ts.loss
+    miss = ts.opacity[:k] == 0
+    assert bool(miss.all())
+    bk = ts.bkgd  # the background the last forward composited over (Adam has moved bkgd_orig since)
+    assert torch.equal(ts.rgb[:k][miss], bk.expand(int(miss.sum()), 1))
