@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--rd", type=int, default=1)
     ap.add_argument("--mode", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pixbw", action="store_true",
+                    help="BASELINE configs[2]: pixel-bandwidth model on (it_sample_size = --it-samples)")
+    ap.add_argument("--it-samples", type=int, default=16)
     ap.add_argument("--cpu-rays", type=int, default=2048, help="rays of the bounded CPU-baseline sample")
     return ap.parse_args()
 
@@ -148,6 +151,41 @@ def cpu_baseline(n_rays, n_samples, rd, threads):
                        f"{dt:.2f} s/step")
 
 
+def cpu_baseline_pixbw(n_rays, n_samples, rd, S, threads):
+    """Bounded CPU sample of the pixel-bandwidth-on step (oracle)."""
+    from oracle import nerf as onerf
+    from oracle import pixbw as opb
+    from oracle.train import pixbw_step_loss
+    from deblur_e_nerf.train import EDS_CALIBRATION, synthetic_pixbw_events
+    torch.set_num_threads(threads)
+    N = max(1, n_rays // (4 * S))
+    raw = synthetic_pixbw_events(N, S, seed=99)
+    prm = opb.calib_to_params(EDS_CALIBRATION)
+    p = onerf.build_params(rd, 0)
+    params = list(p.values())
+    for t in params:
+        t.requires_grad_(True)
+    bk = torch.tensor([0.5413] * rd, requires_grad=True)
+    opt = torch.optim.Adam([{"params": params, "weight_decay": 1e-6}, {"params": [bk]}], lr=0.01)
+
+    def step():
+        opt.zero_grad()
+        total, _, _ = pixbw_step_loss(p, torch.nn.functional.softplus(bk), raw, S, n_samples, prm, 5e7)
+        total.backward()
+        opt.step()
+
+    step()
+    t0 = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        step()
+    dt = (time.perf_counter() - t0) / reps
+    R = 4 * S * N
+    return dict(value=round(R / dt, 2), unit="rays/s", cores=threads, kind="port",
+                sample=f"oracle (PyTorch CPU) pixel-bandwidth-on train step, {N} events x 4 x S={S} = {R} rays x "
+                       f"{n_samples} samples, {reps} timed reps after 1 warm-up, {dt:.2f} s/step")
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -159,12 +197,18 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     from deblur_e_nerf import _native as nat
-    from deblur_e_nerf.train import TrainStep, synthetic_events
+    from deblur_e_nerf.train import PixbwTrainStep, TrainStep, synthetic_events, synthetic_pixbw_events
 
-    assert a.rays % (4 * world) == 0
-    n_events = a.rays // 4 // world
-    ts = TrainStep(n_events, n_samples=a.samples, radiance_dim=a.rd, mode=a.mode, device=dev)
-    ts.load_events(**synthetic_events(n_events, rank=rank, world=world))
+    per_event = 4 * a.it_samples if a.pixbw else 4
+    assert a.rays % (per_event * world) == 0
+    n_events = a.rays // per_event // world
+    if a.pixbw:
+        ts = PixbwTrainStep(n_events, it_sample_size=a.it_samples, n_samples=a.samples, radiance_dim=a.rd,
+                            mode=a.mode, device=dev)
+        ts.load_events(**synthetic_pixbw_events(n_events, a.it_samples, rank=rank, world=world))
+    else:
+        ts = TrainStep(n_events, n_samples=a.samples, radiance_dim=a.rd, mode=a.mode, device=dev)
+        ts.load_events(**synthetic_events(n_events, rank=rank, world=world))
     for _ in range(a.warmup):
         ts.step()
     torch.cuda.synchronize()
@@ -188,10 +232,16 @@ def main():
     value = rays_per_step * a.steps / elapsed
 
     nat.timing_enable(True)
-    phases = phase_times(ts)
+    if a.pixbw:  # autograd-chained step: per-kernel timing over whole steps, no phase split
+        for _ in range(PHASE_REPS):
+            ts.step()
+        torch.cuda.synchronize()
+        phases = {}
+    else:
+        phases = phase_times(ts)
     nat.timing_enable(False)
     kt = nat.timing_collect()
-    n_local = ts.R * ts.S
+    n_local = ts.R * (ts.n_samples if a.pixbw else ts.S)
     kernels = {}
     for k, (tot, cnt) in kt.items():
         if cnt == 0:
@@ -203,7 +253,7 @@ def main():
             b = BYTES_PER_SAMPLE[k] * n_local * PHASE_REPS / cnt  # algorithmic bytes per launch
             e.update(bytes_per_launch=b, gbs=round(b / (avg * 1e-3) / 1e9, 1))
         if k == "render_fwd_kernel":
-            f = 2.0 * MAC_PER_SAMPLE[a.rd] * n_local
+            f = 2.0 * MAC_PER_SAMPLE[a.rd] * n_local * PHASE_REPS / cnt  # algorithmic flop per launch
             e.update(flop_per_launch=f, tflops=round(f / (avg * 1e-3) / 1e12, 1))
         kernels[k] = e
     dom = max(kernels, key=lambda k: kernels[k]["step_ms"])  # the kernel that takes most of the step
@@ -224,7 +274,8 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
             threads = min(16, len(os.sched_getaffinity(0)))
-            cpu = cpu_baseline(a.cpu_rays, a.samples, a.rd, threads)
+            cpu = (cpu_baseline_pixbw(a.cpu_rays, a.samples, a.rd, a.it_samples, threads) if a.pixbw
+                   else cpu_baseline(a.cpu_rays, a.samples, a.rd, threads))
         except Exception as e:  # pragma: no cover - reported, not fatal
             cpu = {"error": repr(e)}
     if rank == 0:
@@ -233,9 +284,11 @@ def main():
             "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": a.mode, "data": "synthetic (chair-like raw events + camera poses, PyTorch default-init weights)",
-            "config": {"workload": f"chair synthetic, pixel-bandwidth off, {a.rays} rays x {a.samples} samples, "
+            "config": {"workload": f"chair synthetic, pixel-bandwidth {'on (it_sample_size=%d)' % a.it_samples if a.pixbw else 'off'}, "
+                                   f"{a.rays} rays x {a.samples} samples, "
                                    f"mlp 8x256 rd={a.rd}, event prep+rays+fwd+bwd+allreduce+Adam",
-                       "rays_per_step": a.rays, "samples_per_ray": a.samples, "events_per_step": a.rays // 4,
+                       "rays_per_step": a.rays, "samples_per_ray": a.samples,
+                       "events_per_step": a.rays // per_event,
                        "parallelism": f"ray-dp{world}"},
             "loss": [round(x, 6) for x in loss],
             "roofline": roofline,

@@ -256,6 +256,12 @@ __device__ __forceinline__ float wave_incl_scan(float v) {
   }
   return v;
 }
+// exclusive prefix sum over the wave (lane 0 gets 0); adds only, no incl - v subtraction
+__device__ __forceinline__ float wave_excl_scan(float v) {
+  const float incl = wave_incl_scan(v);
+  const float prev = __shfl_up(incl, 1, 64);
+  return (threadIdx.x & 63) == 0 ? 0.0f : prev;
+}
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

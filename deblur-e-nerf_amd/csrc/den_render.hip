@@ -253,7 +253,9 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
   // per-sample sigma / rgb (lane group 0 holds rows 0..)
   const int wl = wave * TM + c;  // WG-local sample
   if (grp == 0) {
-    float sigma = expf(sig_acc[0] - 1.0f) * sel;
+    // select, not multiply: a sample outside the box (only zero-length samples of missed rays; nerfacc
+    // never produces one) must get sigma = 0 even where exp overflows (inf * 0 = NaN)
+    float sigma = sel != 0.0f ? expf(sig_acc[0] - 1.0f) : 0.0f;
     float r0 = softplus_b1(rgb_acc[0]);
     float r1 = A.rd > 1 ? softplus_b1(rgb_acc[1]) : 0.0f;
     float r2 = A.rd > 2 ? softplus_b1(rgb_acc[2]) : 0.0f;
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
     RayGeom rg = ray_geom(ro, rdv, A.aabb, A.near_p, A.far_p);
     const float ru = A.jitter[r];
     const int spl = A.n_samples / 64;  // samples per lane (1, 2 or 4)
-    float tau[4], tmid[4], loc[4];
+    float tau[4], tmid[4], locx[4];
     float run = 0.0f;
     
 #pragma unroll
@@ -294,21 +296,22 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
       float a0, a1;
       sample_interval(rg, kk, ru, A.n_samples, &a0, &a1);
       float sg = rec_lds[(wave * A.n_samples + kk) * 4];
-      tau[q] = sg * (a1 - a0);
+      // zero-length samples (missed rays) contribute nothing, also where sigma overflowed
+      tau[q] = (a1 > a0) ? sg * (a1 - a0) : 0.0f;
       tmid[q] = (a0 + a1) / 2.0f;
+      locx[q] = run;
       run += tau[q];
-      loc[q] = run;
     }
-    float incl_lane = wave_incl_scan(run);
-    float base = incl_lane - run;
+    // exclusive optical depth as a sum of the preceding terms only (nerfacc's sequential
+    // exclusive cumsum): never incl - tau, which is inf - inf once a sigma overflows
+    float base = wave_excl_scan(run);
     float cs[3] = {0.f, 0.f, 0.f}, op = 0.f, dp = 0.f;
     
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (q >= spl) break;
       int kk = lane * spl + q;
-      float incl = base + loc[q];
-      float excl = incl - tau[q];
+      float excl = base + locx[q];
       float w = expf(-excl) * (1.0f - expf(-tau[q]));
       const float* rc = rec_lds + (wave * A.n_samples + kk) * 4;
       cs[0] += w * rc[1];
@@ -436,7 +439,7 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch)
         if (ch < A.rd) bk_dot += dC[ch] * A.bkgd[ch];
-    float tau[4], tmid[4], dlt[4], loc[4], sg4[4], rc4[4][3];
+    float tau[4], tmid[4], dlt[4], loc[4], locx[4], sg4[4], rc4[4][3];
     float run = 0.0f;
     
 #pragma unroll
@@ -451,21 +454,20 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
       rc4[q][1] = rv[2];
       rc4[q][2] = rv[3];
       dlt[q] = a1 - a0;
-      tau[q] = rv[0] * dlt[q];
+      tau[q] = (a1 > a0) ? rv[0] * dlt[q] : 0.0f;
       tmid[q] = (a0 + a1) / 2.0f;
+      locx[q] = run;
       run += tau[q];
       loc[q] = run;
     }
-    float incl_lane = wave_incl_scan(run);
-    float base = incl_lane - run;
+    float base = wave_excl_scan(run);
     float w[4], gv[4], op_part = 0.0f;
     float wg_run = 0.0f, wgl[4];
     
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (q >= spl) break;
-      float incl = base + loc[q];
-      float excl = incl - tau[q];
+      float excl = base + locx[q];
       w[q] = expf(-excl) * (1.0f - expf(-tau[q]));
       op_part += w[q];
     }

@@ -240,6 +240,9 @@ class RenderFunction(torch.autograd.Function):
                       _ptr(packed.bias), _ptr(bkgd), _ptr(ws), None, None, None)
         gr = RenderGrad(_ptr(g_rgb), _ptr(g_op), _ptr(g_dp), _ptr(grad_flat), _ptr(grad_bkgd))
         _check(lib().den_render_bwd(ctypes.byref(ctx.desc), ctypes.byref(io), ctypes.byref(gr), _stream(dev)))
+        # release the workspace (the activations kept for this backward) as soon as the
+        # stream is done with it: the caching allocator orders the reuse on the same stream
+        ctx.io_keep = None
         return None, None, None, grad_bkgd, grad_flat, None, None, None, None
 
 

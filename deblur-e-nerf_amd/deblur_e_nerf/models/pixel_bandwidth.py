@@ -44,7 +44,9 @@ class PixelBandwidth(torch.nn.Module):
     NS_TO_S = 1e-9
     PARAM_NAMES = ("tau_mil_it_eff_prod", "A_amp_inv", "A_loop_inv", "tau_out", "tau_sf", "tau_diff")
 
-    def __init__(self, dataset_directory, min_ts, f_c_dominant_min, target_cumprob):
+    def __init__(self, dataset_directory, min_ts, f_c_dominant_min, target_cumprob, calibration=None):
+        """``calibration``: the camera_calibration.npz arrays as a dict, instead of
+        reading them from ``dataset_directory``."""
         super().__init__()
         self.omega_c_dominant_min = 2 * math.pi * f_c_dominant_min  # rad/s
         min_ts = min_ts.detach().clone() if torch.is_tensor(min_ts) else torch.tensor(min_ts)
@@ -52,7 +54,7 @@ class PixelBandwidth(torch.nn.Module):
         self.register_buffer("target_cumprob_max_sample_lifetime",
                              torch.tensor(target_cumprob.max_sample_lifetime), persistent=False)
 
-        calib = load_camera_calibration(dataset_directory)
+        calib = calibration if calibration is not None else load_camera_calibration(dataset_directory)
         k_in = torch.from_numpy(np.asarray(calib[self.TAU_IN_IT_EFF_PROD_KEY]))
         k_mil = torch.from_numpy(np.asarray(calib[self.TAU_MIL_IT_EFF_PROD_KEY]))
         a_amp = torch.from_numpy(np.asarray(calib[self.A_AMP_KEY]))

@@ -18,6 +18,7 @@ render background (a scalar parameter transform, as utils/modules.py keeps).
 import ctypes
 import math
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -261,3 +262,159 @@ def synthetic_events(n_events, seed=1234, radius=4.03, rank=0, world=1, img=800,
                 normalized=norm[:, sl].contiguous(), position=pixel[sl], T_wc_position=pos[:, sl].contiguous(),
                 T_wc_orientation=rot4[:, sl].contiguous(), intrinsics_inverse=torch.linalg.inv(K),
                 jitter=jitter[:, sl].reshape(-1).contiguous())
+
+
+# EDS-assumed DVS constants (reference scripts/eds_to_esim.py:68-79), the synthetic sensor
+EDS_CALIBRATION = dict(
+    input_time_const_eff_it_prod=(35e-12 * 25e-3) / 2000e-12,
+    miller_time_const_eff_it_prod=(0.6e-12 * 25e-3) / 2000e-12,
+    amplifier_gain=140.0, closed_loop_gain=1 / 0.7, output_time_const=25e-6,
+    sf_cutoff_freq=16400.0, diff_amp_cutoff_freq=82000.0)
+
+
+class _TargetCumprob(dict):
+    __getattr__ = dict.__getitem__
+
+
+class PixbwTrainStep:
+    """Training step with the pixel-bandwidth model ON (BASELINE.json configs[2];
+    DeblurENeRF.training_step, deblur_e_nerf.py:414-586, with
+    render_log_intensity's pixel-bandwidth branch :1137-1151): per event, each of
+    the 4 supervision timestamps [diff start (reset_diff), diff end, tv start,
+    tv end] becomes S = it_sample_size intensity samples at the sample timestamps
+    of PixelBandwidth.sample_intensity, i.e. S x N rays per render call and
+    4 S N per step; the pixel-bandwidth filter turns them into log-intensities
+    (den_pixbw_*), then the Huber diff + L1 TV losses, backward, all-reduce, Adam.
+
+    Device ops: den_event_prep, den_pixbw_sample_ts, den_pixel_rays,
+    den_render_fwd/bwd, den_pixbw_fwd/bwd, den_event_loss_fwd/bwd, den_adam_step,
+    den_pack_weights, chained by torch.autograd.  The camera trajectory
+    (trajectories.py, SURVEY.md 8(f) #2, not built) is replaced by a synthetic
+    constant-velocity pose per event, evaluated elementwise in torch.
+    """
+
+    def __init__(self, n_events, it_sample_size=16, n_samples=128, radiance_dim=1, mode="bf16", seed=0,
+                 device="cuda", aabb=(-1.5, -1.5, -1.5, 1.5, 1.5, 1.5), near=1.43, far=6.63, lr=0.01,
+                 weight_decay=1e-6, loss_weight=(1.0, 1e-3), error_fn=("huber", "l1"), min_modeled_intensity=1e-3,
+                 mean_contrast_threshold=0.25, min_ts=5e7, calibration=None):
+        from .models.pixel_bandwidth import PixelBandwidth
+        self.N, self.S, self.n_samples, self.rd = n_events, it_sample_size, n_samples, radiance_dim
+        self.mode = nat.mode_id(mode)
+        self.dev = torch.device(device)
+        self.R = 4 * it_sample_size * n_events
+        torch.manual_seed(seed)
+        field = mlp.VanillaNeRFRadianceField(
+            list(aabb), radiance_dim=radiance_dim, hidden_activation=torch.nn.Softplus(beta=100),
+            density_activation=ngp.shifted_trunc_exp, radiance_activation=torch.nn.Softplus(beta=1), mode=mode)
+        self.P = nat.param_count(radiance_dim)
+        self.flat = field.flat_params.detach().to(self.dev).contiguous().requires_grad_(True)
+        self.bkgd_orig = torch.full((radiance_dim,), math.log(math.expm1(1.0)), device=self.dev)
+        self.gbuf = torch.zeros(self.P + radiance_dim, device=self.dev)
+        self.m, self.v = torch.zeros_like(self.gbuf), torch.zeros_like(self.gbuf)
+        self.t, self.lr, self.wd = 0, lr, weight_decay
+        self.wl, self.fn, self.min_int = loss_weight, error_fn, min_modeled_intensity
+        self.c = torch.tensor([mean_contrast_threshold], device=self.dev)
+        self.ct = torch.tensor([mean_contrast_threshold] * 2, device=self.dev)
+        self.tau = torch.zeros(1, dtype=torch.float64, device=self.dev)
+        self.cfg = dict(mode=self.mode, rd=radiance_dim, aabb=list(aabb), near=near, far=far)
+        self.packed = nat.PackedWeights(self.mode, radiance_dim, self.dev)
+        self.packed.pack(self.flat.detach())
+        cal = {k: np.array(v, dtype=np.float32) for k, v in (calibration or EDS_CALIBRATION).items()}
+        self.pb = PixelBandwidth(None, torch.tensor(min_ts), 21.0, _TargetCumprob(max_sample_lifetime=0.95),
+                                 calibration=cal).to(self.dev)
+        for p in self.pb.parameters():
+            p.requires_grad_(False)  # frozen in the synthetic configuration (synthetic.yaml:41-52)
+        self.loss = torch.zeros(3, device=self.dev)
+
+    def load_events(self, num_pos, num_neg, end_ts, start_ts, normalized, interval_gen, position, T_wc_position,
+                    velocity, T_wc_orientation, intrinsics_inverse, jitter, channel=None):
+        """Raw events (see synthetic_pixbw_events): interval_gen (S-1, N) f64 is the
+        datamodule's normalized interval-generator sample (datamodule.py:199-211);
+        the pose of event i at time t is T_wc_position[i] + velocity[i] (t - end_ts[i]) 1e-9,
+        orientation T_wc_orientation[i]; jitter (4, S N)."""
+        d = self.dev
+        i64 = lambda t: t.to(d, torch.int64).contiguous()
+        f32 = lambda t: t.to(d, torch.float32).contiguous()
+        self.ev = dict(num_pos=i64(num_pos), num_neg=i64(num_neg), end_ts=i64(end_ts), start_ts=i64(start_ts))
+        self.norm = normalized.to(d, torch.float64).contiguous()
+        self.gen = interval_gen.to(d, torch.float64).contiguous()
+        self.position, self.p0, self.vel = f32(position), f32(T_wc_position), f32(velocity)
+        self.rot = f32(T_wc_orientation)[None].expand(self.S, self.N, 3, 3).contiguous()
+        self.K_inv = f32(intrinsics_inverse)
+        self.jitter = f32(jitter).reshape(4, self.S * self.N)
+        self.channel = None if channel is None else i64(channel)
+        self.t_ref = self.ev["end_ts"].to(torch.float64)
+
+    def _intensity_fn(self, g, bkgd):
+        S, N = self.S, self.N
+
+        def fn(ts):  # (S, N) f64 clamped sample timestamps -> intensity (S, N) (render_train_pixels)
+            with torch.no_grad():
+                pos = (self.p0 + self.vel * ((ts - self.t_ref) * 1e-9).float()[..., None]).contiguous()
+                o, dr = nat.pixel_rays(self.K_inv, self.position, pos, self.rot)
+            rgb, op, _ = nat.render(o.reshape(-1, 3), dr.reshape(-1, 3), self.jitter[g], bkgd, self.flat,
+                                    self.cfg, self.packed, self.n_samples)
+            if self.rd > 1:  # bayering (deblur_e_nerf.py:1223-1235)
+                rad = rgb.view(S, N, self.rd).gather(2, self.channel.view(1, N, 1).expand(S, N, 1))[..., 0]
+            else:
+                rad = rgb.view(S, N)
+            return (rad + self.min_int,)
+        return fn
+
+    def forward(self):
+        e = self.ev
+        prep = nat.event_prep(e["num_pos"], e["num_neg"], e["end_ts"], e["start_ts"], self.norm, self.ct, self.tau,
+                              norm_c=self.c)
+        # the gradient buffer holds d/d bkgd (post-softplus), as TrainStep's does
+        bkgd = torch.nn.functional.softplus(self.bkgd_orig.detach()).requires_grad_(True)
+        self.bkgd = bkgd
+        y = [self.pb(self.gen, prep["render_ts"][g], self._intensity_fn(g, bkgd), reset_diff=(g == 0))[0]
+             for g in range(4)]
+        Ld = nat.EventLossFunction.apply(y[1] - y[0], prep["target"], self.c, None, self.fn[0])
+        Lt = nat.EventLossFunction.apply(y[3] - y[2], None, self.c, None, self.fn[1])
+        self.total = self.wl[0] * Ld + self.wl[1] * Lt
+        self.loss = torch.stack([Ld.detach(), Lt.detach(), self.total.detach()])
+
+    def backward(self):
+        self.flat.grad = None
+        self.total.backward()
+        self.gbuf[: self.P].copy_(self.flat.grad)
+        self.gbuf[self.P:].copy_(self.bkgd.grad)
+        # drop the step's graph (and the render workspaces it holds) before the next forward
+        self.total = None
+        self.pb.reset_delta_log_it = self.pb.reset_delta_log_it.detach()
+
+    def step(self):
+        self.forward()
+        self.backward()
+        allreduce_mean(self.gbuf)
+        self.t += 1
+        with torch.no_grad():
+            nat.adam_step(self.flat, self.gbuf[: self.P], self.m[: self.P], self.v[: self.P], self.lr, 0.9, 0.999,
+                          1e-8, self.wd, self.t)
+            g = (self.gbuf[self.P:] * torch.sigmoid(self.bkgd_orig.detach())).contiguous()  # softplus chain rule
+            b, bm, bv = self.bkgd_orig.detach(), self.m[self.P:], self.v[self.P:]
+            nat.adam_step(b, g, bm, bv, self.lr, 0.9, 0.999, 1e-8, 0.0, self.t)
+            self.packed.pack(self.flat.detach())
+        return self.loss
+
+
+def synthetic_pixbw_events(n_events, it_sample_size=16, seed=1234, rank=0, world=1, speed=5.0):
+    """synthetic_events plus the pixel-bandwidth inputs: the (S-1, N) interval
+    generator sample (Triangular(0,1) about 0.5, datamodule.py:199-211) and a
+    per-event camera velocity (units/s) for the constant-velocity trajectory;
+    jitter covers the 4 x S x N rays."""
+    S = it_sample_size
+    b = synthetic_events(n_events, seed=seed, rank=rank, world=world)
+    g = torch.Generator().manual_seed(seed + 1)
+    Nt = n_events * world
+    u = torch.rand(S - 1, Nt, generator=g, dtype=torch.float64)
+    gen = torch.where(u < 0.5, torch.sqrt(u / 2), 1 - torch.sqrt((1 - u) / 2))
+    vel = torch.randn(Nt, 3, generator=g) * speed  # units / s
+    jit = torch.rand(4, S, Nt, generator=g)
+    sl = slice(rank * n_events, (rank + 1) * n_events)
+    b.pop("jitter")
+    b["T_wc_position"] = b["T_wc_position"][0].contiguous()   # the pose at end_ts
+    b["T_wc_orientation"] = b["T_wc_orientation"][0].contiguous()
+    b.update(interval_gen=gen[:, sl].contiguous(), velocity=vel[sl], jitter=jit[:, :, sl].reshape(4, -1).contiguous())
+    return b

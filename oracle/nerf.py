@@ -151,9 +151,12 @@ def composite(t0, t1, rgb, sigma, bkgd=None):
     """nerfacc 0.3.1 render_weight_from_density + accumulate_along_rays
     (vol_rendering.py:89-126), rays laid out densely as (R, N).
     rgb (R, N, rd), sigma (R, N) -> colour (R, rd), opacity (R), depth (R) (un-normalised)."""
-    tau = sigma * (t1 - t0)
+    # zero-length samples (a missed ray's) contribute nothing (nerfacc has no such sample)
+    tau = torch.where(t1 > t0, sigma * (t1 - t0), torch.zeros_like(sigma))
     alpha = 1.0 - torch.exp(-tau)
-    excl = torch.cumsum(tau, dim=-1) - tau
+    # exclusive optical depth: a sum of the preceding terms (nerfacc's exclusive cumsum), not
+    # cumsum - tau, which is inf - inf once a sigma overflows
+    excl = torch.cat([torch.zeros_like(tau[..., :1]), torch.cumsum(tau, dim=-1)[..., :-1]], dim=-1)
     w = torch.exp(-excl) * alpha
     colour = (w[..., None] * rgb).sum(dim=-2)
     opacity = w.sum(dim=-1)

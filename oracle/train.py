@@ -66,3 +66,60 @@ def prepare_batch(raw, contrast_thresholds=(0.25, 0.25), refractory_period=0.0):
                                        raw["T_wc_orientation"])
     return dict(rays_o=ro.reshape(-1, 3), rays_d=rdir.reshape(-1, 3), jitter=raw["jitter"], lid=o["lid"],
                 end_ts=raw["end_ts"], start_ts=o["start_ts"], ts_diff=o["diff"][0])
+
+
+def pixbw_step_loss(p, bkgd, raw, it_sample_size, n_samples, prm, min_ts, w=(1.0, 1e-3), min_int=1e-3, mean_ct=0.25,
+                    fn=("huber", "l1"), dt_dtype=torch.float32):
+    """The pixel-bandwidth-on step (deblur_e_nerf.train.PixbwTrainStep layout):
+    event preparation, then for each supervision timestamp group the S sample
+    timestamps, the constant-velocity poses, rays, renders and the pixel-bandwidth
+    filter (oracle/pixbw.py, reset on the diff start), then the losses
+    (deblur_e_nerf.py:472-549 with render_log_intensity :1137-1151)."""
+    from . import events as oev
+    from . import pixbw as opb
+    S, N = it_sample_size, raw["end_ts"].numel()
+    c = torch.tensor(mean_ct)
+    o = oev.event_prep(raw["num_pos"], raw["num_neg"], raw["end_ts"], raw["start_ts"], raw["normalized"], c, c,
+                       torch.tensor(0.0, dtype=torch.float64))
+    ts_diff, d_s, d_e = o["diff"]
+    _, s_s, s_e = o["subdiff"]
+    grad = o["lid"] / (raw["end_ts"] - o["start_ts"])
+    target = (ts_diff * grad / c).to(torch.float32)
+    orc = opb.PixelBandwidthOracle(prm, min_ts, dt_dtype=dt_dtype)
+    t_ref = raw["end_ts"].to(torch.float64)
+    rot = raw["T_wc_orientation"][None].expand(S, N, 3, 3)
+    jit = raw["jitter"].reshape(4, S * N)
+    ys = []
+    for g, tg in enumerate((d_s, d_e, s_s, s_e)):
+        def intensity(ts, g=g):
+            pos = raw["T_wc_position"] + raw["velocity"] * ((ts - t_ref) * 1e-9).float()[..., None]
+            ro, rdir = oev.pixel_params_to_ray(raw["intrinsics_inverse"], raw["position"], pos, rot)
+            col, _, _, _ = onerf.render_rays(p, ro.reshape(-1, 3).to(bkgd.dtype), rdir.reshape(-1, 3).to(bkgd.dtype),
+                                             jit[g].to(bkgd.dtype), n_samples=n_samples, bkgd=bkgd)
+            if raw.get("channel") is not None:
+                ch = raw["channel"].long().view(1, N, 1).expand(S, N, 1)
+                rad = col.view(S, N, -1).gather(2, ch)[..., 0]
+            else:
+                rad = col[:, 0].view(S, N)
+            return rad + min_int
+        ys.append(orc(raw["interval_gen"], tg, intensity, reset_diff=(g == 0)))
+    cc = c.to(ys[0].dtype)
+    Ld = oloss.ERROR_FNS[fn[0]]((ys[1] - ys[0]) / cc, target.to(ys[0].dtype)).mean()
+    Lt = oloss.ERROR_FNS[fn[1]]((ys[3] - ys[2]) / cc, torch.zeros_like(ys[0])).mean()
+    return w[0] * Ld + w[1] * Lt, Ld, Lt
+
+
+def pixbw_flat_grad(p, bkgd_raw, raw, it_sample_size, n_samples, rd, prm, min_ts, **kw):
+    """Gradient of pixbw_step_loss w.r.t. [MLP params | post-softplus bkgd] + loss terms."""
+    names = [n for n, _, _ in onerf.layer_specs(rd)]
+    leaves = []
+    for n in names:
+        leaves += [p[n + ".weight"], p[n + ".bias"]]
+    for t in leaves:
+        t.requires_grad_(True)
+        t.grad = None
+    bk = torch.nn.functional.softplus(bkgd_raw).detach().requires_grad_(True)
+    total, Ld, Lt = pixbw_step_loss(p, bk, raw, it_sample_size, n_samples, prm, min_ts, **kw)
+    total.backward()
+    g = torch.cat([t.grad.reshape(-1) for t in leaves] + [bk.grad.reshape(-1)])
+    return g.detach(), (float(Ld.detach()), float(Lt.detach()), float(total.detach()))

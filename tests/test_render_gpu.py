@@ -181,3 +181,31 @@ def test_render_rejects_bad_shapes():
     o, d, u = synthetic_rays(3, device=DEV)
     with pytest.raises(nat.DenError):
         nat.render(o, d, u, None, flat, _cfg("bf16", 3), packed, 128)  # 3 rays x 128 is not a tile multiple
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+def test_render_survives_density_overflow(mode):
+    """sigma = exp(x - 1) overflows to inf for x > 89 (the reference's trunc_exp
+    forward does too): alpha = 1, the samples behind it get weight 0 and the
+    render stays finite, as nerfacc's sequential exclusive scan does.  Forced
+    here with a huge sigma-head bias; colour/opacity must match the oracle and
+    the gradient stay finite (trunc_exp's backward clamps at 15)."""
+    nat = _nat()
+    rd, S, R = 1, 128, 16
+    o, d, u = synthetic_rays(R, seed=5, jitter_rad=0.05)  # all rays through the box
+    p = onerf.build_params(rd, 0)
+    p["mlp.sigma_layer.output_layer.bias"] = p["mlp.sigma_layer.output_layer.bias"] + 200.0
+    flat = flat_from_params(p, rd).to(DEV).requires_grad_(True)
+    packed = nat.PackedWeights(mode, rd, DEV)
+    packed.pack(flat.detach())
+    bk = torch.ones(rd, device=DEV)
+    c, op, _ = nat.render(o.to(DEV), d.to(DEV), u.to(DEV), bk, flat, _cfg(mode, rd), packed, S)
+    (c.sum() + op.sum()).backward()
+    torch.cuda.synchronize()
+    ref_c, ref_o, _, _ = onerf.render_rays(p, o, d, u, n_samples=S, bkgd=torch.ones(rd))
+    assert torch.isfinite(ref_c).all()  # the oracle's composite handles inf as nerfacc does
+    assert torch.isfinite(c).all() and torch.isfinite(op).all()
+    assert torch.allclose(op.cpu(), torch.ones(R), atol=1e-6)
+    tol = 1e-4 if mode == "f32" else 3e-2
+    assert rel_err(c, ref_c) <= tol
+    assert torch.isfinite(flat.grad).all()

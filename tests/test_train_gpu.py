@@ -158,3 +158,43 @@ def test_missed_rays_stay_finite_over_training():
     assert bool(miss.all())
     bk = ts.bkgd  # the background the last forward composited over (Adam has moved bkgd_orig since)
     assert torch.equal(ts.rgb[:k][miss], bk.expand(int(miss.sum()), 1))
+
+
+@pytest.mark.parametrize("rd", [1, 3])
+def test_pixbw_train_step_matches_oracle(rd):
+    """Pixel-bandwidth-on step (BASELINE configs[2] shape, small): PixbwTrainStep
+    (event prep, sample timestamps, rays, renders, pixel-bandwidth filter, losses,
+    autograd backward through the HIP kernels) against the oracle's step, F32
+    parity mode; losses 1e-4 relative, gradients judged against the f64 oracle
+    as in test_train_step_matches_oracle."""
+    from deblur_e_nerf.train import PixbwTrainStep, synthetic_pixbw_events
+    from oracle import pixbw as opb
+    from oracle.train import pixbw_flat_grad
+    N, S, n_s = 4, 16, 128
+    ts = PixbwTrainStep(N, it_sample_size=S, n_samples=n_s, radiance_dim=rd, mode="f32", device=DEV, seed=9)
+    raw = synthetic_pixbw_events(N, it_sample_size=S, seed=13)
+    if rd == 3:
+        raw["channel"] = torch.randint(0, 3, (N,), generator=torch.Generator().manual_seed(13))
+    ts.load_events(**raw)
+    prm32 = {"tau_in_it_eff_prod": float(ts.pb.tau_in_it_eff_prod)}
+    for pn in opb.PARAM_NAMES:
+        prm32[pn] = float(getattr(ts.pb, pn).detach())
+    min_ts = float(ts.pb.min_ts)
+    p32 = unflat(ts.flat.detach().cpu(), rd)
+    bk = ts.bkgd_orig.detach().cpu()
+    g32, (Ld, Lt, tot) = pixbw_flat_grad({k: v.clone() for k, v in p32.items()}, bk, raw, S, n_s, rd, prm32, min_ts)
+    raw64 = {k: (v.double() if v.is_floating_point() and v.dtype == torch.float32 else v) for k, v in raw.items()}
+    g64, l64 = pixbw_flat_grad({k: v.double() for k, v in p32.items()}, bk.double(), raw64, S, n_s, rd, prm32,
+                               min_ts, dt_dtype=None)
+    ts.forward()
+    ts.backward()
+    torch.cuda.synchronize()
+    loss = ts.loss.cpu().tolist()
+    # the TV term is an L1 of a log-intensity difference of two nearby renders (~1e-4): judged, like the
+    # gradients, against the f64 oracle with the f32 oracle's own error as the floor
+    for a, r32, r64 in zip(loss, (Ld, Lt, tot), l64):
+        assert abs(a - r64) <= max(1e-4 * abs(r64), 4 * abs(r32 - r64)), (loss, (Ld, Lt, tot), l64)
+    g = ts.gbuf.detach().cpu().double()
+    e, e_cpu = norm_rel(g, g64), norm_rel(g32.double(), g64)
+    print(f"[pixbw rd={rd}] loss {loss} vs {(Ld, Lt, tot)}; grad HIP vs f64 {e:.2e}, f32 oracle vs f64 {e_cpu:.2e}")
+    assert e <= max(1e-4, 4 * e_cpu), (e, e_cpu)
