@@ -13,6 +13,8 @@ Pinning status ("Oracle"):
 * radiance field (encoding, MLP, activations)     -- pinned: mlp_rd{1,3}.npz
 * FOH discretisation / pixel-bandwidth model       -- pinned: foh.npz, pixbw_*.npz
 * event-model contrast thresholds / loss           -- pinned: ct.npz, loss.npz
+* event preparation (contrast threshold, refractory
+  delay, diff/subdiff timestamps) and pixel rays   -- pinned: events.npz, rays.npz
 * nerfacc 0.3.1 compositing + fixed-count sampler  -- PARITY UNPINNED (nerfacc is a
   third-party CUDA package absent from /root/reference); restated from its
   documented semantics and cross-checked against a float64 brute-force loop.
