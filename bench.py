@@ -70,7 +70,8 @@ def pmc_traffic(kernel, a):
         with open(path) as f:
             t = json.load(f)
         w = t["workload"]
-        if (w["rays"], w["samples"], w["mode"], w["rd"]) != (a.rays, a.samples, a.mode, a.rd):
+        if (w["rays"], w["samples"], w["mode"], w["rd"], w.get("pixbw", False)) != (a.rays, a.samples, a.mode, a.rd,
+                                                                                   a.pixbw):
             return None
         return t["kernels"][kernel]["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
