@@ -139,8 +139,12 @@ __device__ __forceinline__ float dsoftplus_b100_from_out(float s) {
 // max(t, 0) as v_med3_f32(t, 0, FLT_MAX): fmaxf lowers to maxnum, which makes the compiler
 // canonicalize an MFMA result first (a second v_max_f32 per element in the forward epilogue).
 __device__ __forceinline__ float softplus2_scaled(float t) {
+#ifdef DEN_EXP_CHEAP_ACT  // measurement experiment only (never in libden.so): VALU cost of the epilogue
+  return __builtin_amdgcn_fmed3f(t, 0.0f, 3.4028235e38f);
+#else
   return __builtin_amdgcn_fmed3f(t, 0.0f, 3.4028235e38f) +
          __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(-fabsf(t)));
+#endif
 }
 // its derivative from the output: sigmoid(100 z) = 1 - 2^-s'
 __device__ __forceinline__ float dsoftplus2_scaled_from_out(float s) { return 1.0f - __builtin_amdgcn_exp2f(-s); }

@@ -25,9 +25,11 @@ constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
 constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
 constexpr int HB_SLOT = 2 * HB_BLOCK;  // LDS ring slot: [dz_l block | S'_{l-1} block]
 constexpr int HB_GRID_MAX = 256;
-constexpr int HB_DEPTH = 3;                              // blocks in flight ahead of the computed one
-constexpr int HB_RING = HB_DEPTH + 1;                    // LDS slots (4 x 32 KiB)
-static_assert((HB_RING & (HB_RING - 1)) == 0, "ring index by mask");
+#ifndef DEN_HB_DEPTH
+#define DEN_HB_DEPTH 3
+#endif
+constexpr int HB_DEPTH = DEN_HB_DEPTH;                   // blocks in flight ahead of the computed one
+constexpr int HB_RING = HB_DEPTH + 1;                    // LDS slots (32 KiB each; <= 5 fit in 160 KiB)
 constexpr int HB_DMA_OPS = 2 * (16 / 4);                 // LDS-DMA instructions per wave per block
 constexpr int HB_STORE_OPS = 4;                          // dz_{l-1} stores per wave per block
 // vector-memory ops a wave issues after its DMA of block b+1 by the end of block b (issue order:
@@ -208,9 +210,9 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   asm volatile("" ::: "memory");
 
   for (int64_t b = b0; b < b1; ++b) {
-    const int u = (int)((b - b0) & (HB_RING - 1));
+    const int u = (int)((b - b0) % HB_RING);
     // prefetch block b + HB_DEPTH into the slot block b - 1 used (free since the last barrier)
-    if (b + HB_DEPTH < b1) fetch(b + HB_DEPTH, lds + ((u + HB_DEPTH) & (HB_RING - 1)) * HB_SLOT);
+    if (b + HB_DEPTH < b1) fetch(b + HB_DEPTH, lds + ((u + HB_DEPTH) % HB_RING) * HB_SLOT);
     hb_block(P, lds + u * HB_SLOT, b, wt, dw, db);
     if (b + HB_DEPTH < b1) hb_wait_vm_lgkm0<HB_YOUNGER>();
     else hb_wait_vm_lgkm0<0>();

@@ -105,3 +105,18 @@ def test_allreduce_mean_equals_full_batch_gradient():
     assert torch.allclose(g0[-RD:], g_full[-RD:], rtol=1e-11, atol=1e-20)
     # the mean of the per-rank losses is the full-batch loss
     assert torch.allclose((l0 + l1) / 2, torch.tensor(losses, dtype=torch.float64), rtol=1e-12)
+
+
+def test_pixbw_event_sharding_partitions_the_global_batch():
+    """synthetic_pixbw_events shards whole events, including the interval
+    generators, velocities and the 4 x S x N jitter."""
+    from deblur_e_nerf.train import synthetic_pixbw_events
+    S = 4
+    full = synthetic_pixbw_events(N_PER_RANK * WORLD, S)
+    parts = [synthetic_pixbw_events(N_PER_RANK, S, rank=r, world=WORLD) for r in range(WORLD)]
+    for k in ("num_pos", "end_ts", "start_ts", "position", "T_wc_position", "velocity", "T_wc_orientation"):
+        assert torch.equal(torch.cat([p[k] for p in parts]), full[k]), k
+    for k in ("normalized", "interval_gen"):
+        assert torch.equal(torch.cat([p[k] for p in parts], dim=1), full[k]), k
+    j = torch.cat([p["jitter"].reshape(4, S, N_PER_RANK) for p in parts], dim=2)
+    assert torch.equal(j, full["jitter"].reshape(4, S, -1))
