@@ -432,8 +432,9 @@ def pixel_rays(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientati
     ([M,] N, 3) f32.  Pixels broadcast over the leading render-group dim M."""
     _require_device(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
     ts = (intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
-    if any(t.dtype != torch.float32 or not t.is_contiguous() for t in ts):
-        raise DenError("pixel_rays: expected contiguous f32 tensors")
+    if any(t.dtype != torch.float32 for t in ts):
+        raise DenError("pixel_rays: expected f32 tensors")
+    intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation = (t.contiguous() for t in ts)
     N = pixel_position.shape[0]
     lead = T_wc_position.shape[:-1]
     M = T_wc_position.numel() // (3 * N) if N else 0

@@ -260,7 +260,7 @@ def synthetic_events(n_events, seed=1234, radius=4.03, rank=0, world=1, img=800,
     sl = slice(rank * n_events, (rank + 1) * n_events)
     return dict(num_pos=num_pos[sl], num_neg=1 - num_pos[sl], end_ts=end_ts[sl], start_ts=start_ts[sl],
                 normalized=norm[:, sl].contiguous(), position=pixel[sl], T_wc_position=pos[:, sl].contiguous(),
-                T_wc_orientation=rot4[:, sl].contiguous(), intrinsics_inverse=torch.linalg.inv(K),
+                T_wc_orientation=rot4[:, sl].contiguous(), intrinsics_inverse=torch.linalg.inv(K).contiguous(),
                 jitter=jitter[:, sl].reshape(-1).contiguous())
 
 
