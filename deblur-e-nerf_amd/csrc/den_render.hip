@@ -69,6 +69,74 @@ __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, 
   __syncthreads();
 }
 
+// ---- forward weight ring: FWD_RING slots, chunk t+2 in flight while chunk t is computed.
+// The LDS-DMA is issued through inline asm, so the compiler does not track it (tracked, it makes
+// the first LDS read of every chunk wait vmcnt(0) -- i.e. for the deeper prefetch and for the
+// activation stores too); each step instead waits explicitly for chunk t+1 only:
+// vmcnt(<DMA ops of chunk t+2> + <stores of this step>), both issued after chunk t+1's DMA.
+#ifndef DEN_FWD_RING
+#define DEN_FWD_RING 3
+#endif
+constexpr int FWD_RING = DEN_FWD_RING;
+static_assert(FWD_RING == 2 || FWD_RING == 3, "forward weight ring: 2 or 3 slots");
+
+// per-wave count of DMA instructions dma_chunk issues for `bytes` (wave-uniform)
+__device__ __forceinline__ int dma_ops(int bytes) {
+  const int wave = threadIdx.x >> 6;
+  int n = 0;
+#pragma unroll
+  for (int q = 0; q < (CHUNK_MAX + WG_THREADS * 16 - 1) / (WG_THREADS * 16); ++q)
+    n += (q * WG_THREADS * 16 + wave * 1024 < bytes) ? 1 : 0;
+  return n;
+}
+
+__device__ __forceinline__ void dma_chunk_untracked(const char* g, char* lds_slot, int bytes) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < (CHUNK_MAX + WG_THREADS * 16 - 1) / (WG_THREADS * 16); ++q) {
+    // wave-uniform offset (readfirstlane is 32-bit: never pass it a 64-bit pointer)
+    const int off = __builtin_amdgcn_readfirstlane(q * WG_THREADS * 16 + wave * 1024);
+    if (off < bytes) {
+      const char* base = g + off;
+      const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(lds_slot + off));
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"((uint32_t)lane * 16),
+                   "s"(base), "s"(m0) : "memory", "m0");
+    }
+  }
+}
+
+// s_waitcnt vmcnt(VM) lgkmcnt(0) (gfx9 encoding; expcnt left at its maximum)
+template <int VM>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+  static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | ((VM >> 4) << 14));
+}
+__device__ __forceinline__ void wait_vm_lgkm0_rt(int n) {  // n wave-uniform, 0..7
+  switch (n) {
+    case 0: wait_vm_lgkm0<0>(); break;
+    case 1: wait_vm_lgkm0<1>(); break;
+    case 2: wait_vm_lgkm0<2>(); break;
+    case 3: wait_vm_lgkm0<3>(); break;
+    case 4: wait_vm_lgkm0<4>(); break;
+    case 5: wait_vm_lgkm0<5>(); break;
+    case 6: wait_vm_lgkm0<6>(); break;
+    default: wait_vm_lgkm0<7>(); break;
+  }
+}
+
+// One forward step: issue chunk t+2 into the slot chunk t-1 used (free since the last barrier),
+// run `body` on chunk t (it issues n_st stores), wait for chunk t+1, barrier.
+template <typename Body>
+__device__ __forceinline__ void chunk_step3(char* lds, const char* wbase, int t, int64_t off2, int bytes2, int n_st,
+                                            Body&& body) {
+  if (bytes2 > 0) dma_chunk_untracked(wbase + off2, lds + ((t + 2) % 3) * LDS_BUF, bytes2);
+  body(lds + (t % 3) * LDS_BUF);
+  wait_vm_lgkm0_rt(dma_ops(bytes2) + n_st);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // chunk geometry helpers (forward / backward)
 template <int MODE>
 __device__ __forceinline__ void fwd_next(int l, int i, int64_t* off, int* bytes) {
@@ -77,6 +145,14 @@ __device__ __forceinline__ void fwd_next(int l, int i, int64_t* off, int* bytes)
   if (nl >= NL) { *off = 0; *bytes = 0; return; }
   *bytes = chunk_bytes_K(fwd_K(MODE, nl));
   *off = fwd_layer_offset(MODE, nl) + (int64_t)ni * *bytes;
+}
+// geometry of the chunk two after (l, i)
+template <int MODE>
+__device__ __forceinline__ void fwd_next2(int l, int i, int64_t* off, int* bytes) {
+  int nl = l, ni = i + 1;
+  if (ni >= fwd_tiles(MODE, l)) { nl = l + 1; ni = 0; }
+  if (nl >= NL) { *off = 0; *bytes = 0; return; }
+  fwd_next<MODE>(nl, ni, off, bytes);
 }
 template <int MODE, int LAST_J>
 __device__ __forceinline__ void bwd_next(int j, int i, int64_t* off, int* bytes) {
@@ -139,20 +215,28 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
   Acc prev;
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
-    int64_t noff;
-    int nbytes;
-    fwd_next<MODE>(L, i, &noff, &nbytes);
-    chunk_step(lds, A.w, CB + i, noff, nbytes, [&](const char* chunk) {
+    auto body = [&](const char* chunk) {
       if (i >= 2) fwd_store<MODE, EPI>(A, sample, i - 2, xo, outA);
       Acc acc;
-      const float* bias = (const float*)(lds + 2 * LDS_BUF) + (CB + i) * TM + grp * T::REGS;
+      const float* bias = (const float*)(lds + FWD_RING * LDS_BUF) + (CB + i) * TM + grp * T::REGS;
 #pragma unroll
       for (int r = 0; r < T::REGS; ++r) acc[r] = bias[r];
       mfma_chunk<MODE, KS1>(chunk, x1, acc);
       if constexpr (KS2 > 0) mfma_chunk<MODE, KS2>(chunk + KS1 * TM * T::KI * es_of(MODE), x2, acc);
       if (i > 0) fwd_epilogue<MODE, L, EPI>(A, sample, prev, i - 1, xo, outA, special);
       prev = acc;
-    });
+    };
+    int64_t noff;
+    int nbytes;
+    if constexpr (FWD_RING == 3) {
+      fwd_next2<MODE>(L, i, &noff, &nbytes);
+      // stores the body issues: fwd_store of tile i-2 (2 bf16 / 1 f32 instructions per tile)
+      const bool st = A.train && i >= 2 && (EPI == 0 || (EPI == 1 && i - 2 < WIDTH / TM));
+      chunk_step3(lds, A.w, CB + i, noff, nbytes, st ? (MODE == 1 ? 2 : 1) : 0, body);
+    } else {
+      fwd_next<MODE>(L, i, &noff, &nbytes);
+      chunk_step(lds, A.w, CB + i, noff, nbytes, body);
+    }
   }
   fwd_epilogue<MODE, L, EPI>(A, sample, prev, NT - 1, xo, outA, special);
   if constexpr (NT >= 2) fwd_store<MODE, EPI>(A, sample, NT - 2, xo, outA);
@@ -169,8 +253,8 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
   constexpr bool EXACT = MODE == 0;
   constexpr int WGS = wg_samples(MODE);
   constexpr int NBIAS = (int)bias_floats(MODE);
-  __shared__ __attribute__((aligned(16))) char lds[2 * LDS_BUF + NBIAS * 4 + WGS * 16];
-  float* bias_lds = (float*)(lds + 2 * LDS_BUF);
+  __shared__ __attribute__((aligned(16))) char lds[FWD_RING * LDS_BUF + NBIAS * 4 + WGS * 16];
+  float* bias_lds = (float*)(lds + FWD_RING * LDS_BUF);
   float* rec_lds = bias_lds + NBIAS;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -179,9 +263,17 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
   const int64_t ray = sample / A.n_samples;
   const int k = (int)(sample - ray * A.n_samples);
 
-  // prologue: whole bias table -> LDS, chunk 0 -> slot 0
+  // prologue: whole bias table -> LDS, chunk 0 -> slot 0 (and chunk 1 -> slot 1 with the 3-slot ring)
   for (int q = threadIdx.x; q < NBIAS; q += WG_THREADS) bias_lds[q] = A.bias[q];
-  dma_chunk(A.w, lds, chunk_bytes_K(fwd_K(MODE, 0)));
+  if constexpr (FWD_RING == 3) {
+    dma_chunk_untracked(A.w, lds, chunk_bytes_K(fwd_K(MODE, 0)));
+    int64_t off1;
+    int bytes1;
+    fwd_next<MODE>(0, 0, &off1, &bytes1);
+    dma_chunk_untracked(A.w + off1, lds + LDS_BUF, bytes1);
+  } else {
+    dma_chunk(A.w, lds, chunk_bytes_K(fwd_K(MODE, 0)));
+  }
 
   float o[3], d[3], xc[3], sel;
   if (A.points) {
@@ -215,6 +307,7 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
     if (A.train) store_tile_vals<MODE>(act_ptr(A, A_PE, sample, p), a);
     acc_to_frags<MODE>(a, pe + p * FPT);
   }
+  if constexpr (FWD_RING == 3) wait_vm_lgkm0<0>();  // the untracked prologue DMAs landed
   __syncthreads();
 
   constexpr int KS = WIDTH / T::KI;  // k-steps of a 256-wide input
