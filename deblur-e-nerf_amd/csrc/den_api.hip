@@ -126,9 +126,10 @@ int check_desc(const den_render_desc* d) {
   if (d->n_rays <= 0) return fail(DEN_EINVAL, "n_rays must be > 0");
   const int wgs = wg_samples(d->mode);
   if (d->n_samples < 64 || d->n_samples > wgs || wgs % d->n_samples != 0)
-    return fail(DEN_EUNSUPPORTED, "n_samples must be 64..WG tile (128 F32 / 256 BF16) and divide it");
-  if (((int64_t)d->n_rays * d->n_samples) % wgs != 0)
-    return fail(DEN_EUNSUPPORTED, "n_rays * n_samples must be a multiple of the workgroup tile");
+    return fail(DEN_EUNSUPPORTED, "n_samples must be 64..128 (F32) / 64..256 (BF16) and divide it");
+  if (((int64_t)d->n_rays * d->n_samples) % std::max(wgs, fwd_wg_samples(d->mode)) != 0)
+    return fail(DEN_EUNSUPPORTED, "n_rays * n_samples must be a multiple of the workgroup tile "
+                                  "(den_render_tile_samples)");
   return DEN_OK;
 }
 
@@ -249,7 +250,8 @@ int render_fwd_impl(const den_render_desc* d, const den_render_io* io, hipStream
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
   {
     DEN_TIMED(T_RENDER_FWD, s);
-    hipLaunchKernelGGL(render_fwd_kernel<MODE>, dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s, A);
+    hipLaunchKernelGGL(render_fwd_kernel<MODE>, dim3((unsigned)(n / fwd_wg_samples(MODE))), dim3(fwd_threads(MODE)),
+                       0, s, A);
   }
   DEN_LAUNCHED();
   return DEN_OK;
@@ -324,6 +326,10 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
 extern "C" {
 
 int den_version(void) { return DEN_VERSION; }
+
+int32_t den_render_tile_samples(int32_t mode) {
+  return (mode == 0 || mode == 1) ? std::max(wg_samples(mode), fwd_wg_samples(mode)) : -1;
+}
 
 int den_timing_enable(int32_t on) {
   std::lock_guard<std::mutex> g(g_timing_mu);

@@ -80,22 +80,36 @@ __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, 
 constexpr int FWD_RING = DEN_FWD_RING;
 static_assert(FWD_RING == 2 || FWD_RING == 3, "forward weight ring: 2 or 3 slots");
 
-// per-wave count of DMA instructions dma_chunk issues for `bytes` (wave-uniform)
+// BF16 forward workgroup: DEN_FWD_WAVES_BF16 waves (32 samples each) share one weight stream.
+// Every workgroup streams the whole packed MLP (1.2 MB) through LDS, so samples per workgroup set
+// the L2 -> LDS weight traffic (78 GB per 2^24-sample step at 256 per workgroup).  Measured: 16
+// waves (one workgroup per CU, half the weight traffic) take 38.4 ms against 28.0 ms for 8 waves
+// (two workgroups per CU whose chunk barriers interleave), so 8 stays.
+#ifndef DEN_FWD_WAVES_BF16
+#define DEN_FWD_WAVES_BF16 8
+#endif
+DEN_HD constexpr int fwd_waves(int mode) { return mode == 1 ? DEN_FWD_WAVES_BF16 : 8; }
+DEN_HD constexpr int fwd_threads(int mode) { return 64 * fwd_waves(mode); }
+DEN_HD constexpr int fwd_wg_samples(int mode) { return fwd_waves(mode) * tm_of(mode); }
+static_assert(FWD_RING == 3 || DEN_FWD_WAVES_BF16 == 8, "the 2-slot ring's tracked DMA assumes 512 threads");
+
+// per-wave count of DMA instructions dma_chunk_untracked<NTH> issues for `bytes` (wave-uniform)
+template <int NTH>
 __device__ __forceinline__ int dma_ops(int bytes) {
   const int wave = threadIdx.x >> 6;
   int n = 0;
 #pragma unroll
-  for (int q = 0; q < (CHUNK_MAX + WG_THREADS * 16 - 1) / (WG_THREADS * 16); ++q)
-    n += (q * WG_THREADS * 16 + wave * 1024 < bytes) ? 1 : 0;
+  for (int q = 0; q < (CHUNK_MAX + NTH * 16 - 1) / (NTH * 16); ++q) n += (q * NTH * 16 + wave * 1024 < bytes) ? 1 : 0;
   return n;
 }
 
+template <int NTH>
 __device__ __forceinline__ void dma_chunk_untracked(const char* g, char* lds_slot, int bytes) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int q = 0; q < (CHUNK_MAX + WG_THREADS * 16 - 1) / (WG_THREADS * 16); ++q) {
+  for (int q = 0; q < (CHUNK_MAX + NTH * 16 - 1) / (NTH * 16); ++q) {
     // wave-uniform offset (readfirstlane is 32-bit: never pass it a 64-bit pointer)
-    const int off = __builtin_amdgcn_readfirstlane(q * WG_THREADS * 16 + wave * 1024);
+    const int off = __builtin_amdgcn_readfirstlane(q * NTH * 16 + wave * 1024);
     if (off < bytes) {
       const char* base = g + off;
       const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(lds_slot + off));
@@ -126,12 +140,12 @@ __device__ __forceinline__ void wait_vm_lgkm0_rt(int n) {  // n wave-uniform, 0.
 
 // One forward step: issue chunk t+2 into the slot chunk t-1 used (free since the last barrier),
 // run `body` on chunk t (it issues n_st stores), wait for chunk t+1, barrier.
-template <typename Body>
+template <int NTH, typename Body>
 __device__ __forceinline__ void chunk_step3(char* lds, const char* wbase, int t, int64_t off2, int bytes2, int n_st,
                                             Body&& body) {
-  if (bytes2 > 0) dma_chunk_untracked(wbase + off2, lds + ((t + 2) % 3) * LDS_BUF, bytes2);
+  if (bytes2 > 0) dma_chunk_untracked<NTH>(wbase + off2, lds + ((t + 2) % 3) * LDS_BUF, bytes2);
   body(lds + (t % 3) * LDS_BUF);
-  wait_vm_lgkm0_rt(dma_ops(bytes2) + n_st);
+  wait_vm_lgkm0_rt(dma_ops<NTH>(bytes2) + n_st);
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -232,7 +246,7 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
       fwd_next2<MODE>(L, i, &noff, &nbytes);
       // stores the body issues: fwd_store of tile i-2 (2 bf16 / 1 f32 instructions per tile)
       const bool st = A.train && i >= 2 && (EPI == 0 || (EPI == 1 && i - 2 < WIDTH / TM));
-      chunk_step3(lds, A.w, CB + i, noff, nbytes, st ? (MODE == 1 ? 2 : 1) : 0, body);
+      chunk_step3<fwd_threads(MODE)>(lds, A.w, CB + i, noff, nbytes, st ? (MODE == 1 ? 2 : 1) : 0, body);
     } else {
       fwd_next<MODE>(L, i, &noff, &nbytes);
       chunk_step(lds, A.w, CB + i, noff, nbytes, body);
@@ -245,13 +259,14 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
 
 // ------------------------------------------------------------------ forward kernel
 template <int MODE>
-__global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) {
+__global__ __launch_bounds__(fwd_threads(MODE), 1024 / fwd_threads(MODE)) void render_fwd_kernel(RenderArgs<MODE> A) {
   using T = Tr<MODE>;
   using Frag = typename T::Frag;
   using Acc = typename T::Acc;
   constexpr int TM = T::TM, FPT = T::FPT, REGS = T::REGS;
   constexpr bool EXACT = MODE == 0;
-  constexpr int WGS = wg_samples(MODE);
+  constexpr int WGS = fwd_wg_samples(MODE);
+  constexpr int NTH = fwd_threads(MODE);
   constexpr int NBIAS = (int)bias_floats(MODE);
   __shared__ __attribute__((aligned(16))) char lds[FWD_RING * LDS_BUF + NBIAS * 4 + WGS * 16];
   float* bias_lds = (float*)(lds + FWD_RING * LDS_BUF);
@@ -264,13 +279,13 @@ __global__ __launch_bounds__(512, 2) void render_fwd_kernel(RenderArgs<MODE> A) 
   const int k = (int)(sample - ray * A.n_samples);
 
   // prologue: whole bias table -> LDS, chunk 0 -> slot 0 (and chunk 1 -> slot 1 with the 3-slot ring)
-  for (int q = threadIdx.x; q < NBIAS; q += WG_THREADS) bias_lds[q] = A.bias[q];
+  for (int q = threadIdx.x; q < NBIAS; q += NTH) bias_lds[q] = A.bias[q];
   if constexpr (FWD_RING == 3) {
-    dma_chunk_untracked(A.w, lds, chunk_bytes_K(fwd_K(MODE, 0)));
+    dma_chunk_untracked<NTH>(A.w, lds, chunk_bytes_K(fwd_K(MODE, 0)));
     int64_t off1;
     int bytes1;
     fwd_next<MODE>(0, 0, &off1, &bytes1);
-    dma_chunk_untracked(A.w + off1, lds + LDS_BUF, bytes1);
+    dma_chunk_untracked<NTH>(A.w + off1, lds + LDS_BUF, bytes1);
   } else {
     dma_chunk(A.w, lds, chunk_bytes_K(fwd_K(MODE, 0)));
   }

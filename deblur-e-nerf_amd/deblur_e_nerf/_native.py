@@ -43,6 +43,7 @@ _lib = None
 
 _SIGS = {
     "den_version": (ctypes.c_int, []),
+    "den_render_tile_samples": (ctypes.c_int32, [ctypes.c_int32]),
     "den_last_error": (ctypes.c_char_p, []),
     "den_timing_enable": (ctypes.c_int, [ctypes.c_int32]),
     "den_timing_collect": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
@@ -187,7 +188,8 @@ def _desc(cfg, n_rays, n_samples, train, has_bkgd, points=False):
 
 
 def wg_samples(mode):
-    return 128 if mode_id(mode) == MODE_F32 else 256
+    """Samples per render workgroup tile: n_rays * n_samples must be a multiple."""
+    return int(lib().den_render_tile_samples(mode_id(mode)))
 
 
 def render_workspace_bytes(desc):
@@ -259,10 +261,11 @@ def field(points, dirs, flat, cfg, packed):
     if pad:
         points = torch.cat([points, points.new_zeros(pad, 3)])
         dirs = torch.cat([dirs, dirs.new_zeros(pad, 3) + torch.tensor([0.0, 0.0, 1.0], device=dirs.device)])
-    # "rays" of `tile` points each; the jitter buffer is unused in point mode
+    # "rays" of `group` points each (<= the per-ray sample limit); the jitter buffer is unused in point mode
+    group = min(tile, 128 if mode_id(cfg["mode"]) == MODE_F32 else 256)
     dummy = torch.zeros(points.shape[0], device=points.device)
     rgb, sig, _ = RenderFunction.apply(points.contiguous(), dirs.contiguous(), dummy, None, flat, cfg, packed,
-                                       tile, True)
+                                       group, True)
     return rgb[:n], sig[:n]
 
 

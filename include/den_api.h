@@ -72,8 +72,9 @@ typedef struct den_render_desc {
   int32_t mode;            /* den_mode */
   int32_t radiance_dim;    /* 1 or 3 */
   int32_t n_rays;          /* rays in this call */
-  int32_t n_samples;       /* samples per ray, fixed count; must divide the
-                              workgroup tile (128 samples in F32 mode, 256 in BF16) */
+  int32_t n_samples;       /* samples per ray, fixed count, 64..(128 F32 / 256 BF16),
+                              dividing it; n_rays * n_samples a multiple of
+                              den_render_tile_samples(mode) */
   float aabb[6];           /* min xyz, max xyz (nerf.py:212, AABB contraction) */
   float near_plane;        /* < 0 => none */
   float far_plane;         /* < 0 => none */
@@ -114,6 +115,9 @@ typedef struct den_render_grad {
 } den_render_grad;
 
 int den_version(void);
+/* Samples per render workgroup tile: n_rays * n_samples must be a multiple of it
+ * (128 in F32 mode, 512 in BF16 mode). */
+int32_t den_render_tile_samples(int32_t mode);
 const char* den_last_error(void);
 
 /* Kernel timing, for measurement only (bench.py's roofline).  While enabled,
