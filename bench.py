@@ -116,6 +116,22 @@ def phase_times(ts, reps=PHASE_REPS):
     return {k: v / reps for k, v in acc.items()}
 
 
+def measured_gemm_peak(dev, dtype, n=8192, reps=10):
+    """Achievable dense-GEMM rate on this box (torch.matmul -> hipBLASLt), TFLOP/s:
+    the measured denominator SURVEY.md 8(d) asks for beside the spec peak."""
+    a = torch.randn(n, n, device=dev, dtype=dtype)
+    b = torch.randn(n, n, device=dev, dtype=dtype)
+    for _ in range(3):
+        a @ b
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        a @ b
+    e1.record()
+    torch.cuda.synchronize()
+    return round(2.0 * n ** 3 * reps / (e0.elapsed_time(e1) * 1e-3) / 1e12, 1)
+
+
 def cpu_baseline(n_rays, n_samples, rd, threads):
     """The oracle (PyTorch-CPU restatement of the reference path) timed on a
     bounded sample: n_rays rays through render fwd + event loss + backward +
@@ -268,6 +284,10 @@ def main():
     roofline.update(kernel=dom, avg_launch_ms=de["avg_ms"], timing="hipEvents on the launch stream (den_timing_*)")
     step_flop = 3.0 * 2.0 * MAC_PER_SAMPLE[a.rd] * n_local
     roofline["step_mfma_frac"] = round(step_flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.mode], 4)
+    if rank == 0:
+        gp = measured_gemm_peak(dev, torch.bfloat16 if a.mode == "bf16" else torch.float32)
+        roofline["mfma_peak_measured"] = {"tflops": gp, "how": "torch.matmul 8192^3 (hipBLASLt), HIP events",
+                                          "step_frac": round(step_flop / (ms * 1e-3) / 1e12 / gp, 4)}
     roofline["kernels"] = kernels
     roofline["phases_ms"] = {k: round(v, 3) for k, v in phases.items()}
 
