@@ -50,6 +50,11 @@ def test_host_queries():
     assert nat.param_count(3) == 595844
     assert nat.param_count(1) == 595844 - 2 * 129
     assert L.den_packed_fwd_bytes(nat.MODE_BF16) > 0 and L.den_packed_fwd_bytes(nat.MODE_F32) > 0
+    # render tile: the bench's 2^17 x 128 samples and its 8-way shard must tile it
+    for mode in (nat.MODE_F32, nat.MODE_BF16):
+        tile = L.den_render_tile_samples(mode)
+        assert tile in (128, 256, 512) and (131072 * 128 // 8) % tile == 0
+    assert L.den_render_tile_samples(7) == -1
 
 
 def test_invalid_shapes_fail_with_error_text():
