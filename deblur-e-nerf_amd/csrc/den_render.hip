@@ -83,8 +83,8 @@ static_assert(FWD_RING == 2 || FWD_RING == 3, "forward weight ring: 2 or 3 slots
 // BF16 forward workgroup: DEN_FWD_WAVES_BF16 waves (32 samples each) share one weight stream.
 // Every workgroup streams the whole packed MLP (1.2 MB) through LDS, so samples per workgroup set
 // the L2 -> LDS weight traffic (78 GB per 2^24-sample step at 256 per workgroup).  Measured: 16
-// waves (one workgroup per CU, half the weight traffic) take 38.4 ms against 28.0 ms for 8 waves
-// (two workgroups per CU whose chunk barriers interleave), so 8 stays.
+// waves (half the weight traffic) take 38.4 ms against 28.0 ms for 8 waves: the 8-wave kernel holds
+// 202 VGPRs per wave (one workgroup per CU), and 16 waves per workgroup cap a wave at 128.
 #ifndef DEN_FWD_WAVES_BF16
 #define DEN_FWD_WAVES_BF16 8
 #endif
