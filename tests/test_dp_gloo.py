@@ -37,7 +37,16 @@ def _f64(b):
     return {k: (v.double() if v.is_floating_point() else v) for k, v in b.items()}
 
 
-def _worker(rank, world, port, out):
+def _batch(rank, world, raw):
+    from deblur_e_nerf.train import synthetic_batch, synthetic_events
+    from oracle.train import prepare_batch
+    if raw:  # raw events sharded per rank, prepared (event prep + rays) per rank as the GPU step does
+        return _f64(prepare_batch(synthetic_events(N_PER_RANK,
+                                                   rank=rank, world=world), (0.27, 0.22), 1500.0))
+    return _f64(synthetic_batch(N_PER_RANK, rank=rank, world=world))
+
+
+def _worker(rank, world, port, out, raw=False):
     import sys
     from conftest import PKG, ROOT
     for p in (ROOT, PKG):
@@ -46,9 +55,9 @@ def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from deblur_e_nerf.train import allreduce_mean, synthetic_batch
+    from deblur_e_nerf.train import allreduce_mean
     from oracle.train import flat_grad
-    b = _f64(synthetic_batch(N_PER_RANK, rank=rank, world=world))
+    b = _batch(rank, world, raw)
     g, losses = flat_grad(_params(), torch.zeros(RD, dtype=torch.float64), b, S, RD)
     allreduce_mean(g)
     out[rank] = (g, torch.tensor(losses, dtype=torch.float64), b["end_ts"].clone())
@@ -83,18 +92,24 @@ def test_raw_event_sharding_partitions_the_global_batch():
 
 
 @pytest.mark.timeout(300)
-def test_allreduce_mean_equals_full_batch_gradient():
-    from deblur_e_nerf.train import synthetic_batch
+@pytest.mark.parametrize("raw", [False, True])
+def test_allreduce_mean_equals_full_batch_gradient(raw):
     from oracle.train import flat_grad
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(WORLD, port, out), nprocs=WORLD, join=True)
+    mp.spawn(_worker, args=(WORLD, port, out, raw), nprocs=WORLD, join=True)
     g0, l0, e0 = out[0]
     g1, l1, e1 = out[1]
     assert not torch.equal(e0, e1)           # ranks saw different events
     assert torch.equal(g0, g1)               # identical averaged gradient on every rank
-    full = _f64(synthetic_batch(N_PER_RANK * WORLD))
+    if raw:
+        from deblur_e_nerf.train import synthetic_events
+        from oracle.train import prepare_batch
+        full = _f64(prepare_batch(synthetic_events(N_PER_RANK * WORLD), (0.27, 0.22), 1500.0))
+    else:
+        from deblur_e_nerf.train import synthetic_batch
+        full = _f64(synthetic_batch(N_PER_RANK * WORLD))
     g_full, losses = flat_grad(_params(), torch.zeros(RD, dtype=torch.float64), full, S, RD)
     rel = float((g0 - g_full).norm() / g_full.norm())
     assert rel < 1e-12, rel
