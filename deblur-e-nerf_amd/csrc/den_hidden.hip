@@ -25,6 +25,9 @@ constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
 constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
 constexpr int HB_SLOT = 2 * HB_BLOCK;  // LDS ring slot: [dz_l block | S'_{l-1} block]
 constexpr int HB_GRID_MAX = 256;
+#ifndef DEN_HB_NT
+#define DEN_HB_NT 1  // non-temporal dz_l / S'_{l-1} loads and dz_{l-1} stores (streamed once)
+#endif
 #ifndef DEN_HB_DEPTH
 #define DEN_HB_DEPTH 3
 #endif
@@ -85,8 +88,13 @@ __device__ __forceinline__ void hb_dma_untracked(const char* src, char* dst) {
     const int pc = __builtin_amdgcn_readfirstlane(q * HB_WAVES + wave);
     const char* base = src + pc * 1024;
     const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(dst + pc * 1024));
+#if DEN_HB_NT
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"((pc & 1) ? off1 : off0),
+                 "s"(base), "s"(m0) : "memory", "m0");
+#else
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"((pc & 1) ? off1 : off0),
                  "s"(base), "s"(m0) : "memory", "m0");
+#endif
   }
 }
 
@@ -148,8 +156,13 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     bf16x8 of[2];
     acc_to_frags<1>(acc, of);
     char* d = P.dz_out + (b * 8 + 2 * wave + t) * HB_TILE + lane * 16;
+#if DEN_HB_NT
+    __builtin_nontemporal_store(of[0], (bf16x8*)d);
+    __builtin_nontemporal_store(of[1], (bf16x8*)(d + 1024));
+#else
     *(bf16x8*)d = of[0];
     *(bf16x8*)(d + 1024) = of[1];
+#endif
     // keep the scheduler from hoisting the next phase's LDS reads here (register pressure: W^T lives
     // in 128 VGPRs and dW in all 256 AGPRs for the whole launch)
     __builtin_amdgcn_sched_barrier(0);
