@@ -70,13 +70,38 @@ __device__ __forceinline__ typename Tr<MODE>::Acc acc_zero() {
 // so every store / load instruction of a wave moves 1 KiB of consecutive bytes.
 // `tile` is the (wave-uniform) base of the tile; each lane adds its own offset.
 
+// Activation / dz tiles are written once and read once, by a later kernel, after far more data
+// than the caches hold: BF16 stores and loads of them go non-temporal (DEN_NT_STREAMS).
+#ifndef DEN_NT_STREAMS
+#define DEN_NT_STREAMS 1
+#endif
+typedef unsigned int den_u32x4 __attribute__((ext_vector_type(4)));
+template <typename V>
+__device__ __forceinline__ void st_stream(V* p, V v) {
+#if DEN_NT_STREAMS
+  static_assert(sizeof(V) == 16, "16-byte streams");
+  __builtin_nontemporal_store(__builtin_bit_cast(den_u32x4, v), (den_u32x4*)p);
+#else
+  *p = v;
+#endif
+}
+template <typename V>
+__device__ __forceinline__ V ld_stream(const V* p) {
+#if DEN_NT_STREAMS
+  static_assert(sizeof(V) == 16, "16-byte streams");
+  return __builtin_bit_cast(V, __builtin_nontemporal_load((const den_u32x4*)p));
+#else
+  return *p;
+#endif
+}
+
 // Store a lane's operand fragments of one tile (stored order: regs 0..REGS-1).
 template <int MODE>
 __device__ __forceinline__ void store_tile_frags(void* tile, const typename Tr<MODE>::Frag* f) {
   char* p = (char*)tile + (threadIdx.x & 63) * 16;
   if constexpr (MODE == 1) {
-    *(bf16x8*)p = f[0];
-    *(bf16x8*)(p + 1024) = f[1];
+    st_stream((bf16x8*)p, f[0]);
+    st_stream((bf16x8*)(p + 1024), f[1]);
   } else {
     f32x4 v = {f[0], f[1], f[2], f[3]};
     *(f32x4*)p = v;
@@ -94,8 +119,8 @@ __device__ __forceinline__ void store_tile_vals(void* tile, const typename Tr<MO
       __bf16 lo = (__bf16)a[2 * q], hi = (__bf16)a[2 * q + 1];
       w[q] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
     }
-    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
-    *(uint4*)(p + 1024) = make_uint4(w[4], w[5], w[6], w[7]);
+    st_stream((uint4*)p, make_uint4(w[0], w[1], w[2], w[3]));
+    st_stream((uint4*)(p + 1024), make_uint4(w[4], w[5], w[6], w[7]));
   } else {
     *(f32x4*)p = a;
   }
@@ -106,7 +131,7 @@ __device__ __forceinline__ typename Tr<MODE>::Acc load_tile_vals(const void* til
   typename Tr<MODE>::Acc a;
   const char* p = (const char*)tile + (threadIdx.x & 63) * 16;
   if constexpr (MODE == 1) {
-    uint4 u0 = *(const uint4*)p, u1 = *(const uint4*)(p + 1024);
+    uint4 u0 = ld_stream((const uint4*)p), u1 = ld_stream((const uint4*)(p + 1024));
     uint32_t w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
 #pragma unroll
     for (int q = 0; q < 8; ++q) {

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64 * MT * WN) void dw_gemm_kernel(DwArgs P) {
         const char* src;
         char* dst;
         const int row = unit(u, k0, &src, &dst, lds);
-        if (k0 + row < k_end) v = *(const uint4*)src;
+        if (k0 + row < k_end) v = MODE == 1 ? ld_stream((const uint4*)src) : *(const uint4*)src;
       }
       st[q] = v;
     }
