@@ -44,19 +44,36 @@ def parse():
     ap.add_argument("--rd", type=int, default=1)
     ap.add_argument("--mode", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gemm-peak", action="store_true", help="skip the hipBLASLt reference GEMM (profiling runs)")
     ap.add_argument("--pixbw", action="store_true",
                     help="BASELINE configs[2]: pixel-bandwidth model on (it_sample_size = --it-samples)")
     ap.add_argument("--it-samples", type=int, default=16)
-    ap.add_argument("--cpu-rays", type=int, default=2048, help="rays of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-rays", type=int, default=2048,
+                    help="rays of the bounded pixel-bandwidth-on CPU-baseline sample (--pixbw)")
     return ap.parse_args()
 
 
 PHASE_REPS = 3
-# algorithmic HBM bytes per sample and STEP of each render-path kernel class, BF16 layout
-# (DESIGN.md section 4): hidden_bwd: 7 launches (L7..L1), each reading dz_l + a_(l-1) and writing
-# dz_(l-1), 256 bf16 each = 1536 B; render_fwd: the activations + record it stores for the
-# backward; render_bwd: head activations read + dz written; dw_gemm: the dz/x operand streams of the
-# split-K GEMMs of L0, L5-pe, Lb, sigma, Lg, Lr.  Per launch = per step / launches per step.
+# Algorithmic work of each render-path kernel class per sample and STEP (BF16 layout, DESIGN.md
+# section 4), rd = 1 (rd = 3 adds 2 x 128 MACs to the forward and to the head backward).
+#   render_fwd : the forward MLP, 2 x 593,152 MAC
+#   render_bwd : compositing adjoint + the head chain Lr^T (rd x 128), Lg^T (128 x 256, bottleneck
+#                part only), Lb^T (257 x 256): dX only
+#   hidden_bwd : 7 launches (L7..L1), each dX (256 x 256) + dW (256 x 256) MACs
+#   dw_gemm    : the weight gradients of L0 (256 x 63), L5's pe columns (256 x 63), Lb (256 x 256),
+#                sigma (256), Lg (128 x 283), Lr (rd x 128)
+# FLOP = 2 x MAC.  Per launch = per step / launches per step.
+def flop_per_sample(rd):
+    return {"render_fwd_kernel": 2.0 * MAC_PER_SAMPLE[rd],
+            "render_bwd_kernel": 2.0 * (rd * 128 + 128 * 256 + 257 * 256),
+            "hidden_bwd_kernel": 2.0 * 7 * 2 * 256 * 256,
+            "dw_gemm_kernel": 2.0 * (256 * 63 * 2 + 256 * 256 + 256 + 128 * 283 + rd * 128)}
+
+
+# algorithmic HBM bytes per sample and STEP of each kernel class, BF16 layout:
+# hidden_bwd: 7 launches (L7..L1), each reading dz_l + a_(l-1) and writing dz_(l-1), 256 bf16 each =
+# 1536 B; render_fwd: the activations + record it stores for the backward; render_bwd: head
+# activations read + dz written; dw_gemm: the dz/x operand streams of the split-K GEMMs.
 BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "render_fwd_kernel": 5072, "render_bwd_kernel": 2192,
                     "dw_gemm_kernel": 4032}
 
@@ -132,44 +149,84 @@ def measured_gemm_peak(dev, dtype, n=8192, reps=10):
     return round(2.0 * n ** 3 * reps / (e0.elapsed_time(e1) * 1e-3) / 1e12, 1)
 
 
-def cpu_baseline(n_rays, n_samples, rd, threads):
-    """The oracle (PyTorch-CPU restatement of the reference path) timed on a
-    bounded sample: n_rays rays through render fwd + event loss + backward +
-    Adam (the same step as the GPU line, fewer rays)."""
+def _cpu_info(threads):
+    """CPU model (/proc/cpuinfo, as lscpu reports it), cores visible and used, torch version."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return dict(cpu_model=model, cores_visible=len(os.sched_getaffinity(0)), torch=torch.__version__,
+                threads=threads)
+
+
+def cpu_threads():
+    """All cores of this process's affinity mask, capped by the
+    OMP_NUM_THREADS share the GPU box assigns to one GPU's job."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+
+
+def _time_median(fn, warmup, reps):
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2], ts
+
+
+def cpu_baseline(rd, threads, legs=((4096, 64, 2, 5), (4096, 128, 1, 3))):
+    """The oracle (PyTorch-CPU restatement of the reference path, parity-checked
+    against the reference modules) timed on the host cores: one full train step
+    (event prep + rays + render fwd + event loss + backward + Adam) per leg.
+    Leg 0 is BASELINE configs[0] (chair easy, 4096 rays x 64 samples; median of 5
+    after 2 warm-ups); leg 1 is the benchmark's 2^17 x 128
+    workload scaled down to 4096 x 128 (median of 3 after 1 warm-up, bounded)."""
     from oracle import nerf as onerf
     from oracle.train import prepare_batch, step_loss
     from deblur_e_nerf.train import synthetic_events
     torch.set_num_threads(threads)
-    N = n_rays // 4
-    raw = synthetic_events(N, seed=99)
-    p = onerf.build_params(rd, 0)
-    params = list(p.values())
-    for t in params:
-        t.requires_grad_(True)
-    bk = torch.tensor([0.5413] * rd, requires_grad=True)
-    opt = torch.optim.Adam([{"params": params, "weight_decay": 1e-6}, {"params": [bk]}], lr=0.01)
+    out = []
+    for n_rays, n_samples, warm, reps in legs:
+        raw = synthetic_events(n_rays // 4, seed=99)
+        p = onerf.build_params(rd, 0)
+        params = list(p.values())
+        for t in params:
+            t.requires_grad_(True)
+        bk = torch.tensor([0.5413] * rd, requires_grad=True)
+        opt = torch.optim.Adam([{"params": params, "weight_decay": 1e-6}, {"params": [bk]}], lr=0.01)
 
-    def step():
-        opt.zero_grad()
-        b = prepare_batch(raw)
-        total, _, _ = step_loss(p, torch.nn.functional.softplus(bk), b, n_samples)
-        total.backward()
-        opt.step()
+        def step():
+            opt.zero_grad()
+            b = prepare_batch(raw)
+            total, _, _ = step_loss(p, torch.nn.functional.softplus(bk), b, n_samples)
+            total.backward()
+            opt.step()
 
-    step()  # warm-up
-    t0 = time.perf_counter()
-    reps = 4
-    for _ in range(reps):
-        step()
-    dt = (time.perf_counter() - t0) / reps
-    return dict(value=round(n_rays / dt, 2), unit="rays/s", cores=threads, kind="port",
-                sample=f"oracle (PyTorch CPU) train step on {n_rays} rays x {n_samples} samples "
-                       f"(event prep + rays + render fwd + event loss + backward + Adam), {reps} timed reps after 1 warm-up, "
-                       f"{dt:.2f} s/step")
+        med, ts = _time_median(step, warm, reps)
+        out.append(dict(rays=n_rays, samples=n_samples, rays_per_s=round(n_rays / med, 2),
+                        s_per_step_median=round(med, 3), s_per_step_all=[round(t, 3) for t in ts],
+                        warmup=warm, reps=reps))
+    lead = out[0]
+    return dict(value=lead["rays_per_s"], unit="rays/s", cores=threads, kind="port",
+                sample=f"oracle (PyTorch CPU) train step, BASELINE configs[0] shape {lead['rays']} rays x "
+                       f"{lead['samples']} samples (event prep + rays + render fwd + event loss + backward + Adam), "
+                       f"median of {lead['reps']} after {lead['warmup']} warm-ups; second leg "
+                       f"{out[1]['rays']} x {out[1]['samples']} (the 2^17 x 128 workload scaled down)",
+                legs=out, **_cpu_info(threads))
 
 
 def cpu_baseline_pixbw(n_rays, n_samples, rd, S, threads):
-    """Bounded CPU sample of the pixel-bandwidth-on step (oracle)."""
+    """Bounded CPU sample of the pixel-bandwidth-on step (oracle): median of 3 after 1 warm-up."""
     from oracle import nerf as onerf
     from oracle import pixbw as opb
     from oracle.train import pixbw_step_loss
@@ -191,16 +248,12 @@ def cpu_baseline_pixbw(n_rays, n_samples, rd, S, threads):
         total.backward()
         opt.step()
 
-    step()
-    t0 = time.perf_counter()
-    reps = 2
-    for _ in range(reps):
-        step()
-    dt = (time.perf_counter() - t0) / reps
+    med, ts = _time_median(step, 1, 3)
     R = 4 * S * N
-    return dict(value=round(R / dt, 2), unit="rays/s", cores=threads, kind="port",
+    return dict(value=round(R / med, 2), unit="rays/s", cores=threads, kind="port",
                 sample=f"oracle (PyTorch CPU) pixel-bandwidth-on train step, {N} events x 4 x S={S} = {R} rays x "
-                       f"{n_samples} samples, {reps} timed reps after 1 warm-up, {dt:.2f} s/step")
+                       f"{n_samples} samples, median of 3 after 1 warm-up, {med:.2f} s/step",
+                **_cpu_info(threads))
 
 
 def main():
@@ -259,6 +312,8 @@ def main():
     nat.timing_enable(False)
     kt = nat.timing_collect()
     n_local = ts.R * (ts.n_samples if a.pixbw else ts.S)
+    fps = flop_per_sample(a.rd)
+    peak = PEAK_TFLOPS[a.mode]
     kernels = {}
     for k, (tot, cnt) in kt.items():
         if cnt == 0:
@@ -266,25 +321,29 @@ def main():
         avg = tot / cnt
         e = {"launches_per_step": cnt // PHASE_REPS, "avg_ms": round(avg, 4),
              "step_ms": round(tot / PHASE_REPS, 3)}
+        if k in fps:
+            f = fps[k] * n_local * PHASE_REPS / cnt  # algorithmic flop per launch
+            e.update(flop_per_launch=f, tflops=round(f / (avg * 1e-3) / 1e12, 1),
+                     mfma_frac=round(f / (avg * 1e-3) / 1e12 / peak, 4))
         if k in BYTES_PER_SAMPLE and a.mode == "bf16":
-            b = BYTES_PER_SAMPLE[k] * n_local * PHASE_REPS / cnt  # algorithmic bytes per launch
-            e.update(bytes_per_launch=b, gbs=round(b / (avg * 1e-3) / 1e9, 1))
-        if k == "render_fwd_kernel":
-            f = 2.0 * MAC_PER_SAMPLE[a.rd] * n_local * PHASE_REPS / cnt  # algorithmic flop per launch
-            e.update(flop_per_launch=f, tflops=round(f / (avg * 1e-3) / 1e12, 1))
+            b = BYTES_PER_SAMPLE[k] * n_local * PHASE_REPS / cnt  # algorithmic (design) bytes per launch
+            e.update(bytes_per_launch=b, gbs=round(b / (avg * 1e-3) / 1e9, 1),
+                     hbm_frac=round(b / (avg * 1e-3) / 1e9 / PEAK_HBM_GBS, 4))
         kernels[k] = e
-    dom = max(kernels, key=lambda k: kernels[k]["step_ms"])  # the kernel that takes most of the step
+    # the roofline line is on SURVEY.md 8(d)'s axis (MFMA, algorithmic FLOP) for the kernel that
+    # takes most of the step; its HBM-axis figures (the design's streamed bytes) ride along
+    dom = max((k for k in kernels if k in fps), key=lambda k: kernels[k]["step_ms"])
     de = kernels[dom]
-    if dom == "render_fwd_kernel":
-        roofline = {"bound": "mfma", "achieved": de["tflops"], "peak": PEAK_TFLOPS[a.mode], "unit": "TFLOP/s"}
-    else:
-        roofline = {"bound": "hbm", "achieved": de["gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s"}
-    roofline["frac"] = round(roofline["achieved"] / roofline["peak"], 4)
-    roofline["traffic"] = pmc_traffic(dom, a)
-    roofline.update(kernel=dom, avg_launch_ms=de["avg_ms"], timing="hipEvents on the launch stream (den_timing_*)")
+    roofline = {"bound": "mfma", "achieved": de["tflops"], "peak": peak, "unit": "TFLOP/s",
+                "frac": de["mfma_frac"], "traffic": pmc_traffic(dom, a), "traffic_unit": "bytes per launch (PMC)",
+                "kernel": dom, "avg_launch_ms": de["avg_ms"], "flop_per_launch": de["flop_per_launch"],
+                "timing": "hipEvents on the launch stream (den_timing_*)"}
+    if "gbs" in de:
+        roofline["hbm"] = {"achieved": de["gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": de["hbm_frac"],
+                           "bytes_per_launch": de["bytes_per_launch"]}
     step_flop = 3.0 * 2.0 * MAC_PER_SAMPLE[a.rd] * n_local
-    roofline["step_mfma_frac"] = round(step_flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.mode], 4)
-    if rank == 0:
+    roofline["step_mfma_frac"] = round(step_flop / (ms * 1e-3) / 1e12 / peak, 4)
+    if rank == 0 and not a.no_gemm_peak:
         gp = measured_gemm_peak(dev, torch.bfloat16 if a.mode == "bf16" else torch.float32)
         roofline["mfma_peak_measured"] = {"tflops": gp, "how": "torch.matmul 8192^3 (hipBLASLt), HIP events",
                                           "step_frac": round(step_flop / (ms * 1e-3) / 1e12 / gp, 4)}
@@ -294,9 +353,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            threads = min(16, len(os.sched_getaffinity(0)))
+            threads = cpu_threads()
             cpu = (cpu_baseline_pixbw(a.cpu_rays, a.samples, a.rd, a.it_samples, threads) if a.pixbw
-                   else cpu_baseline(a.cpu_rays, a.samples, a.rd, threads))
+                   else cpu_baseline(a.rd, threads))
         except Exception as e:  # pragma: no cover - reported, not fatal
             cpu = {"error": repr(e)}
     if rank == 0:

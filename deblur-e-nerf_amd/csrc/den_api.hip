@@ -15,6 +15,7 @@
 #include "den_dw.hip"
 #include "den_events.hip"
 #include "den_hidden.hip"
+#include "den_march.hip"
 #include "den_misc.hip"
 #include "den_pixbw.hip"
 #include "den_render.hip"
@@ -130,6 +131,10 @@ int check_desc(const den_render_desc* d) {
   if (((int64_t)d->n_rays * d->n_samples) % std::max(wgs, fwd_wg_samples(d->mode)) != 0)
     return fail(DEN_EUNSUPPORTED, "n_rays * n_samples must be a multiple of the workgroup tile "
                                   "(den_render_tile_samples)");
+  if (d->points < 0 || d->points > 2) return fail(DEN_EINVAL, "points must be 0, 1 or 2");
+  if (d->contraction < 0 || d->contraction > 2) return fail(DEN_EINVAL, "contraction must be 0 (AABB), 1 (tanh) or 2 (sphere)");
+  if (d->points == 0 && d->contraction != 0)
+    return fail(DEN_EUNSUPPORTED, "the fixed-count sampler (points = 0) marches the AABB: contraction must be 0");
   return DEN_OK;
 }
 
@@ -142,12 +147,16 @@ RenderArgs<MODE> make_args(const den_render_desc* d, const den_render_io* io, co
   A.train = d->train;
   A.has_bkgd = d->has_bkgd;
   A.points = d->points;
+  A.contraction = d->contraction;
   for (int i = 0; i < 6; ++i) A.aabb[i] = d->aabb[i];
   A.near_p = d->near_plane;
   A.far_p = d->far_plane;
   A.rays_o = io->rays_o;
   A.rays_d = io->rays_d;
   A.jitter = io->jitter;
+  A.ray_idx = io->ray_indices;
+  A.t_start = io->t_starts;
+  A.t_end = io->t_ends;
   A.bias = io->bias_pk;
   A.bkgd = io->bkgd;
   char* ws = (char*)io->workspace;
@@ -390,9 +399,11 @@ size_t den_render_workspace_bytes(const den_render_desc* d) {
 int den_render_fwd(const den_render_desc* d, const den_render_io* io, void* stream) {
   int rc = check_desc(d);
   if (rc) return rc;
-  if (!io || !io->rays_o || !io->rays_d || !io->jitter || !io->w_fwd || !io->bias_pk || !io->out_rgb ||
-      !io->out_opacity || !io->out_depth)
+  if (!io || !io->rays_o || !io->rays_d || !io->w_fwd || !io->bias_pk || !io->out_rgb || !io->out_opacity ||
+      !io->out_depth || (d->points == 0 && !io->jitter))
     return fail(DEN_EINVAL, "null pointer in den_render_io");
+  if (d->points == 2 && (!io->ray_indices || !io->t_starts || !io->t_ends))
+    return fail(DEN_EINVAL, "points = 2 needs ray_indices, t_starts and t_ends");
   if (d->has_bkgd && !io->bkgd) return fail(DEN_EINVAL, "has_bkgd but bkgd == NULL");
   if (d->points && d->has_bkgd) return fail(DEN_EINVAL, "points mode has no background");
   if (!io->workspace) return fail(DEN_EINVAL, "workspace is required (den_render_workspace_bytes)");
@@ -403,7 +414,7 @@ int den_render_bwd(const den_render_desc* d, const den_render_io* io, const den_
   int rc = check_desc(d);
   if (rc) return rc;
   if (!d->train) return fail(DEN_EINVAL, "den_render_bwd needs a train=1 forward");
-  if (!io || !io->workspace || !io->w_bwd || !io->rays_o || !io->rays_d || !io->jitter)
+  if (!io || !io->workspace || !io->w_bwd || !io->rays_o || !io->rays_d || (d->points == 0 && !io->jitter))
     return fail(DEN_EINVAL, "null pointer in den_render_io");
   if (!g || !g->d_rgb || !g->grad_params) return fail(DEN_EINVAL, "null pointer in den_render_grad");
   if (d->has_bkgd && !io->bkgd) return fail(DEN_EINVAL, "has_bkgd but bkgd == NULL");
@@ -630,6 +641,278 @@ int den_pixel_rays(int32_t M, int32_t N, const float* k_inv, const float* pixel,
   const int64_t n = (int64_t)M * N;
   hipLaunchKernelGGL(pixel_rays_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, M, N,
                      k_inv, pixel, t_pos, t_rot, ray_o, ray_d);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+// ------------------------------------------------------------------ packed rendering (den_march.hip)
+static int march_args(int32_t n_rays, const float* o, const float* d, const float* t_min, const float* t_max,
+                      const float* roi, const int32_t* res, const uint8_t* grid, int32_t contraction, float step,
+                      float cone, MarchArgs* M) {
+  if (n_rays <= 0 || !o || !d || !t_min || !t_max || !(step > 0.0f) || !(cone >= 0.0f))
+    return fail(DEN_EINVAL, "bad arguments");
+  if (contraction < 0 || contraction > 2) return fail(DEN_EINVAL, "contraction must be 0, 1 or 2");
+  if (grid && (!roi || !res || res[0] <= 0 || res[1] <= 0 || res[2] <= 0))
+    return fail(DEN_EINVAL, "an occupancy grid needs roi and a positive resolution");
+  *M = MarchArgs{};
+  M->n_rays = n_rays;
+  M->rays_o = o;
+  M->rays_d = d;
+  M->t_min = t_min;
+  M->t_max = t_max;
+  if (grid) {
+    for (int a = 0; a < 6; ++a) M->roi[a] = roi[a];
+    for (int a = 0; a < 3; ++a) M->res[a] = res[a];
+  }
+  M->grid = grid;
+  M->contraction = grid ? contraction : CONTRACT_AABB;
+  M->step = step;
+  M->cone = cone;
+  M->max_iter = 1 << 20;
+  return DEN_OK;
+}
+
+int den_march_prep(int32_t n_rays, const float* rays_o, const float* rays_d, const float* aabb, float near_plane,
+                   float far_plane, const float* jitter, float step, float* t_min, float* t_max, void* stream) {
+  if (n_rays <= 0 || !rays_o || !rays_d || !t_min || !t_max || !(step > 0.0f)) return fail(DEN_EINVAL, "bad arguments");
+  MarchPrepArgs P{};
+  P.n_rays = n_rays;
+  P.rays_o = rays_o;
+  P.rays_d = rays_d;
+  P.has_aabb = aabb ? 1 : 0;
+  if (aabb)
+    for (int a = 0; a < 6; ++a) P.aabb[a] = aabb[a];
+  P.near_p = near_plane;
+  P.far_p = far_plane;
+  P.jitter = jitter;
+  P.step = step;
+  P.t_min = t_min;
+  P.t_max = t_max;
+  hipLaunchKernelGGL(march_prep_kernel, dim3((n_rays + 255) / 256), dim3(256), 0, (hipStream_t)stream, P);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_march_count(int32_t n_rays, const float* rays_o, const float* rays_d, const float* t_min, const float* t_max,
+                    const float* roi, const int32_t* res, const uint8_t* grid, int32_t contraction, float step,
+                    float cone, int32_t* counts, void* stream) {
+  MarchArgs M;
+  int rc = march_args(n_rays, rays_o, rays_d, t_min, t_max, roi, res, grid, contraction, step, cone, &M);
+  if (rc) return rc;
+  if (!counts) return fail(DEN_EINVAL, "counts is required");
+  M.counts = counts;
+  hipLaunchKernelGGL(march_kernel<false>, dim3((n_rays + 127) / 128), dim3(128), 0, (hipStream_t)stream, M);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_march_fill(int32_t n_rays, const float* rays_o, const float* rays_d, const float* t_min, const float* t_max,
+                   const float* roi, const int32_t* res, const uint8_t* grid, int32_t contraction, float step,
+                   float cone, const int64_t* offsets, int32_t* ray_indices, float* t_starts, float* t_ends,
+                   void* stream) {
+  MarchArgs M;
+  int rc = march_args(n_rays, rays_o, rays_d, t_min, t_max, roi, res, grid, contraction, step, cone, &M);
+  if (rc) return rc;
+  if (!offsets || !ray_indices || !t_starts || !t_ends) return fail(DEN_EINVAL, "null output");
+  M.offsets = offsets;
+  M.ray_idx = ray_indices;
+  M.t0 = t_starts;
+  M.t1 = t_ends;
+  hipLaunchKernelGGL(march_kernel<true>, dim3((n_rays + 127) / 128), dim3(128), 0, (hipStream_t)stream, M);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+size_t den_scan_workspace_bytes(int64_t n) {
+  return n <= 0 ? 8 : (size_t)((n + SCAN_TILE - 1) / SCAN_TILE) * sizeof(int64_t);
+}
+
+int den_exclusive_scan(int64_t n, const int32_t* counts, int64_t* offsets, void* workspace, void* stream) {
+  if (n < 0 || !offsets || (n > 0 && (!counts || !workspace))) return fail(DEN_EINVAL, "bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    DEN_HIP(hipMemsetAsync(offsets, 0, sizeof(int64_t), st));
+    return DEN_OK;
+  }
+  const int64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  int64_t* sums = (int64_t*)workspace;
+  hipLaunchKernelGGL(scan_tile_kernel, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, st, n, counts, offsets, sums);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(SCAN_BLOCK), 0, st, tiles, sums, offsets, n);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, (const int64_t*)sums,
+                     offsets);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_pack_info(int32_t n_rays, int64_t n, const int32_t* ray_indices, int64_t* offsets, void* stream) {
+  if (n_rays <= 0 || n < 0 || !offsets || (n > 0 && !ray_indices)) return fail(DEN_EINVAL, "bad arguments");
+  hipLaunchKernelGGL(pack_info_kernel, dim3((n_rays + 256) / 256), dim3(256), 0, (hipStream_t)stream, n_rays, n,
+                     ray_indices, offsets);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+constexpr int RAYS_PER_WG = 4;  // one wave per ray
+
+int den_visibility(int32_t n_rays, const int64_t* offsets, const float* t_starts, const float* t_ends,
+                   const float* sigmas, const float* alphas, float early_stop_eps, float alpha_thre, uint8_t* keep,
+                   int32_t* counts, void* stream) {
+  if (n_rays <= 0 || !offsets || !t_starts || !t_ends || (!sigmas && !alphas) || !keep || !counts)
+    return fail(DEN_EINVAL, "bad arguments");
+  VisArgs V{};
+  V.n_rays = n_rays;
+  V.offsets = offsets;
+  V.t0 = t_starts;
+  V.t1 = t_ends;
+  V.sigma = sigmas;
+  V.alpha = sigmas ? nullptr : alphas;
+  V.early_stop_eps = early_stop_eps;
+  V.alpha_thre = alpha_thre;
+  V.keep = keep;
+  V.counts = counts;
+  hipLaunchKernelGGL(visibility_kernel, dim3((n_rays + RAYS_PER_WG - 1) / RAYS_PER_WG), dim3(64 * RAYS_PER_WG), 0,
+                     (hipStream_t)stream, V);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_compact(int32_t n_rays, const int64_t* offsets, const uint8_t* keep, const int64_t* out_offsets,
+                const int32_t* ray_indices, const float* t_starts, const float* t_ends, int32_t* out_ray_indices,
+                float* out_t_starts, float* out_t_ends, void* stream) {
+  if (n_rays <= 0 || !offsets || !keep || !out_offsets || !ray_indices || !t_starts || !t_ends || !out_ray_indices ||
+      !out_t_starts || !out_t_ends)
+    return fail(DEN_EINVAL, "bad arguments");
+  VisArgs V{};
+  V.n_rays = n_rays;
+  V.offsets = offsets;
+  V.t0 = t_starts;
+  V.t1 = t_ends;
+  V.keep = (uint8_t*)keep;
+  V.out_offsets = out_offsets;
+  V.in_ray = ray_indices;
+  V.out_ray = out_ray_indices;
+  V.out_t0 = out_t_starts;
+  V.out_t1 = out_t_ends;
+  hipLaunchKernelGGL(compact_kernel, dim3((n_rays + RAYS_PER_WG - 1) / RAYS_PER_WG), dim3(64 * RAYS_PER_WG), 0,
+                     (hipStream_t)stream, V);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_composite_fwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts, const float* t_ends,
+                      const float* sigmas, const float* rgbs, const float* bkgd, float* colors, float* opacities,
+                      float* depths, void* stream) {
+  if (n_rays <= 0 || rd < 1 || rd > 3 || !offsets || !t_starts || !t_ends || !sigmas || !rgbs || !colors ||
+      !opacities || !depths)
+    return fail(DEN_EINVAL, "bad arguments");
+  CompArgs C{};
+  C.n_rays = n_rays;
+  C.rd = rd;
+  C.offsets = offsets;
+  C.t0 = t_starts;
+  C.t1 = t_ends;
+  C.sigma = sigmas;
+  C.rgb = rgbs;
+  C.bkgd = bkgd;
+  C.color = colors;
+  C.opacity = opacities;
+  C.depth = depths;
+  hipLaunchKernelGGL(composite_fwd_kernel, dim3((n_rays + RAYS_PER_WG - 1) / RAYS_PER_WG), dim3(64 * RAYS_PER_WG), 0,
+                     (hipStream_t)stream, C);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+size_t den_composite_workspace_bytes(int32_t n_rays, int32_t rd) {
+  return n_rays > 0 && rd > 0 ? (size_t)n_rays * rd * sizeof(float) : 0;
+}
+
+int den_composite_bwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts, const float* t_ends,
+                      const float* sigmas, const float* rgbs, const float* bkgd, const float* d_colors,
+                      const float* d_opacities, const float* d_depths, float* d_sigmas, float* d_rgbs, float* d_bkgd,
+                      void* workspace, void* stream) {
+  if (n_rays <= 0 || rd < 1 || rd > 3 || !offsets || !t_starts || !t_ends || !sigmas || !rgbs || !d_colors ||
+      !d_sigmas || !d_rgbs || (d_bkgd && (!bkgd || !workspace)))
+    return fail(DEN_EINVAL, "bad arguments");
+  CompArgs C{};
+  C.n_rays = n_rays;
+  C.rd = rd;
+  C.offsets = offsets;
+  C.t0 = t_starts;
+  C.t1 = t_ends;
+  C.sigma = sigmas;
+  C.rgb = rgbs;
+  C.bkgd = bkgd;
+  C.d_color = d_colors;
+  C.d_opacity = d_opacities;
+  C.d_depth = d_depths;
+  C.d_sigma = d_sigmas;
+  C.d_rgb = d_rgbs;
+  C.bkgd_partial = d_bkgd ? (float*)workspace : nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(composite_bwd_kernel, dim3((n_rays + RAYS_PER_WG - 1) / RAYS_PER_WG), dim3(64 * RAYS_PER_WG), 0,
+                     st, C);
+  DEN_LAUNCHED();
+  if (d_bkgd) {
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(rd), dim3(256), 0, st, rd, n_rays, (const float*)workspace, d_bkgd);
+    DEN_LAUNCHED();
+  }
+  return DEN_OK;
+}
+
+constexpr int OCC_NB = 1024;  // fixed reduction width (deterministic mean)
+
+size_t den_occ_workspace_bytes(void) { return OCC_NB * sizeof(float); }
+
+int den_occ_points(int64_t m, const int64_t* cell_indices, const float* jitter, const int32_t* res, const float* roi,
+                   int32_t contraction, float* points, uint8_t* mask, uint8_t* sampled, void* stream) {
+  if (m <= 0 || !cell_indices || !jitter || !res || !roi || !points || !mask || !sampled || contraction < 0 ||
+      contraction > 2)
+    return fail(DEN_EINVAL, "bad arguments");
+  OccArgs A{};
+  A.m = m;
+  A.idx = cell_indices;
+  A.u = jitter;
+  for (int a = 0; a < 3; ++a) A.res[a] = res[a];
+  for (int a = 0; a < 6; ++a) A.roi[a] = roi[a];
+  A.contraction = contraction;
+  A.pts = points;
+  A.mask = mask;
+  A.sampled = sampled;
+  hipLaunchKernelGGL(occ_points_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_occ_update(int64_t m, const int64_t* cell_indices, const uint8_t* mask, const float* sigmas,
+                   const float* step_sizes, float step_size, float ema_decay, float occ_thre, int64_t cells,
+                   float* occs, uint8_t* sampled, uint8_t* binary, void* workspace, void* stream) {
+  if (m <= 0 || cells <= 0 || !cell_indices || !mask || !sigmas || !occs || !sampled || !binary || !workspace)
+    return fail(DEN_EINVAL, "bad arguments");
+  OccArgs A{};
+  A.m = m;
+  A.idx = cell_indices;
+  A.mask = (uint8_t*)mask;
+  A.sigma = sigmas;
+  A.step = step_sizes;
+  A.step_c = step_size;
+  A.decay = ema_decay;
+  A.occ_thre = occ_thre;
+  A.cells = cells;
+  A.occs = occs;
+  A.sampled = sampled;
+  A.binary = binary;
+  A.part = (float*)workspace;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(occ_decay_kernel, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, st, A);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(occ_max_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, A);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(occ_mean_partial_kernel, dim3(OCC_NB), dim3(OCC_BLOCK), 0, st, A);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(occ_binary_kernel, dim3(1024), dim3(256), 0, st, A, OCC_NB);
   DEN_LAUNCHED();
   return DEN_OK;
 }

@@ -229,32 +229,52 @@ __device__ __forceinline__ void sample_interval(const RayGeom& g, int k, float u
   *t1 = mid + half;
 }
 
-// contracted position x' = 2*pi*((x - lo)/(hi - lo) - 0.5) and selector
-__device__ __forceinline__ void contract(const float* o, const float* d, float t0, float t1, const float* aabb,
-                                         float* xc, float* sel) {
+// Input-space contraction of VanillaNeRFRadianceField.contract_input_space (mlp.py:321-335):
+//   type 0 AABB   : x = (p - lo)/(hi - lo)
+//   type 1 tanh   : x = (tanh((p - lo)/(hi - lo) - 0.5) + 1)/2          (ngp.py:96-106)
+//   type 2 sphere : y = 2(p - lo)/(hi - lo) - 1, |y| > 1 -> (2 - 1/|y|) y/|y|, x = y/4 + 0.5 (ngp.py:68-93)
+// then selector = all(0 < x < 1) and x' = 2*pi*(x - 0.5).
+enum { CONTRACT_AABB = 0, CONTRACT_TANH = 1, CONTRACT_SPHERE = 2 };
+
+__device__ __forceinline__ void contract_point(const float* pos, const float* aabb, float* xc, float* sel,
+                                               int type = CONTRACT_AABB) {
 #pragma clang fp contract(off)
-  float tt = t0 + t1;
+  float x[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) x[a] = __fdiv_rn(pos[a] - aabb[a], aabb[3 + a] - aabb[a]);
+  if (type == CONTRACT_SPHERE) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) x[a] = x[a] * 2.0f - 1.0f;
+    const float mag = __fsqrt_rn(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+    if (mag > 1.0f) {
+      const float s = 2.0f - __fdiv_rn(1.0f, mag);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) x[a] = s * __fdiv_rn(x[a], mag);
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) x[a] = __fdiv_rn(x[a], 4.0f) + 0.5f;
+  } else if (type == CONTRACT_TANH) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) x[a] = __fdiv_rn(tanhf(x[a] - 0.5f) + 1.0f, 2.0f);
+  }
   bool in = true;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    float pos = o[a] + __fdiv_rn(d[a] * tt, 2.0f);
-    float xh = __fdiv_rn(pos - aabb[a], aabb[3 + a] - aabb[a]);
-    in = in && (xh > 0.0f) && (xh < 1.0f);
-    xc[a] = 6.2831855f * (xh - 0.5f);
+    in = in && (x[a] > 0.0f) && (x[a] < 1.0f);
+    xc[a] = 6.2831855f * (x[a] - 0.5f);
   }
   *sel = in ? 1.0f : 0.0f;
 }
 
-__device__ __forceinline__ void contract_point(const float* pos, const float* aabb, float* xc, float* sel) {
+// sample position o + d*(t0 + t1)/2 (external/utils.py:83-87), then the contraction
+__device__ __forceinline__ void contract(const float* o, const float* d, float t0, float t1, const float* aabb,
+                                         float* xc, float* sel, int type = CONTRACT_AABB) {
 #pragma clang fp contract(off)
-  bool in = true;
+  const float tt = t0 + t1;
+  float pos[3];
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    float xh = __fdiv_rn(pos[a] - aabb[a], aabb[3 + a] - aabb[a]);
-    in = in && (xh > 0.0f) && (xh < 1.0f);
-    xc[a] = 6.2831855f * (xh - 0.5f);
-  }
-  *sel = in ? 1.0f : 0.0f;
+  for (int a = 0; a < 3; ++a) pos[a] = o[a] + __fdiv_rn(d[a] * tt, 2.0f);
+  contract_point(pos, aabb, xc, sel, type);
 }
 
 // encoding feature f of [v, sin(v*2^k), sin(v*2^k + pi/2)] (scale-major, dim-minor)

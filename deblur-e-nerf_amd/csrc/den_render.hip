@@ -27,12 +27,16 @@ struct RenderArgs {
   int rd;
   int train;
   int has_bkgd;
-  int points;
+  int points;             // 0 fixed-count sampler, 1 given points, 2 packed samples (ray_idx, t_start, t_end)
+  int contraction;        // CONTRACT_* (den_device.h)
   float aabb[6];
   float near_p, far_p;
   const float* rays_o;
   const float* rays_d;
   const float* jitter;
+  const int* ray_idx;     // points == 2: per-sample ray index, t_start, t_end (nerfacc packed layout)
+  const float* t_start;
+  const float* t_end;
   const char* w;          // packed fwd (or bwd) chunks
   const float* bias;      // packed biases (fwd)
   const float* bkgd;
@@ -291,13 +295,22 @@ __global__ __launch_bounds__(fwd_threads(MODE), 1024 / fwd_threads(MODE)) void r
   }
 
   float o[3], d[3], xc[3], sel;
-  if (A.points) {
+  if (A.points == 1) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       o[a] = A.rays_o[sample * 3 + a];
       d[a] = A.rays_d[sample * 3 + a];
     }
-    contract_point(o, A.aabb, xc, &sel);
+    contract_point(o, A.aabb, xc, &sel, A.contraction);
+  } else if (A.points == 2) {
+    // packed ray-marching samples: position o + d (t0 + t1)/2 of the sample's ray (utils.py:83-87)
+    const int64_t r = A.ray_idx[sample];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      o[a] = A.rays_o[r * 3 + a];
+      d[a] = A.rays_d[r * 3 + a];
+    }
+    contract(o, d, A.t_start[sample], A.t_end[sample], A.aabb, xc, &sel, A.contraction);
   } else {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {

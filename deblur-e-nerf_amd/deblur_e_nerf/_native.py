@@ -27,12 +27,13 @@ class RenderDesc(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("radiance_dim", ctypes.c_int32), ("n_rays", ctypes.c_int32),
                 ("n_samples", ctypes.c_int32), ("aabb", ctypes.c_float * 6), ("near_plane", ctypes.c_float),
                 ("far_plane", ctypes.c_float), ("train", ctypes.c_int32), ("has_bkgd", ctypes.c_int32),
-                ("points", ctypes.c_int32)]
+                ("points", ctypes.c_int32), ("contraction", ctypes.c_int32)]
 
 
 class RenderIO(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("rays_o", "rays_d", "jitter", "w_fwd", "w_bwd", "bias_pk", "bkgd",
-                                               "workspace", "out_rgb", "out_opacity", "out_depth")]
+                                               "workspace", "out_rgb", "out_opacity", "out_depth", "ray_indices",
+                                               "t_starts", "t_ends")]
 
 
 class RenderGrad(ctypes.Structure):
@@ -78,6 +79,29 @@ _SIGS = {
     "den_pixbw_blocks": (ctypes.c_int, [ctypes.c_int32]),
     "den_pixbw_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
     "den_pixbw_bwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 13),
+    # packed (ray-marching) rendering, den_march.hip
+    "den_march_prep": (ctypes.c_int, [ctypes.c_int32] + [ctypes.c_void_p] * 3 + [ctypes.c_float] * 2
+                       + [ctypes.c_void_p, ctypes.c_float] + [ctypes.c_void_p] * 3),
+    "den_march_count": (ctypes.c_int, [ctypes.c_int32] + [ctypes.c_void_p] * 7 + [ctypes.c_int32, ctypes.c_float,
+                                                                                   ctypes.c_float]
+                        + [ctypes.c_void_p] * 2),
+    "den_march_fill": (ctypes.c_int, [ctypes.c_int32] + [ctypes.c_void_p] * 7 + [ctypes.c_int32, ctypes.c_float,
+                                                                                  ctypes.c_float]
+                       + [ctypes.c_void_p] * 5),
+    "den_scan_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "den_exclusive_scan": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4),
+    "den_pack_info": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64] + [ctypes.c_void_p] * 3),
+    "den_visibility": (ctypes.c_int, [ctypes.c_int32] + [ctypes.c_void_p] * 5 + [ctypes.c_float] * 2
+                       + [ctypes.c_void_p] * 3),
+    "den_compact": (ctypes.c_int, [ctypes.c_int32] + [ctypes.c_void_p] * 10),
+    "den_composite_fwd": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 10),
+    "den_composite_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32] * 2),
+    "den_composite_bwd": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 14),
+    "den_occ_workspace_bytes": (ctypes.c_size_t, []),
+    "den_occ_points": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int32]
+                       + [ctypes.c_void_p] * 4),
+    "den_occ_update": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 5 + [ctypes.c_float] * 3
+                       + [ctypes.c_int64] + [ctypes.c_void_p] * 5),
 }
 
 
@@ -171,7 +195,7 @@ class PackedWeights:
 
 
 # ----------------------------------------------------------------------------- render
-def _desc(cfg, n_rays, n_samples, train, has_bkgd, points=False):
+def _desc(cfg, n_rays, n_samples, train, has_bkgd, points=0):
     d = RenderDesc()
     d.mode = cfg["mode"]
     d.radiance_dim = cfg["rd"]
@@ -184,6 +208,7 @@ def _desc(cfg, n_rays, n_samples, train, has_bkgd, points=False):
     d.train = int(train)
     d.has_bkgd = int(has_bkgd)
     d.points = int(points)
+    d.contraction = int(cfg.get("contraction", 0))
     return d
 
 
@@ -204,34 +229,37 @@ class RenderFunction(torch.autograd.Function):
 
     inputs: rays_o (R,3), rays_d (R,3), jitter (R), bkgd (rd) or None, flat
     params (P,) f32, plus non-tensor config; outputs colour (R,rd), opacity (R),
-    depth (R) (un-normalised).  ``points=True`` evaluates the radiance field at
+    depth (R) (un-normalised).  ``points=1`` evaluates the radiance field at
     given points instead: rays_o = positions (n,3), rays_d = directions (n,3),
-    outputs rgb (n,rd), sigma (n), unused (n)."""
+    outputs rgb (n,rd), sigma (n), unused (n).  ``points=2`` evaluates it at the
+    packed samples ``samples = (ray_indices (n) i32, t_starts (n), t_ends (n))`` of
+    the rays rays_o / rays_d (n a multiple of the tile): outputs rgb (n,rd), sigma (n)."""
 
     @staticmethod
-    def forward(ctx, rays_o, rays_d, jitter, bkgd, flat, cfg, packed, n_samples, points):
+    def forward(ctx, rays_o, rays_d, jitter, bkgd, flat, cfg, packed, n_samples, points, samples=None):
         _require_device(rays_o, rays_d, jitter, bkgd, flat)
-        R = rays_o.shape[0]
         rd = cfg["rd"]
         train = torch.is_grad_enabled() and (flat.requires_grad or (bkgd is not None and bkgd.requires_grad))
         train = train or ctx.needs_input_grad[4] or (bkgd is not None and ctx.needs_input_grad[3])
-        n_rays = R
-        desc = _desc(cfg, n_rays if not points else R // n_samples, n_samples, train, bkgd is not None, points)
+        R = samples[0].numel() if points == 2 else rays_o.shape[0]
+        desc = _desc(cfg, R if not points else R // n_samples, n_samples, train, bkgd is not None, points)
         ws = torch.empty(render_workspace_bytes(desc), dtype=torch.uint8, device=rays_o.device)
         out_rgb = torch.empty(R, rd, dtype=torch.float32, device=rays_o.device)
         out_op = torch.empty(R, dtype=torch.float32, device=rays_o.device)
         out_dp = torch.empty(R, dtype=torch.float32, device=rays_o.device)
+        ri, t0, t1 = samples if points == 2 else (None, None, None)
         io = RenderIO(_ptr(rays_o), _ptr(rays_d), _ptr(jitter), _ptr(packed.fwd), _ptr(packed.bwd),
-                      _ptr(packed.bias), _ptr(bkgd), _ptr(ws), _ptr(out_rgb), _ptr(out_op), _ptr(out_dp))
+                      _ptr(packed.bias), _ptr(bkgd), _ptr(ws), _ptr(out_rgb), _ptr(out_op), _ptr(out_dp),
+                      _ptr(ri), _ptr(t0), _ptr(t1))
         _check(lib().den_render_fwd(ctypes.byref(desc), ctypes.byref(io), _stream(rays_o.device)))
-        ctx.desc, ctx.io_keep = desc, (rays_o, rays_d, jitter, bkgd, ws, packed)
+        ctx.desc, ctx.io_keep = desc, (rays_o, rays_d, jitter, bkgd, ws, packed, ri, t0, t1)
         ctx.flat_shape = flat.shape
         ctx.has_bkgd = bkgd is not None
         return out_rgb, out_op, out_dp
 
     @staticmethod
     def backward(ctx, g_rgb, g_op, g_dp):
-        rays_o, rays_d, jitter, bkgd, ws, packed = ctx.io_keep
+        rays_o, rays_d, jitter, bkgd, ws, packed, ri, t0, t1 = ctx.io_keep
         dev = rays_o.device
         g_rgb = torch.zeros_like(g_rgb) if g_rgb is None else g_rgb.contiguous()
         g_op = None if g_op is None else g_op.contiguous()
@@ -239,33 +267,57 @@ class RenderFunction(torch.autograd.Function):
         grad_flat = torch.empty(ctx.flat_shape, dtype=torch.float32, device=dev)
         grad_bkgd = torch.empty(bkgd.shape, dtype=torch.float32, device=dev) if ctx.has_bkgd else None
         io = RenderIO(_ptr(rays_o), _ptr(rays_d), _ptr(jitter), _ptr(packed.fwd), _ptr(packed.bwd),
-                      _ptr(packed.bias), _ptr(bkgd), _ptr(ws), None, None, None)
+                      _ptr(packed.bias), _ptr(bkgd), _ptr(ws), None, None, None, _ptr(ri), _ptr(t0), _ptr(t1))
         gr = RenderGrad(_ptr(g_rgb), _ptr(g_op), _ptr(g_dp), _ptr(grad_flat), _ptr(grad_bkgd))
         _check(lib().den_render_bwd(ctypes.byref(ctx.desc), ctypes.byref(io), ctypes.byref(gr), _stream(dev)))
         # release the workspace (the activations kept for this backward) as soon as the
         # stream is done with it: the caching allocator orders the reuse on the same stream
         ctx.io_keep = None
-        return None, None, None, grad_bkgd, grad_flat, None, None, None, None
+        return None, None, None, grad_bkgd, grad_flat, None, None, None, None, None
 
 
 def render(rays_o, rays_d, jitter, bkgd, flat, cfg, packed, n_samples):
     return RenderFunction.apply(rays_o.contiguous(), rays_d.contiguous(), jitter.contiguous(),
-                                None if bkgd is None else bkgd.contiguous(), flat, cfg, packed, n_samples, False)
+                                None if bkgd is None else bkgd.contiguous(), flat, cfg, packed, n_samples, 0)
+
+
+def _point_group(cfg):
+    tile = wg_samples(cfg["mode"])
+    # "rays" of `group` points each (<= the per-ray sample limit)
+    return tile, min(tile, 128 if mode_id(cfg["mode"]) == MODE_F32 else 256)
 
 
 def field(points, dirs, flat, cfg, packed):
     """Radiance field at arbitrary points (n,3)/(n,3): -> rgb (n,rd), sigma (n)."""
     n = points.shape[0]
-    tile = wg_samples(cfg["mode"])
+    tile, group = _point_group(cfg)
     pad = (-n) % tile
     if pad:
         points = torch.cat([points, points.new_zeros(pad, 3)])
         dirs = torch.cat([dirs, dirs.new_zeros(pad, 3) + torch.tensor([0.0, 0.0, 1.0], device=dirs.device)])
-    # "rays" of `group` points each (<= the per-ray sample limit); the jitter buffer is unused in point mode
-    group = min(tile, 128 if mode_id(cfg["mode"]) == MODE_F32 else 256)
-    dummy = torch.zeros(points.shape[0], device=points.device)
-    rgb, sig, _ = RenderFunction.apply(points.contiguous(), dirs.contiguous(), dummy, None, flat, cfg, packed,
-                                       group, True)
+    rgb, sig, _ = RenderFunction.apply(points.contiguous(), dirs.contiguous(), None, None, flat, cfg, packed,
+                                       group, 1)
+    return rgb[:n], sig[:n]
+
+
+def field_packed(rays_o, rays_d, ray_indices, t_starts, t_ends, flat, cfg, packed):
+    """Radiance field at packed ray-marching samples (den_render points = 2): sample s is at
+    rays_o[r] + rays_d[r] (t_starts[s] + t_ends[s]) / 2, r = ray_indices[s], viewed along
+    rays_d[r] (external/utils.py:83-96) -> rgb (n, rd), sigma (n)."""
+    n = ray_indices.numel()
+    if n == 0:  # no sample survived the march: nothing to evaluate
+        return (torch.zeros(0, cfg["rd"], device=rays_o.device), torch.zeros(0, device=rays_o.device))
+    tile, group = _point_group(cfg)
+    pad = (-n) % tile
+    ri = ray_indices.reshape(-1).to(torch.int32)
+    t0 = t_starts.reshape(-1).to(torch.float32)
+    t1 = t_ends.reshape(-1).to(torch.float32)
+    if pad:  # zero-length samples of ray 0 (outputs dropped, no gradient)
+        ri = torch.cat([ri, ri.new_zeros(pad)])
+        t0 = torch.cat([t0, t0.new_zeros(pad)])
+        t1 = torch.cat([t1, t1.new_zeros(pad)])
+    rgb, sig, _ = RenderFunction.apply(rays_o.float().contiguous(), rays_d.float().contiguous(), None, None, flat,
+                                       cfg, packed, group, 2, (ri.contiguous(), t0.contiguous(), t1.contiguous()))
     return rgb[:n], sig[:n]
 
 

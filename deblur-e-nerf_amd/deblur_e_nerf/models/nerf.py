@@ -1,22 +1,29 @@
 """NeRF renderer -- MI355X-native mirror of the reference's
 ``deblur_e_nerf/models/nerf.py`` (NeRF, nerf.py:31-286).
 
-Same constructor signature (plus ``n_samples`` and ``mode``), same
-``forward(ray_origin, ray_direction) -> (radiance, opacity, depth,
-mean_num_samples_per_ray)`` contract and the same parameter names
-(``radiance_field.*``, ``parametrizations.render_bkgd.original``).
+Same constructor signature, the same ``forward(ray_origin, ray_direction) ->
+(radiance, opacity, depth, mean_num_samples_per_ray)`` contract, the same
+``update_occ_grid`` / ``pixel_params_to_ray`` and the same parameter / buffer
+names (``radiance_field.*``, ``occupancy_grid.*``,
+``parametrizations.render_bkgd.original``).
 
-Ray marching: nerfacc's occupancy-grid marching with a constant
-``render_step_size`` and early stopping (external/utils.py:106-119) is replaced
-by the fused fixed-count stratified sampler of den_render_fwd (n_samples per
-ray, one jitter per ray while training, u = 0 in eval as nerfacc's
-``stratified=radiance_field.training``).  The packed occupancy-grid path is the
-next row of SURVEY.md 8(f) (#1); ``update_occ_grid`` is accepted and ignored.
+Two samplers:
+
+* ``sampler="occupancy"`` (default; the reference's): nerfacc-style occupancy-grid
+  marching with the constant ``render_step_size`` (or the cone step), the
+  early-stop density pre-pass and packed compositing (external/utils.py
+  render_image on den_march.hip + the fused MLP at packed samples).
+* ``sampler="fixed"``: the fused fixed-count stratified sampler of
+  den_render_fwd (``n_samples`` per ray, one jitter per ray while training,
+  u = 0 in eval) -- BASELINE.json's "131072 rays x 128 samples" workload, which
+  the benchmark and ``train.TrainStep`` run; it marches the AABB and ignores the
+  occupancy grid.
 """
 import torch
 
 from .. import _native
-from ..external import mlp, ngp
+from ..external import mlp, ngp, utils
+from ..external.marching import ContractionType, OccupancyGrid, contraction_id
 from ..utils import modules
 
 
@@ -41,8 +48,14 @@ class NeRF(torch.nn.Module):
 
     def __init__(self, aabb, contraction_type, occ_grid_config, near_plane, far_plane, render_step_size,
                  render_bkgd, cone_angle, early_stop_eps, alpha_thre, test_chunk_size, arch, arch_config, num_dim,
-                 radiance_dim, opacity_eps=1e-10, n_samples=128, mode="f32"):
+                 radiance_dim, opacity_eps=1e-10, sampler="occupancy", n_samples=128, mode="f32"):
         super().__init__()
+        if occ_grid_config is not None:
+            assert torch.all(torch.tensor(occ_grid_config.resolution) > 0)
+            assert 0 <= occ_grid_config.occ_thre <= 1
+            assert 0 <= occ_grid_config.ema_decay <= 1
+            assert occ_grid_config.warmup_steps > 0
+            assert occ_grid_config.n > 0
         if (near_plane is not None) and (far_plane is not None):
             assert 0 <= near_plane <= far_plane
         assert render_step_size > 0
@@ -50,8 +63,11 @@ class NeRF(torch.nn.Module):
             or isinstance(render_bkgd, torch.Tensor)
         assert cone_angle >= 0 and 0 <= early_stop_eps <= 1 and 0 <= alpha_thre <= 1
         assert test_chunk_size > 0 and num_dim > 0 and radiance_dim > 0 and opacity_eps > 0
+        assert sampler in ("occupancy", "fixed")
         if arch != "mlp":
             raise NotImplementedError("the ngp arch (tcnn HashGrid) is out of scope; use arch: mlp")
+        if sampler == "fixed" and contraction_id(contraction_type) != 0:
+            raise NotImplementedError("the fixed-count sampler marches the AABB: use contraction_type AABB")
         self.register_buffer("aabb", torch.tensor(aabb), persistent=False)
         self.contraction_type = contraction_type
         self.occ_grid_config = occ_grid_config
@@ -70,7 +86,11 @@ class NeRF(torch.nn.Module):
         self.alpha_thre = alpha_thre
         self.test_chunk_size = test_chunk_size
         self.opacity_eps = opacity_eps
+        self.sampler = sampler
         self.n_samples = n_samples
+        # the occupancy grid (nerf.py:98-102)
+        resolution = occ_grid_config.resolution if occ_grid_config is not None else 128
+        self.occupancy_grid = OccupancyGrid(roi_aabb=aabb, resolution=resolution, contraction_type=contraction_type)
         self.radiance_field = mlp.VanillaNeRFRadianceField(
             aabb=aabb,
             net_depth=arch_config.net_depth,
@@ -91,9 +111,29 @@ class NeRF(torch.nn.Module):
         )
 
     def update_occ_grid(self, step, T_wc_position):
-        """Occupancy-grid update (nerf.py:170-204): not needed by the fixed-count
-        sampler; kept so the reference's training_step runs unchanged."""
-        return None
+        """nerf.py:170-204: every ``occ_grid.n`` steps, the EMA occupancy of the grid cells from
+        the density at a random point of each sampled cell times the marching step (the cone step
+        of a random camera when cone_angle > 0).  No-op for the fixed-count sampler."""
+        if self.sampler != "occupancy" or self.occ_grid_config is None:
+            return None
+        step_size = self.render_step_size
+
+        def occ_eval_fn(x):
+            if self.cone_angle > 0.0:
+                camera_ids = torch.randint(0, len(T_wc_position), (x.shape[0],), device=T_wc_position.device)
+                origins = T_wc_position[camera_ids, :]
+                t = (origins - x).norm(dim=-1, keepdim=True)
+                s = torch.clamp(t * self.cone_angle, min=self.render_step_size)
+                if (self.near_plane is not None) and (self.far_plane is not None):
+                    s = torch.where((t > self.near_plane) & (t < self.far_plane), s, torch.zeros_like(s))
+            else:
+                s = step_size
+            with torch.no_grad():
+                density = self.radiance_field.query_density(x)
+            return density * s
+
+        cfg = self.occ_grid_config
+        self.occupancy_grid.every_n_step(step, occ_eval_fn, cfg.occ_thre, cfg.ema_decay, cfg.warmup_steps, cfg.n)
 
     @staticmethod
     def pixel_params_to_ray(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation):
@@ -103,16 +143,13 @@ class NeRF(torch.nn.Module):
         return _native.pixel_rays(intrinsics_inverse.float().contiguous(), pixel_position.float().contiguous(),
                                   T_wc_position.float().contiguous(), T_wc_orientation.float().contiguous())
 
-    def forward(self, ray_origin, ray_direction):
+    def _forward_fixed(self, ray_origin, ray_direction):
         shape = ray_origin.shape[:-1]
         o = ray_origin.reshape(-1, 3).float().contiguous()
         d = ray_direction.reshape(-1, 3).float().contiguous()
         R = o.shape[0]
         rf = self.radiance_field
-        if self.training:
-            jitter = torch.rand(R, device=o.device)
-        else:
-            jitter = torch.zeros(R, device=o.device)
+        jitter = torch.rand(R, device=o.device) if self.training else torch.zeros(R, device=o.device)
         # the kernel renders whole workgroup tiles: pad the ray batch
         tile_rays = _native.wg_samples(rf.mode) // self.n_samples
         pad = (-R) % tile_rays
@@ -125,7 +162,27 @@ class NeRF(torch.nn.Module):
             o, d, jitter, None if bkgd is None else bkgd.float(), rf.flat_leaf(),
             rf.render_cfg(self.near_plane, self.far_plane), rf.packed(), self.n_samples)
         radiance, opacity, depth = radiance[:R], opacity[:R], depth[:R]
-        radiance = radiance.reshape(*shape, -1).squeeze(-1)
-        opacity = opacity.reshape(shape)
-        depth = depth.reshape(shape) / (opacity + self.opacity_eps)
-        return radiance, opacity, depth, float(self.n_samples)
+        return radiance.reshape(*shape, -1), opacity.reshape(*shape, 1), depth.reshape(*shape, 1), \
+            float(self.n_samples) * R
+
+    def forward(self, ray_origin, ray_direction):
+        if self.sampler == "fixed":
+            radiance, opacity, depth, num_samples_across_rays = self._forward_fixed(ray_origin, ray_direction)
+        else:
+            rays = utils.Rays(origins=ray_origin, viewdirs=ray_direction)
+            ray_marching_aabb = self.aabb if contraction_id(self.contraction_type) == 0 else None
+            radiance, opacity, depth, num_samples_across_rays = utils.render_image(
+                self.radiance_field, self.occupancy_grid, rays, ray_marching_aabb, self.near_plane, self.far_plane,
+                self.render_step_size, self.render_bkgd, self.cone_angle, self.early_stop_eps, self.alpha_thre,
+                self.test_chunk_size)
+        # nerf.py:279-286
+        radiance = radiance.squeeze(dim=-1)
+        opacity = opacity.squeeze(dim=-1)
+        depth = depth.squeeze(dim=-1)
+        depth = depth / (opacity + self.opacity_eps)
+        num_rays = ray_origin.numel() // ray_origin.shape[-1]
+        mean_num_samples_per_ray = num_samples_across_rays / num_rays
+        return radiance, opacity, depth, mean_num_samples_per_ray
+
+
+__all__ = ["NeRF", "ContractionType", "shifted_softplus"]

@@ -37,6 +37,13 @@
  *   den_event_target
  *   den_adam_step    <- torch.optim.Adam as configured by
  *                       deblur_e_nerf/models/deblur_e_nerf.py:1055-1112
+ *   den_march_* / den_visibility / den_compact / den_pack_info / den_exclusive_scan
+ *                    <- nerfacc 0.3.1 ray_marching (+ render_visibility), called at
+ *                       deblur_e_nerf/external/utils.py:106-119
+ *   den_composite_*  <- deblur_e_nerf/external/vol_rendering.py:81-126 (nerfacc
+ *                       render_weight_from_density + accumulate_along_rays)
+ *   den_occ_*        <- nerfacc OccupancyGrid.every_n_step, called at
+ *                       deblur_e_nerf/models/nerf.py:170-204
  */
 #ifndef DEN_API_H
 #define DEN_API_H
@@ -48,7 +55,7 @@
 extern "C" {
 #endif
 
-#define DEN_VERSION 1
+#define DEN_VERSION 2
 
 enum den_status {
   DEN_OK = 0,
@@ -80,12 +87,21 @@ typedef struct den_render_desc {
   float far_plane;         /* < 0 => none */
   int32_t train;           /* 1: keep activations in the workspace for den_render_bwd */
   int32_t has_bkgd;        /* 1: composite over bkgd (render_bkgd, nerf.py:219-230) */
-  int32_t points;          /* 1: evaluate the radiance field at given points instead of
-                              rendering rays (VanillaNeRFRadianceField.forward, mlp.py:350-358):
+  int32_t points;          /* 0: render rays with the fused fixed-count sampler + compositing.
+                              1: evaluate the radiance field at given points instead
+                              (VanillaNeRFRadianceField.forward, mlp.py:350-358):
                               rays_o/rays_d = per-point positions/directions (n,3),
                               n = n_rays*n_samples; out_rgb = rgb (n,rd), out_opacity =
                               sigma (n); in den_render_bwd d_rgb/d_opacity are dL/drgb,
-                              dL/dsigma per point. */
+                              dL/dsigma per point.
+                              2: the same for packed ray-marching samples (the rgb_sigma_fn
+                              closure of external/utils.py:83-96): sample s is at
+                              rays_o[r] + rays_d[r] * (t_starts[s] + t_ends[s]) / 2 with
+                              r = ray_indices[s], viewed along rays_d[r]; n = n_rays*n_samples
+                              samples (pad with zero-length samples of any valid ray). */
+  int32_t contraction;     /* input-space contraction (mlp.py:321-335): 0 AABB, 1 tanh
+                              (ngp.py:96-106), 2 unbounded sphere (ngp.py:68-93); the
+                              fixed-count sampler (points = 0) needs 0 */
 } den_render_desc;
 
 /* Device buffers of one render call. */
@@ -101,6 +117,9 @@ typedef struct den_render_io {
   float* out_rgb;          /* (R,rd) composited radiance */
   float* out_opacity;      /* (R) */
   float* out_depth;        /* (R) sum_i w_i t_mid_i (not yet divided by opacity) */
+  const int32_t* ray_indices; /* points = 2: (n) ray of each packed sample */
+  const float* t_starts;   /* points = 2: (n) */
+  const float* t_ends;     /* points = 2: (n) */
 } den_render_io;
 
 /* Upstream gradients / outputs of den_render_bwd. */
@@ -262,6 +281,69 @@ int den_event_prep(int32_t N, int32_t has_diff, int32_t has_tv, const int64_t* n
  * ray_o, ray_d (M,N,3): exactly the (R,3) ray layout den_render_fwd reads, R = M*N. */
 int den_pixel_rays(int32_t M, int32_t N, const float* k_inv, const float* pixel, const float* t_pos,
                    const float* t_rot, float* ray_o, float* ray_d, void* stream);
+
+/* ---------------------------------------------------------------- packed rendering (nerfacc path)
+ * The reference's occupancy-grid marching + volume rendering (models/nerf.py:98-102,170-204,
+ * 230-286 -> external/utils.py:38-140 -> external/vol_rendering.py:16-128), i.e. nerfacc 0.3.1's
+ * ray_marching / render_visibility / render_weight_from_density / accumulate_along_rays /
+ * OccupancyGrid (environment.yml:32; restated, not vendored).  Packed samples are sorted by
+ * ray; offsets (n_rays + 1) i64 = exclusive scan of the per-ray counts (packed_info).
+ * Grids are (res0, res1, res2) u8 in meshgrid "ij" order, 1 = occupied. */
+
+/* t_min / t_max per ray: AABB slab test (aabb NULL: 0 / 1e10; a miss: 1e10 / 1e10), clamped by
+ * near / far (< 0: none), then t_min += jitter * step when jitter != NULL (stratified)
+ * (nerfacc ray_marching prologue, called at external/utils.py:106-119). */
+int den_march_prep(int32_t n_rays, const float* rays_o, const float* rays_d, const float* aabb, float near_plane,
+                   float far_plane, const float* jitter, float step, float* t_min, float* t_max, void* stream);
+/* Per-ray sample counts of the constant / cone step march with occupancy skipping (DDA skip for
+ * the AABB contraction).  grid NULL: no skipping (roi/res unused). */
+int den_march_count(int32_t n_rays, const float* rays_o, const float* rays_d, const float* t_min, const float* t_max,
+                    const float* roi, const int32_t* res, const uint8_t* grid, int32_t contraction, float step,
+                    float cone, int32_t* counts, void* stream);
+/* The same march writing the packed samples at offsets (from den_exclusive_scan of the counts). */
+int den_march_fill(int32_t n_rays, const float* rays_o, const float* rays_d, const float* t_min, const float* t_max,
+                   const float* roi, const int32_t* res, const uint8_t* grid, int32_t contraction, float step,
+                   float cone, const int64_t* offsets, int32_t* ray_indices, float* t_starts, float* t_ends,
+                   void* stream);
+/* offsets[0..n] = exclusive scan of counts[0..n) (offsets[n] = total). */
+size_t den_scan_workspace_bytes(int64_t n);
+int den_exclusive_scan(int64_t n, const int32_t* counts, int64_t* offsets, void* workspace, void* stream);
+/* offsets (n_rays + 1) of n samples with sorted ray_indices (nerfacc pack_info). */
+int den_pack_info(int32_t n_rays, int64_t n, const int32_t* ray_indices, int64_t* offsets, void* stream);
+/* render_visibility: alpha = 1 - exp(-sigma (t1 - t0)) (or given alphas), T = exclusive cumprod
+ * (1 - alpha); keep = T >= early_stop_eps [and alpha >= alpha_thre when alpha_thre > 0];
+ * counts = kept samples per ray. */
+int den_visibility(int32_t n_rays, const int64_t* offsets, const float* t_starts, const float* t_ends,
+                   const float* sigmas, const float* alphas, float early_stop_eps, float alpha_thre, uint8_t* keep,
+                   int32_t* counts, void* stream);
+/* Keep the samples with keep != 0, at out_offsets (exclusive scan of den_visibility's counts). */
+int den_compact(int32_t n_rays, const int64_t* offsets, const uint8_t* keep, const int64_t* out_offsets,
+                const int32_t* ray_indices, const float* t_starts, const float* t_ends, int32_t* out_ray_indices,
+                float* out_t_starts, float* out_t_ends, void* stream);
+/* vol_rendering.rendering after rgb_sigma_fn: weights from density, colours (n_rays, rd),
+ * opacities (n_rays), depths (n_rays) = sum w (t0 + t1)/2, colours += bkgd (1 - opacity). */
+int den_composite_fwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts, const float* t_ends,
+                      const float* sigmas, const float* rgbs, const float* bkgd, float* colors, float* opacities,
+                      float* depths, void* stream);
+/* Its adjoint: d_sigmas (n), d_rgbs (n, rd) overwritten; d_bkgd (rd, may be NULL) overwritten,
+ * using workspace of den_composite_workspace_bytes. d_opacities / d_depths may be NULL. */
+size_t den_composite_workspace_bytes(int32_t n_rays, int32_t rd);
+int den_composite_bwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts, const float* t_ends,
+                      const float* sigmas, const float* rgbs, const float* bkgd, const float* d_colors,
+                      const float* d_opacities, const float* d_depths, float* d_sigmas, float* d_rgbs, float* d_bkgd,
+                      void* workspace, void* stream);
+/* OccupancyGrid._update, part 1: world positions of the sampled cells (cell index + jitter in
+ * [0,1)^3, / res, inverse contraction); mask = 0 for cells outside the unit sphere (sphere
+ * contraction); marks the sampled cells in `sampled` (cells bytes, zero on entry). */
+int den_occ_points(int64_t m, const int64_t* cell_indices, const float* jitter, const int32_t* res, const float* roi,
+                   int32_t contraction, float* points, uint8_t* mask, uint8_t* sampled, void* stream);
+/* part 2, after the density at the points: occs[c] *= ema_decay on the sampled cells, then
+ * occs[idx] = max(occs[idx], sigma * step) (step_sizes (m) or the constant step_size), then
+ * binary = occs > min(mean(occs), occ_thre).  Clears `sampled`.  workspace: den_occ_workspace_bytes. */
+size_t den_occ_workspace_bytes(void);
+int den_occ_update(int64_t m, const int64_t* cell_indices, const uint8_t* mask, const float* sigmas,
+                   const float* step_sizes, float step_size, float ema_decay, float occ_thre, int64_t cells,
+                   float* occs, uint8_t* sampled, uint8_t* binary, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------- reductions / optimizer */
 /* out[j] = sum_b partial[j*n_blocks + b] for j < n (deterministic order). */

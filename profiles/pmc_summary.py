@@ -38,6 +38,50 @@ def per_launch(path, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
+def per_launch_all(path):
+    """{kernel: {counter: mean per launch}} of one --pmc pass."""
+    acc = defaultdict(lambda: defaultdict(list))
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            k = short(row["Kernel_Name"])
+            if k:
+                acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def mfma_summary(out_dir, tag, n_simd=1024):
+    """MFMA utilisation and stall breakdown per kernel from the two SQ passes of
+    profiles/gpu_r02a.sh.  Calibration: SQ_VALU_MFMA_BUSY_CYCLES = 32 x SQ_INSTS_MFMA for
+    v_mfma_f32_32x32x16_bf16 (MI355X_MICROARCH.md), summed over the SIMDs; GRBM_GUI_ACTIVE is the
+    sum over the 8 XCDs, so the kernel's clock cycles are GRBM_GUI_ACTIVE / 8; utilisation =
+    MFMA busy / (1024 SIMDs x kernel cycles).  SQ_WAVE_CYCLES and the SQ_WAIT_* / SQ_ACTIVE_*
+    counters are in the same (quad-cycle) unit, so their ratios are wave-time fractions."""
+    a = per_launch_all(os.path.join(out_dir, "pmc_mfma", "run_counter_collection.csv"))
+    b = per_launch_all(os.path.join(out_dir, "pmc_mfma2", "run_counter_collection.csv"))
+    res = {}
+    for k in a:
+        c = dict(a[k])
+        c.update(b.get(k, {}))
+        cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+        wave = c["SQ_WAVE_CYCLES"]
+        res[k] = {"counters_per_launch": {n: round(v) for n, v in sorted(c.items())},
+                  "kernel_cycles": round(cycles),
+                  "mfma_util": round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (n_simd * cycles), 4),
+                  "mfma_busy_per_inst": round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / max(c.get("SQ_INSTS_MFMA", 1), 1), 2),
+                  "wave_frac_wait_any": round(c["SQ_WAIT_ANY"] / wave, 4),
+                  "wave_frac_wait_inst_any": round(c.get("SQ_WAIT_INST_ANY", 0) / wave, 4),
+                  "wave_frac_active_inst_any": round(c.get("SQ_ACTIVE_INST_ANY", 0) / wave, 4),
+                  "wave_frac_wait_inst_lds": round(c["SQ_WAIT_INST_LDS"] / wave, 4),
+                  "lds_bank_conflict_frac": round(c["SQ_LDS_BANK_CONFLICT"] / max(c.get("SQ_LDS_IDX_ACTIVE", 1), 1), 4),
+                  "valu_mfma_coexec_frac": round(c.get("SQ_VALU_MFMA_COEXEC_CYCLES", 0) / max(
+                      c["SQ_VALU_MFMA_BUSY_CYCLES"], 1), 4)}
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), f"{tag}_pmc_mfma.json"), "w") as f:
+        json.dump({"source": f"rocprofv3 --pmc, two SQ passes ({tag}); see pmc_summary.mfma_summary",
+                   "command": "bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak", "kernels": res}, f,
+                  indent=1)
+    return res
+
+
 def main(out_dir, tag):
     here = os.path.dirname(os.path.abspath(__file__))
     fetch = per_launch(os.path.join(out_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
@@ -50,7 +94,7 @@ def main(out_dir, tag):
                    "hbm_bytes_per_launch": rd + wr}
     res = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes ({tag}); "
                      "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes",
-           "command": "bench.py --steps 1 --warmup 1 --no-cpu-baseline (profiles/gpu_round.sh)",
+           "command": "bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak (profiles/gpu_r02a.sh)",
            "workload": {"rays": 131072, "samples": 128, "mode": "bf16", "rd": 1},
            "kernels": kern}
     with open(os.path.join(here, "pmc_traffic.json"), "w") as f:
@@ -61,7 +105,7 @@ def main(out_dir, tag):
             rows.append(r)
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
              "Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python bench.py --steps 5 --warmup 2 "
-             "--no-cpu-baseline` (profiles/gpu_round.sh); 7 train steps + 3 phase-timing reps per kernel.", "",
+             "--no-cpu-baseline --no-gemm-peak` (profiles/gpu_r02a.sh); 7 train steps + 3 phase-timing reps per kernel.", "",
              "| kernel | calls | avg ms | total % |", "|---|---|---|---|"]
     for r in rows[:20]:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | "
@@ -71,6 +115,16 @@ def main(out_dir, tag):
     for k, v in kern.items():
         lines.append(f"| `{k}` | {v['hbm_read_bytes_per_launch'] / 1e9:.2f} | "
                      f"{v['hbm_write_bytes_per_launch'] / 1e9:.2f} | {v['hbm_bytes_per_launch'] / 1e9:.2f} |")
+    if os.path.exists(os.path.join(out_dir, "pmc_mfma", "run_counter_collection.csv")):
+        mf = mfma_summary(out_dir, tag)
+        lines += ["", f"MFMA utilisation and wave-time breakdown (separate SQ passes, profiles/{tag}_pmc_mfma.json):",
+                  "", "| kernel | MFMA util | wait (waitcnt/barrier) | issue stall | active | LDS-issue stall | "
+                  "LDS bank-conflict share | VALU-MFMA co-exec / MFMA busy |", "|---|---|---|---|---|---|---|---|"]
+        for k, v in mf.items():
+            lines.append(f"| `{k}` | {v['mfma_util']:.3f} | {v['wave_frac_wait_any']:.2f} | "
+                         f"{v['wave_frac_wait_inst_any']:.2f} | {v['wave_frac_active_inst_any']:.2f} | "
+                         f"{v['wave_frac_wait_inst_lds']:.3f} | {v['lds_bank_conflict_frac']:.2f} | "
+                         f"{v['valu_mfma_coexec_frac']:.2f} |")
     with open(os.path.join(here, f"{tag}_kernel_stats.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print(json.dumps(kern, indent=1))
