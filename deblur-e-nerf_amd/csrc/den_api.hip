@@ -449,8 +449,19 @@ int den_adam_step(int64_t n, float* p, const float* g, float* m, float* v, float
   const double bc2 = 1.0 - std::pow(b2, (double)step);
   const float step_size = (float)((double)lr / bc1);
   const float bc2s = (float)std::sqrt(bc2);
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, p, g, m,
-                     v, step_size, (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), eps, wd, bc2s);
+  hipLaunchKernelGGL(adam_kernel<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, p, g,
+                     m, v, step_size, (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), eps, wd, bc2s);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_adam_step_f64(int64_t n, double* p, const double* g, double* m, double* v, double lr, double beta1,
+                      double beta2, double eps, double wd, int64_t step, void* stream) {
+  if (n <= 0 || !p || !g || !m || !v || step < 1) return fail(DEN_EINVAL, "bad arguments");
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  hipLaunchKernelGGL(adam_kernel<double>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, p,
+                     g, m, v, lr / bc1, 1.0 - beta1, beta2, 1.0 - beta2, eps, wd, std::sqrt(bc2));
   DEN_LAUNCHED();
   return DEN_OK;
 }
@@ -913,6 +924,80 @@ int den_occ_update(int64_t m, const int64_t* cell_indices, const uint8_t* mask, 
   hipLaunchKernelGGL(occ_mean_partial_kernel, dim3(OCC_NB), dim3(OCC_BLOCK), 0, st, A);
   DEN_LAUNCHED();
   hipLaunchKernelGGL(occ_binary_kernel, dim3(1024), dim3(256), 0, st, A, OCC_NB);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_trajectory(int64_t n, int32_t C, const int64_t* cam_ts, const float* cam_pos, const float* cam_quat,
+                   const double* query_ts, float* position, float* rotation, int32_t* status, void* stream) {
+  if (n < 0 || C < 2 || !cam_ts || !cam_pos || !cam_quat || (n > 0 && (!query_ts || !position || !rotation)))
+    return fail(DEN_EINVAL, "bad arguments (a trajectory needs >= 2 poses)");
+  if (n == 0) return DEN_OK;
+  TrajArgs T{n, C, cam_ts, cam_pos, cam_quat, query_ts, position, rotation, status};
+  hipLaunchKernelGGL(trajectory_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, T);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+size_t den_event_prep_workspace_bytes(int32_t N) {
+  return N > 0 ? (size_t)(4 * ((N + PREP_BWD_BLOCK - 1) / PREP_BWD_BLOCK)) * sizeof(double) : 0;
+}
+
+int den_event_prep_bwd(int32_t N, int32_t has_diff, int32_t has_tv, const int64_t* num_pos, const int64_t* num_neg,
+                       const int64_t* end_ts, const int64_t* start_ts, const double* norm, const float* ct,
+                       const double* refractory, const float* norm_c, const float* g_lid, const double* g_start,
+                       const double* g_render_ts, const double* g_ts_diff, const double* g_ts_subdiff,
+                       const float* g_target, void* workspace, double* d_params, void* stream) {
+  if (N <= 0 || !num_pos || !num_neg || !end_ts || !start_ts || !norm || !ct || !refractory || !workspace ||
+      !d_params || (g_target && (!norm_c || !has_diff)))
+    return fail(DEN_EINVAL, "bad arguments");
+  EventPrepBwdArgs B{};
+  B.F = EventPrepArgs{N, has_diff ? 1 : 0, has_tv ? 1 : 0, num_pos, num_neg, end_ts, start_ts, norm, ct, refractory,
+                      norm_c, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  B.g_lid = g_lid;
+  B.g_start = g_start;
+  B.g_render = g_render_ts;
+  B.g_ts_diff = g_ts_diff;
+  B.g_ts_subdiff = g_ts_subdiff;
+  B.g_target = g_target;
+  B.part = (double*)workspace;
+  const int nb = (N + PREP_BWD_BLOCK - 1) / PREP_BWD_BLOCK;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(event_prep_bwd_kernel, dim3(nb), dim3(PREP_BWD_BLOCK), 0, st, B);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(sum_partials_f64_kernel, dim3(4), dim3(256), 0, st, 4, nb, (const double*)B.part, d_params);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_event_target_bwd(int32_t N, const double* ts_diff, const float* lid, const int64_t* end_ts,
+                         const double* start_ts, const float* norm_c, const float* g_target, double* d_ts_diff,
+                         float* d_lid, double* d_start, void* workspace, double* d_c, void* stream) {
+  if (N <= 0 || !ts_diff || !lid || !end_ts || !start_ts || !norm_c || !g_target || !workspace || !d_c)
+    return fail(DEN_EINVAL, "bad arguments");
+  const int nb = (N + PREP_BWD_BLOCK - 1) / PREP_BWD_BLOCK;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(event_target_bwd_kernel, dim3(nb), dim3(PREP_BWD_BLOCK), 0, st, N, ts_diff, lid, end_ts, start_ts,
+                     norm_c, g_target, d_ts_diff, d_lid, d_start, (double*)workspace);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(sum_partials_f64_kernel, dim3(1), dim3(256), 0, st, 1, nb, (const double*)workspace, d_c);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+size_t den_image_error_workspace_bytes(int32_t n_img) {
+  return n_img > 0 ? (size_t)n_img * 2 * IMG_SLICES * sizeof(double) : 0;
+}
+
+int den_image_error(int32_t n_img, int64_t pixels, const float* pred, const float* target, void* workspace,
+                    double* sse_sae, void* stream) {
+  if (n_img <= 0 || pixels <= 0 || !pred || !target || !workspace || !sse_sae) return fail(DEN_EINVAL, "bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(image_error_kernel, dim3(IMG_SLICES, n_img), dim3(IMG_BLOCK), 0, st, pixels, pred, target,
+                     (double*)workspace);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(sum_partials_f64_kernel, dim3(2 * n_img), dim3(256), 0, st, 2 * n_img, IMG_SLICES,
+                     (const double*)workspace, sse_sae);
   DEN_LAUNCHED();
   return DEN_OK;
 }

@@ -93,19 +93,20 @@ __global__ void pack_kernel(PackArgs P) {
 //   p += -(lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
 // Scalars are formed in double on the host and rounded to f32 exactly as torch
 // rounds its Python-float scalars.
-__global__ void adam_kernel(int64_t n, float* p, const float* g, float* m, float* v, float step_size, float w1,
-                            float b2, float w2, float eps, float wd, float bc2_sqrt) {
+template <typename T>
+__global__ void adam_kernel(int64_t n, T* p, const T* g, T* m, T* v, T step_size, T w1, T b2, T w2, T eps, T wd,
+                            T bc2_sqrt) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float gi = g[i];
-  const float pi = p[i];
-  if (wd != 0.0f) gi = gi + wd * pi;
-  const float mo = m[i];
-  const float mi = w1 < 0.5f ? mo + w1 * (gi - mo) : gi - (gi - mo) * (1.0f - w1);
-  const float vi = v[i] * b2 + w2 * gi * gi;
+  T gi = g[i];
+  const T pi = p[i];
+  if (wd != T(0)) gi = gi + wd * pi;
+  const T mo = m[i];
+  const T mi = w1 < T(0.5) ? mo + w1 * (gi - mo) : gi - (gi - mo) * (T(1) - w1);
+  const T vi = v[i] * b2 + w2 * gi * gi;
   m[i] = mi;
   v[i] = vi;
-  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  const T denom = sqrt(vi) / bc2_sqrt + eps;
   p[i] = pi + (-step_size) * (mi / denom);
 }
 
@@ -338,6 +339,37 @@ __global__ void event_step_bwd_kernel(EventStepArgs E) {
     const int64_t base = ((int64_t)g * E.N + i) * E.rd;
     const float I = E.radiance[base + ch] + E.min_int;
     for (int k = 0; k < E.rd; ++k) E.d_radiance[base + k] = (k == ch) ? dy[g] / I : 0.0f;
+  }
+}
+
+// ------------------------------------------------------------------ image errors (Metric.compute, metric.py:28-92)
+// per image b: sum of squared and of absolute pixel errors (f64 accumulation), one block per
+// (image, slice); partials [img][2][slices] reduced in a fixed order by sum_partials_f64_kernel.
+constexpr int IMG_BLOCK = 256, IMG_SLICES = 64;
+__global__ void image_error_kernel(int64_t pix, const float* pred, const float* target, double* part) {
+  const int b = blockIdx.y, sl = blockIdx.x;
+  const float* p = pred + (int64_t)b * pix;
+  const float* t = target + (int64_t)b * pix;
+  double se = 0.0, ae = 0.0;
+  for (int64_t k = (int64_t)sl * IMG_BLOCK + threadIdx.x; k < pix; k += (int64_t)IMG_SLICES * IMG_BLOCK) {
+    const double d = (double)p[k] - (double)t[k];
+    se += d * d;
+    ae += fabs(d);
+  }
+  __shared__ double s0[IMG_BLOCK], s1[IMG_BLOCK];
+  s0[threadIdx.x] = se;
+  s1[threadIdx.x] = ae;
+  __syncthreads();
+  for (int w = IMG_BLOCK / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      s0[threadIdx.x] += s0[threadIdx.x + w];
+      s1[threadIdx.x] += s1[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[((int64_t)b * 2 + 0) * IMG_SLICES + sl] = s0[0];
+    part[((int64_t)b * 2 + 1) * IMG_SLICES + sl] = s1[0];
   }
 }
 }  // namespace den

@@ -97,6 +97,14 @@ _SIGS = {
     "den_composite_fwd": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 10),
     "den_composite_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32] * 2),
     "den_composite_bwd": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 14),
+    "den_event_prep_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "den_event_prep_bwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 17),
+    "den_event_target_bwd": (ctypes.c_int, [ctypes.c_int32] + [ctypes.c_void_p] * 12),
+    "den_image_error_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "den_image_error": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64] + [ctypes.c_void_p] * 5),
+    "den_adam_step_f64": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_double] * 5
+                          + [ctypes.c_int64, ctypes.c_void_p]),
+    "den_trajectory": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 8),
     "den_occ_workspace_bytes": (ctypes.c_size_t, []),
     "den_occ_points": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int32]
                        + [ctypes.c_void_p] * 4),
@@ -328,8 +336,9 @@ def sum_partials(part, n, nb, out):
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):
     _require_device(param, grad, exp_avg, exp_avg_sq)
-    _check(lib().den_adam_step(param.numel(), _ptr(param), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), lr, beta1,
-                               beta2, eps, weight_decay, int(step), _stream(param.device)))
+    fn = lib().den_adam_step_f64 if param.dtype == torch.float64 else lib().den_adam_step
+    _check(fn(param.numel(), _ptr(param), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), lr, beta1, beta2, eps,
+              weight_decay, int(step), _stream(param.device)))
 
 
 # ----------------------------------------------------------------------------- event loss
@@ -501,4 +510,114 @@ def pixel_rays(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientati
     _check(lib().den_pixel_rays(M, N, _ptr(intrinsics_inverse), _ptr(pixel_position), _ptr(T_wc_position),
                                 _ptr(T_wc_orientation), _ptr(out[0]), _ptr(out[1]),
                                 _stream(pixel_position.device)))
+    return out
+
+
+def trajectory(cam_ts, cam_pos, cam_quat, query_ts, status=None):
+    """den_trajectory (LinearTrajectory.forward): pose stamps (C) i64, positions (C,3) f32, XYZW
+    quaternions (C,4) f32, query timestamps (...) f64 -> positions (..., 3), rotations (..., 3, 3).
+    ``status`` (device i32, optional) gets bit 0 for queries outside the pose span."""
+    _require_device(cam_ts, cam_pos, cam_quat, query_ts, status)
+    shape = query_ts.shape
+    q = query_ts.reshape(-1).to(torch.float64).contiguous()
+    n = q.numel()
+    C = cam_ts.numel()
+    pos = torch.empty(n, 3, dtype=torch.float32, device=q.device)
+    rot = torch.empty(n, 3, 3, dtype=torch.float32, device=q.device)
+    _check(lib().den_trajectory(n, C, _ptr(cam_ts.to(torch.int64).contiguous()),
+                                _ptr(cam_pos.to(torch.float32).contiguous()),
+                                _ptr(cam_quat.to(torch.float32).contiguous()), _ptr(q), _ptr(pos), _ptr(rot),
+                                _ptr(status), _stream(q.device)))
+    return pos.reshape(*shape, 3), rot.reshape(*shape, 3, 3)
+
+
+class EventTargetFunction(torch.autograd.Function):
+    """The normalised diff-loss target f32(ts_diff * (lid / (end - start)) / c) (loss.py:72-78),
+    differentiable in ts_diff, lid, start and c (den_event_target / den_event_target_bwd)."""
+
+    @staticmethod
+    def forward(ctx, ts_diff, lid, end_ts, start_ts, c):
+        _require_device(ts_diff, lid, end_ts, start_ts, c)
+        td = ts_diff.to(torch.float64).contiguous()
+        ld = lid.to(torch.float32).contiguous()
+        et = end_ts.to(torch.int64).contiguous()
+        st = start_ts.to(torch.float64).contiguous()
+        cc = c.to(torch.float32).reshape(1).contiguous()
+        N = ld.numel()
+        out = torch.empty(N, dtype=torch.float32, device=ld.device)
+        _check(lib().den_event_target(N, _ptr(td), _ptr(ld), _ptr(et), _ptr(st), _ptr(cc), _ptr(out),
+                                      _stream(ld.device)))
+        ctx.save_for_backward(td, ld, et, st, cc)
+        ctx.dtypes = (ts_diff.dtype, lid.dtype, start_ts.dtype, c.dtype, c.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        td, ld, et, st, cc = ctx.saved_tensors
+        N, dev = ld.numel(), ld.device
+        g = g.to(torch.float32).contiguous()
+        d_td = torch.empty(N, dtype=torch.float64, device=dev) if ctx.needs_input_grad[0] else None
+        d_ld = torch.empty(N, dtype=torch.float32, device=dev) if ctx.needs_input_grad[1] else None
+        d_st = torch.empty(N, dtype=torch.float64, device=dev) if ctx.needs_input_grad[3] else None
+        d_c = torch.empty(1, dtype=torch.float64, device=dev)
+        ws = torch.empty(max(1, lib().den_event_prep_workspace_bytes(N) // 8), dtype=torch.float64, device=dev)
+        _check(lib().den_event_target_bwd(N, _ptr(td), _ptr(ld), _ptr(et), _ptr(st), _ptr(cc), _ptr(g), _ptr(d_td),
+                                          _ptr(d_ld), _ptr(d_st), _ptr(ws), _ptr(d_c), _stream(dev)))
+        t_dt, l_dt, s_dt, c_dt, c_shape = ctx.dtypes
+        return (None if d_td is None else d_td.to(t_dt), None if d_ld is None else d_ld.to(l_dt), None,
+                None if d_st is None else d_st.to(s_dt), d_c.to(c_dt).reshape(c_shape))
+
+
+class EventPrepFunction(torch.autograd.Function):
+    """den_event_prep with its reverse mode (den_event_prep_bwd): differentiable in C+ / C- (ct,
+    (2) f32), tau_r (refractory, (1) f64) and the normalising constant c (norm_c, (1) f32).
+    -> lid (N) f32, start_ts (N) f64, render_ts (4,N) f64, ts_diff (N) f64, ts_subdiff (N) f64,
+    target (N) f32 (zeros when norm_c is None)."""
+
+    @staticmethod
+    def forward(ctx, num_pos, num_neg, end_ts, start_ts, normalized, ct, refractory, norm_c, has_diff, has_tv):
+        out = event_prep(num_pos, num_neg, end_ts, start_ts, normalized, ct.detach().float().contiguous(),
+                         refractory.detach().double().reshape(1).contiguous(),
+                         None if norm_c is None else norm_c.detach().float().reshape(1).contiguous(),
+                         has_diff=has_diff, has_tv=has_tv)
+        tgt = out["target"] if out["target"] is not None else torch.zeros_like(out["lid"])
+        ctx.save_for_backward(num_pos, num_neg, end_ts, start_ts, normalized, ct.detach().float().contiguous(),
+                              refractory.detach().double().reshape(1).contiguous(),
+                              None if norm_c is None else norm_c.detach().float().reshape(1).contiguous())
+        ctx.flags = (has_diff, has_tv, norm_c is not None)
+        ctx.shapes = (ct.shape, ct.dtype, refractory.shape, refractory.dtype,
+                      None if norm_c is None else (norm_c.shape, norm_c.dtype))
+        return out["lid"], out["start_ts"], out["render_ts"], out["ts_diff"], out["ts_subdiff"], tgt
+
+    @staticmethod
+    def backward(ctx, g_lid, g_start, g_render, g_tsd, g_tss, g_tgt):
+        num_pos, num_neg, end_ts, start_ts, norm, ct, tau, c = ctx.saved_tensors
+        has_diff, has_tv, has_c = ctx.flags
+        N, dev = end_ts.numel(), end_ts.device
+        f = lambda t, dt: None if t is None else t.to(dt).contiguous()  # noqa: E731
+        ws = torch.empty(max(1, lib().den_event_prep_workspace_bytes(N) // 8), dtype=torch.float64, device=dev)
+        d = torch.empty(4, dtype=torch.float64, device=dev)
+        _check(lib().den_event_prep_bwd(N, int(has_diff), int(has_tv), _ptr(num_pos), _ptr(num_neg), _ptr(end_ts),
+                                        _ptr(start_ts), _ptr(norm), _ptr(ct), _ptr(tau), _ptr(c),
+                                        _ptr(f(g_lid, torch.float32)), _ptr(f(g_start, torch.float64)),
+                                        _ptr(f(g_render, torch.float64)), _ptr(f(g_tsd, torch.float64)),
+                                        _ptr(f(g_tss, torch.float64)),
+                                        _ptr(f(g_tgt, torch.float32)) if has_c else None, _ptr(ws), _ptr(d),
+                                        _stream(dev)))
+        ct_shape, ct_dtype, tau_shape, tau_dtype, c_meta = ctx.shapes
+        d_c = None if c_meta is None else d[3:4].to(c_meta[1]).reshape(c_meta[0])
+        return (None, None, None, None, None, d[:2].to(ct_dtype).reshape(ct_shape),
+                d[2:3].to(tau_dtype).reshape(tau_shape), d_c, None, None)
+
+
+def image_error(pred, target):
+    """den_image_error: (B, ...) images -> (B, 2) f64 [sum of squared errors, sum of absolute errors]."""
+    _require_device(pred, target)
+    assert pred.shape == target.shape
+    B = pred.shape[0]
+    p = pred.reshape(B, -1).to(torch.float32).contiguous()
+    t = target.reshape(B, -1).to(torch.float32).contiguous()
+    ws = torch.empty(lib().den_image_error_workspace_bytes(B) // 8, dtype=torch.float64, device=p.device)
+    out = torch.empty(B, 2, dtype=torch.float64, device=p.device)
+    _check(lib().den_image_error(B, p.shape[1], _ptr(p), _ptr(t), _ptr(ws), _ptr(out), _stream(p.device)))
     return out

@@ -1,0 +1,467 @@
+"""DeblurENeRF -- mirror of the reference's LightningModule (models/deblur_e_nerf.py:20-1308)
+for the training path, so that scripts/run.py and PyTorch Lightning drive it unchanged.
+
+Same constructor arguments (:32-53), the same component attributes and parameter names
+(``contrast_threshold``, ``refractory_period``, ``pixel_bandwidth``, ``nerf``, ``trajectory``,
+``loss``, ``metric``), the same ``training_step(batch, batch_index)`` (:396-586),
+``render_log_intensity`` (:1129-1160), ``render_train_pixels`` (:1162-1183),
+``render_pixels`` (:1185-1221), ``bayering`` (:1223-1235), ``derive_mean_value``
+(:1237-1250), ``update_train_batch_size`` (:1252-1308) and ``configure_optimizers``
+(:1055-1112).  Every array computation of the step runs in libden.so:
+
+  den_event_prep(_bwd)   ContrastThreshold + RefractoryPeriod + the supervision timestamps
+  den_trajectory         LinearTrajectory (poses at the render timestamps)
+  den_pixel_rays         NeRF.pixel_params_to_ray
+  den_march_* / den_render (points = 2) / den_composite_*   occupancy-grid marching, the fused
+                         MLP at the packed samples, compositing (NeRF sampler "occupancy", the
+                         reference's); or den_render_fwd/bwd with the fixed-count sampler
+  den_pixbw_*            PixelBandwidth
+  den_event_target(_bwd), den_event_loss_*   Loss.compute
+  den_adam_step          optim.Adam (configure_optimizers)
+
+The pixel-bandwidth-off step renders its four supervision groups (diff start / end, TV start /
+end) in ONE render call of 4N rays instead of four: same results, one launch.
+
+Without pytorch_lightning (absent in this image) the class derives from torch.nn.Module and
+provides the few Trainer attributes the step reads (``trainer.accumulate_grad_batches``,
+``global_step``, ``log``, ``all_gather``); ``fit_step`` runs one optimisation step (forward,
+backward, DDP-style gradient all-reduce, optimizer) without a Trainer.
+
+Evaluation (validation / test epochs with the affine + black-level correction and
+SSIM / LPIPS) is outside the hot path; ``render_image_eval`` + ``loss_metric.metric`` give the
+rendered image and its PSNR.
+"""
+import functools
+import math
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from ..data import datasets
+from ..loss_metric import loss as loss_lib
+from ..loss_metric import metric as metric_lib
+from ..optim import Adam
+from ..utils import modules
+from ..utils.easydict import EasyDict
+from . import event_generation_params, nerf as nerf_lib, pixel_bandwidth as pixbw_lib, trajectories
+
+try:  # the reference's base class when PyTorch Lightning is installed
+    import pytorch_lightning as _pl
+    _Base = _pl.LightningModule
+    _HAS_PL = True
+except ImportError:  # pragma: no cover - the image has no pytorch_lightning
+    _Base = torch.nn.Module
+    _HAS_PL = False
+
+
+class _TrainerStub:
+    """What training_step reads of a pytorch_lightning Trainer when there is none."""
+
+    def __init__(self, accumulate_grad_batches=1, datamodule=None):
+        self.accumulate_grad_batches = accumulate_grad_batches
+        self.datamodule = datamodule
+
+
+class DeblurENeRF(_Base):
+    INTRINSICS_KEY = "intrinsics"
+    NUM_DIM = 3
+    MAX_NUM_SAMPLES_PER_RAY = 1024
+    MODEL_COMPONENTS = ["contrast_threshold", "refractory_period", "nerf"]
+    MULTI_PARAM_MODEL_COMPONENTS = ["contrast_threshold"]
+
+    def __init__(self, git_head_hash, eval_target, num_nodes, gpus, min_modeled_intensity,
+                 eval_save_pred_intensity_img, checkpoint_filepath, contrast_threshold, refractory_period,
+                 pixel_bandwidth, nerf, correction, loss, metric, optimizer, lr_scheduler, dataset_directory,
+                 alpha_over_white_bg, train_eff_ray_sample_batch_size):
+        super().__init__()
+        assert isinstance(min_modeled_intensity, (int, float)) and min_modeled_intensity > 0
+        for cfg in (contrast_threshold, refractory_period, nerf):
+            assert isinstance(cfg.load_state_dict, bool)
+            assert isinstance(cfg.freeze, (bool, dict))
+        assert isinstance(train_eff_ray_sample_batch_size, int) and train_eff_ray_sample_batch_size > 0
+        if nerf.freeze:
+            assert nerf.load_state_dict
+        num_gpus = num_nodes * (len(gpus) if gpus is not None else 1)
+        self.train_ray_sample_batch_size = train_eff_ray_sample_batch_size // num_gpus
+        self.eval_save_pred_intensity_img = eval_save_pred_intensity_img
+        self.correction = correction
+        self.MODEL_COMPONENTS = list(type(self).MODEL_COMPONENTS)
+        self.MULTI_PARAM_MODEL_COMPONENTS = list(type(self).MULTI_PARAM_MODEL_COMPONENTS)
+
+        cal = datasets.Event.load_camera_calibration(dataset_directory)
+        bayer = str(cal[datasets.Event.BAYER_PATTERN_KEY]) if datasets.Event.BAYER_PATTERN_KEY in cal else ""
+        self.has_bayer_filter = bayer != datasets.Event.NULL_BAYER_PATTERN
+        self.register_buffer("train_intrinsics_inv",
+                             torch.linalg.inv(torch.from_numpy(np.asarray(cal[self.INTRINSICS_KEY])).float()),
+                             persistent=False)
+        self.render_bkgd = "parameter" if alpha_over_white_bg else None
+
+        hp = EasyDict(git_head_hash=git_head_hash, min_modeled_intensity=min_modeled_intensity,
+                      checkpoint_filepath=checkpoint_filepath, contrast_threshold=contrast_threshold,
+                      refractory_period=refractory_period, pixel_bandwidth=pixel_bandwidth, nerf=nerf, loss=loss,
+                      metric=metric, optimizer=optimizer, lr_scheduler=lr_scheduler)
+        if _HAS_PL:
+            self.save_hyperparameters(dict(hp))
+        else:
+            self._hparams = hp
+            self._trainer = _TrainerStub()
+            self._global_step = 0
+            self.logged = {}
+
+        self.contrast_threshold = event_generation_params.ContrastThreshold(
+            dataset_directory, self.hparams.contrast_threshold.parameterize_mean_ct)
+        self.refractory_period = event_generation_params.RefractoryPeriod(dataset_directory)
+        camera_poses = datasets.CameraPose(dataset_directory, None)
+        if self.hparams.pixel_bandwidth.enable:
+            self.pixel_bandwidth = pixbw_lib.PixelBandwidth(
+                dataset_directory, camera_poses.camera_poses.T_wc_timestamp.min(),
+                self.hparams.pixel_bandwidth.f_c_dominant_min, self.hparams.pixel_bandwidth.target_cumprob)
+            self.MODEL_COMPONENTS.append("pixel_bandwidth")
+            self.MULTI_PARAM_MODEL_COMPONENTS.append("pixel_bandwidth")
+        self.nerf = self._build_nerf(camera_poses)
+        self.trajectory = trajectories.LinearTrajectory(camera_poses)
+        self._load_model_component_state_dicts()
+        self._freeze_model_components()
+        self.loss = loss_lib.Loss(loss.weight, loss.error_fn, loss.normalize)
+        self.metric = metric_lib.Metric(getattr(metric, "lpips_net", None))
+
+    # ------------------------------------------------------------------ trainer glue
+    if not _HAS_PL:
+        @property
+        def hparams(self):
+            return self._hparams
+
+        @property
+        def trainer(self):
+            return self._trainer
+
+        @trainer.setter
+        def trainer(self, t):
+            self._trainer = t
+
+        @property
+        def global_step(self):
+            return self._global_step
+
+        def log(self, name, value, **kwargs):
+            self.logged[name] = value.detach() if torch.is_tensor(value) else value
+
+        def all_gather(self, t):
+            t = torch.as_tensor(t, device=self.trajectory.T_wc_position.device)
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+                out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+                dist.all_gather(out, t)
+                return torch.stack(out)
+            return t[None]
+
+    # ------------------------------------------------------------------ components
+    def _build_nerf(self, camera_poses):
+        cfg = self.hparams.nerf
+        if cfg.aabb == "auto":
+            p = camera_poses.camera_poses.T_wc_position
+            aabb = torch.cat((p.min(dim=0).values, p.max(dim=0).values)).tolist()
+        else:
+            aabb = list(cfg.aabb)
+        ctype = {"aabb": nerf_lib.ContractionType.AABB, "sphere": nerf_lib.ContractionType.UN_BOUNDED_SPHERE,
+                 "tanh": nerf_lib.ContractionType.UN_BOUNDED_TANH}[cfg.contraction_type]
+        if cfg.render_step_size == "auto":
+            a = torch.tensor(aabb)
+            step = math.sqrt(self.NUM_DIM) * torch.max(a[3:] - a[:3]).item() / self.MAX_NUM_SAMPLES_PER_RAY
+        else:
+            step = cfg.render_step_size
+        rd = 3 if self.has_bayer_filter else 1
+        return nerf_lib.NeRF(aabb, ctype, cfg.occ_grid, cfg.near_plane, cfg.far_plane, step, self.render_bkgd,
+                             cfg.cone_angle, cfg.early_stop_eps, cfg.alpha_thre, cfg.test_chunk_size, cfg.arch,
+                             arch_config=cfg[cfg.arch], num_dim=self.NUM_DIM, radiance_dim=rd,
+                             sampler=cfg.get("sampler", "occupancy"), n_samples=cfg.get("n_samples", 128),
+                             mode=cfg.get("compute_mode", "f32"))
+
+    def _load_model_component_state_dicts(self):
+        if not any(self.hparams[c].load_state_dict for c in self.MODEL_COMPONENTS):
+            return
+        ckpt = torch.load(self.hparams.checkpoint_filepath, map_location="cpu", weights_only=True)
+        for c in self.MODEL_COMPONENTS:
+            if self.hparams[c].load_state_dict:
+                prefix = c + "."
+                sd = {k[len(prefix):]: v for k, v in ckpt["state_dict"].items() if k.startswith(prefix)}
+                getattr(self, c).load_state_dict(sd)
+
+    def _freeze_model_components(self):
+        for c in self.MODEL_COMPONENTS:
+            f = self.hparams[c].freeze
+            if isinstance(f, dict):
+                f = f.default
+            if f:
+                modules.freeze(getattr(self, c))
+        for c in self.MULTI_PARAM_MODEL_COMPONENTS:
+            if isinstance(self.hparams[c].freeze, bool):
+                continue
+            comp = getattr(self, c)
+            for name, fr in self.hparams[c].freeze.items():
+                if name == "default":
+                    continue
+                getattr(comp.parametrizations, name).original.requires_grad_(not fr)
+
+    # ------------------------------------------------------------------ training step
+    def forward(self, batch):
+        pass
+
+    def training_step(self, batch, batch_index):
+        batch = EasyDict(batch)
+        batch.size = batch.event.start_ts.numel()
+        for v in batch.normalized.values():
+            assert v.shape[-1] == batch.size
+        for k, v in batch.event.items():
+            batch.event[k] = v.squeeze(dim=0)
+        for k, v in batch.normalized.items():
+            batch.normalized[k] = v.squeeze(dim=0)
+        if self.has_bayer_filter:
+            batch.event.channel_idx = batch.event.channel_idx.to(torch.int64)
+        else:
+            batch.event.channel_idx = None
+        w = self.hparams.loss.weight
+        has_diff, has_tv = w.log_intensity_diff > 0, w.log_intensity_tv > 0
+        dev = batch.event.end_ts.device
+        N = batch.size
+
+        # ContrastThreshold + RefractoryPeriod + supervision timestamps (deblur_e_nerf.py:414-455),
+        # one fused kernel with its reverse mode (gradients into C+/C-/tau_r when unfrozen)
+        zeros = torch.zeros(N, dtype=torch.float64, device=dev)
+        nz = batch.normalized
+        norm = torch.stack([nz.get("ts_diff", zeros), nz.get("diff_start_ts", zeros), nz.get("ts_subdiff", zeros),
+                            nz.get("subdiff_start_ts", zeros)]).to(torch.float64).contiguous()
+        ct = torch.stack([self.contrast_threshold.pos_contrast_threshold,
+                          self.contrast_threshold.neg_contrast_threshold]).reshape(2)
+        tau = self.refractory_period.refractory_period.reshape(1)
+        ev = batch.event
+        lid, start_ts, render_ts, ts_diff, ts_subdiff, _ = _native.EventPrepFunction.apply(
+            ev.num_pos.to(torch.int64).contiguous(), ev.num_neg.to(torch.int64).contiguous(),
+            ev.end_ts.to(torch.int64).contiguous(), ev.start_ts.to(torch.int64).contiguous(), norm, ct, tau, None,
+            has_diff, has_tv)
+        ev.log_intensity_diff = lid
+        ev.start_ts = start_ts
+        ev.pop("num_pos")
+        ev.pop("num_neg")
+        batch.diff = EasyDict(ts_diff=ts_diff, start_ts=render_ts[0], end_ts=render_ts[1]) if has_diff else None
+        batch.subdiff = EasyDict(ts_diff=ts_subdiff, start_ts=render_ts[2], end_ts=render_ts[3]) if has_tv else None
+        interval_gen = batch.normalized.get("interval_gen", None)
+        batch.pop("normalized")
+
+        if batch_index % self.trainer.accumulate_grad_batches == 0:
+            self.nerf.update_occ_grid(step=self.global_step, T_wc_position=self.trajectory.T_wc_position)
+
+        groups = [(batch.diff, "start"), (batch.diff, "end")] if has_diff else []
+        groups += [(batch.subdiff, "start"), (batch.subdiff, "end")] if has_tv else []
+        if self.hparams.pixel_bandwidth.enable:
+            # stateful differencing-amplifier reset on the first call (pixel_bandwidth.py:419-446)
+            for gi, (d, side) in enumerate(groups):
+                li, occ, spr, valid = self.render_log_intensity(d[side + "_ts"], ev.position, ev.channel_idx,
+                                                                interval_gen, reset_diff=(gi == 0))
+                d[side + "_log_intensity"], d[side + "_mean_ray_occ_rate"] = li, occ
+                d[side + "_mean_num_samples_per_ray"], d["is_" + side + "_valid"] = spr, valid
+        else:
+            # the four groups as ONE render of len(groups) x N rays
+            ts = torch.stack([d[side + "_ts"] for d, side in groups])
+            li, occ, spr, valid = self.render_log_intensity(ts, ev.position, ev.channel_idx)
+            for gi, (d, side) in enumerate(groups):
+                d[side + "_log_intensity"], d[side + "_mean_ray_occ_rate"] = li[gi], occ[gi]
+                d[side + "_mean_num_samples_per_ray"], d["is_" + side + "_valid"] = spr, valid[gi]
+        for d in (batch.diff, batch.subdiff):
+            if d is None:
+                continue
+            d.log_intensity_diff = d.end_log_intensity - d.start_log_intensity
+            d.is_valid = d.is_start_valid | d.is_end_valid
+            for k in ("start_ts", "end_ts", "start_log_intensity", "end_log_intensity"):
+                d.pop(k)
+        ev.pop("position")
+        if self.has_bayer_filter:
+            ev.pop("channel_idx")
+
+        batch.mean_num_samples_per_ray = self.update_train_batch_size(batch.diff, batch.subdiff, batch_index)
+        batch.mean_loss = self.loss.compute(ev, batch.diff, batch.subdiff,
+                                            self.contrast_threshold.mean_contrast_threshold)
+        batch.weighted_mean_loss = EasyDict({k: v * self.hparams.loss.weight[k] for k, v in batch.mean_loss.items()})
+        train_loss = sum(batch.weighted_mean_loss.values())
+
+        self.log("train/loss", train_loss, prog_bar=True)
+        for k, v in batch.mean_loss.items():
+            self.log(f"train/{k}", v)
+        for c in self.MULTI_PARAM_MODEL_COMPONENTS:
+            comp = getattr(self, c)
+            for name in comp.parametrizations.keys():
+                p = getattr(comp, name)
+                if p.requires_grad:
+                    self.log(f"train/{c}/{name}", p)
+        if not self.hparams.refractory_period.freeze:
+            self.log("train/refractory_period", self.refractory_period.refractory_period)
+        batch.mean_ray_occ_rate = self.derive_mean_value(
+            [(batch.diff, ["start_mean_ray_occ_rate", "end_mean_ray_occ_rate"]),
+             (batch.subdiff, ["start_mean_ray_occ_rate", "end_mean_ray_occ_rate"])])
+        batch.mean_valid_rate = self.derive_mean_value(
+            [(batch.diff, ["is_start_valid", "is_end_valid"]), (batch.subdiff, ["is_start_valid", "is_end_valid"])],
+            value_transform=lambda b: b.to(torch.get_default_dtype()).mean())
+        self.log("train/batch_size", batch.size)
+        self.log("train/mean_num_samples_per_ray", batch.mean_num_samples_per_ray)
+        self.log("train/mean_ray_occ_rate", batch.mean_ray_occ_rate)
+        self.log("train/mean_valid_rate", batch.mean_valid_rate)
+        return train_loss
+
+    # ------------------------------------------------------------------ rendering
+    def render_log_intensity(self, timestamp, pixel_position, pixel_channel_idx=None, normalized_interval_gen=None,
+                             reset_diff=False):
+        """deblur_e_nerf.py:1129-1160 -> (log intensity ([G,] N), mean ray occupancy rate, mean
+        samples per ray, is_valid ([G,] N)).  ``timestamp`` may carry a leading group dim G
+        (pixel bandwidth off) to render several supervision groups in one call."""
+        if self.hparams.pixel_bandwidth.enable:
+            fn = functools.partial(self.render_train_pixels, pixel_position=pixel_position,
+                                   pixel_channel_idx=pixel_channel_idx)
+            log_intensity, aux = self.pixel_bandwidth(normalized_interval_gen, timestamp, fn, reset_diff)
+            mean_ray_occ_rate, mean_num_samples_per_ray, is_valid = aux
+            is_valid = is_valid.any(dim=0)
+        else:
+            intensity, mean_ray_occ_rate, mean_num_samples_per_ray, is_valid = self.render_train_pixels(
+                timestamp, pixel_position, pixel_channel_idx)
+            log_intensity = intensity.log()
+        return log_intensity, mean_ray_occ_rate, mean_num_samples_per_ray, is_valid
+
+    def render_train_pixels(self, timestamp, pixel_position, pixel_channel_idx=None):
+        """deblur_e_nerf.py:1162-1183: poses at the timestamps ([G,] N), rays, render, bayering."""
+        T_wc_position, T_wc_orientation = self.trajectory(timestamp)
+        intensity, opacity, _, mean_num_samples_per_ray, is_valid = self.render_pixels(
+            self.train_intrinsics_inv, pixel_position, T_wc_position, T_wc_orientation)
+        if self.has_bayer_filter:
+            intensity = self.bayering(intensity, pixel_channel_idx)
+        occ = (opacity > 0).to(torch.get_default_dtype())
+        mean_ray_occ_rate = occ.mean() if timestamp.dim() == 1 else occ.reshape(occ.shape[0], -1).mean(dim=1)
+        return intensity, mean_ray_occ_rate, mean_num_samples_per_ray, is_valid
+
+    def render_pixels(self, intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation):
+        """deblur_e_nerf.py:1185-1221 -> intensity ([3,] [M,] N), opacity, depth, mean samples per
+        ray, is_valid."""
+        ray_origin, ray_direction = self.nerf.pixel_params_to_ray(intrinsics_inverse, pixel_position,
+                                                                   T_wc_position, T_wc_orientation)
+        intensity, opacity, depth, mean_num_samples_per_ray = self.nerf(ray_origin, ray_direction)
+        if intensity.dim() > opacity.dim():
+            intensity = intensity.permute(-1, *range(opacity.dim()))
+        intensity = intensity + self.hparams.min_modeled_intensity
+        if self.render_bkgd is None:
+            is_valid = opacity > 0
+        else:
+            is_valid = torch.ones_like(opacity, dtype=torch.bool)
+        depth = depth * torch.sum(ray_direction * T_wc_orientation[..., 2], dim=-1)
+        return intensity, opacity, depth, mean_num_samples_per_ray, is_valid
+
+    def bayering(self, intensity, channel_idx):
+        """deblur_e_nerf.py:1223-1235: (3, [S,] N) -> ([S,] N), the event's colour channel."""
+        idx = channel_idx.unsqueeze(dim=0)
+        if intensity.dim() == 3:
+            idx = idx.unsqueeze(dim=0).expand(-1, intensity.shape[1], -1)
+        return intensity.gather(dim=0, index=idx).squeeze(dim=0)
+
+    @staticmethod
+    def derive_mean_value(dict_keys_pairs, value_transform=lambda v: v):
+        pairs = [(d, [k for k in keys if k in d.keys()]) for d, keys in dict_keys_pairs if d is not None]
+        values = [value_transform(d[k]) for d, keys in pairs for k in keys]
+        return sum(values) / len(values)
+
+    def update_train_batch_size(self, batch_diff, batch_subdiff, batch_index):
+        """deblur_e_nerf.py:1252-1308: the mean samples per ray over the renders, averaged over
+        the ranks (all_gather), sets the next event batch size so that the samples per render
+        call stay ~ train_eff_ray_sample_batch_size / gpus (on the second-to-last micro-batch of
+        an accumulation group)."""
+        mspr = self.derive_mean_value([(batch_diff, ["start_mean_num_samples_per_ray", "end_mean_num_samples_per_ray"]),
+                                       (batch_subdiff, ["start_mean_num_samples_per_ray",
+                                                        "end_mean_num_samples_per_ray"])])
+        mspr = torch.mean(self.all_gather(torch.tensor(float(mspr))).float())
+        acc = self.trainer.accumulate_grad_batches
+        if acc > 1 and (batch_index % acc) != (acc - 2):
+            return mspr
+        new_size = int(self.train_ray_sample_batch_size / mspr)
+        self.train_batch_size = new_size
+        dm = getattr(self.trainer, "datamodule", None)
+        if dm is not None and hasattr(dm, "train_dataset"):
+            dm.train_dataset.batch_size = new_size
+            for s in dm.train_normalized_sampler.datasets:
+                s.size = new_size if isinstance(s.size, int) else (*s.size[:-1], new_size)
+        return mspr
+
+    # ------------------------------------------------------------------ optimisation
+    def configure_optimizers(self):
+        """deblur_e_nerf.py:1055-1112 with optim.Adam (den_adam_step) in place of torch.optim.Adam."""
+        refr = list(self.refractory_period.parameters())
+        mlp = [p for n, p in self.named_parameters() if n.startswith("nerf.radiance_field.mlp")]
+        groups = [{"params": refr,
+                   "lr": self.refractory_period.max_refractory_period.item()
+                   * self.hparams.optimizer.relative_lr.refractory_period},
+                  {"params": mlp, "weight_decay": self.hparams.loss.weight.nerf_mlp_weight_decay}]
+        for c in self.MULTI_PARAM_MODEL_COMPONENTS:
+            comp = getattr(self, c)
+            groups.extend({"params": [getattr(comp.parametrizations, n).original], "lr": lr}
+                          for n, lr in self.hparams.optimizer.lr[c].items())
+        collated = set(p for g in groups for p in g["params"])
+        other = [p for p in self.parameters() if p not in collated]
+        groups.append({"params": other})
+        if self.hparams.optimizer.algo != "adam":
+            raise NotImplementedError
+        optimizer = Adam(groups, lr=self.hparams.optimizer.lr.default)
+        if self.hparams.lr_scheduler.algo != "multi_step_lr":
+            raise NotImplementedError
+        sched = torch.optim.lr_scheduler.MultiStepLR(optimizer,
+                                                     milestones=self.hparams.lr_scheduler.multi_step_lr.milestones,
+                                                     gamma=self.hparams.lr_scheduler.multi_step_lr.gamma)
+        return {"optimizer": optimizer, "lr_scheduler": {"scheduler": sched,
+                                                         "interval": self.hparams.lr_scheduler.interval}}
+
+    def fit_step(self, batch, batch_index, optimizer):
+        """One optimisation step without a Trainer: training_step, backward, the DDP gradient
+        all-reduce (mean over ranks, one flat buffer), optimizer step on the last micro-batch of
+        an accumulation group (PL's accumulate_grad_batches semantics: gradients summed over the
+        group, each micro-batch loss scaled by 1 / accumulate_grad_batches)."""
+        acc = self.trainer.accumulate_grad_batches
+        loss = self.training_step(batch, batch_index)
+        (loss / acc).backward()
+        if (batch_index + 1) % acc == 0:
+            allreduce_gradients(self)
+            optimizer.step()
+            optimizer.zero_grad(set_to_none=True)
+            if not _HAS_PL:
+                self._global_step += 1
+        return loss
+
+    @torch.no_grad()
+    def render_image_eval(self, intrinsics_inverse, T_wc_position, T_wc_orientation, img_height, img_width):
+        """evaluation_step's render (deblur_e_nerf.py:602-652): the (H, W) image of one camera
+        pose -> intensity ([3,] H, W)."""
+        dev = self.train_intrinsics_inv.device
+        pix = torch.stack(torch.meshgrid(torch.arange(img_width), torch.arange(img_height), indexing="xy"),
+                          dim=2).to(torch.get_default_dtype()).to(dev)
+        pos = T_wc_position.reshape(1, 1, 3).expand(img_height, img_width, -1).to(dev)
+        rot = T_wc_orientation.reshape(1, 1, 3, 3).expand(img_height, img_width, -1, -1).to(dev)
+        was = self.training
+        self.eval()
+        try:
+            intensity, _, _, _, _ = self.render_pixels(intrinsics_inverse.to(dev), pix, pos, rot)
+        finally:
+            self.train(was)
+        return intensity
+
+
+def allreduce_gradients(module):
+    """DDP gradient semantics over the ranks of the default process group: the mean of each
+    gradient, as one all-reduce of one flat buffer (RCCL over xGMI on the GPU box)."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return
+    grads = [p.grad for p in module.parameters() if p.grad is not None]
+    if not grads:
+        return
+    flat = torch.cat([g.reshape(-1).to(torch.float64 if g.dtype == torch.float64 else torch.float32) for g in grads])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    flat.div_(dist.get_world_size())
+    off = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[off:off + n].view_as(g))
+        off += n

@@ -25,6 +25,9 @@ from .. import _native
 from ..utils import modules
 
 CAMERA_CALIBRATION_FILENAME = "camera_calibration.npz"
+# The reference asserts on device tensors inside forward (pixel_bandwidth.py:375, 440), which
+# forces two host syncs per call.  The kernels do not need the checks; set True to run them.
+CHECK_INPUTS = False
 
 
 def load_camera_calibration(root_directory):
@@ -113,8 +116,9 @@ class PixelBandwidth(torch.nn.Module):
     def forward(self, normalized_interval_gen, output_ts, intensity_sampling_fn, reset_diff=False):
         intensity_sample, sample_ts, auxiliary_output = self.sample_intensity(
             normalized_interval_gen, output_ts, intensity_sampling_fn)
-        # intensity_sample_to_weight (:375)
-        assert torch.all(sample_ts.diff(dim=0).to(torch.float32) > 0)
+        # intensity_sample_to_weight (:375) -- a host sync, so only when CHECK_INPUTS is set
+        if CHECK_INPUTS:
+            assert torch.all(sample_ts.diff(dim=0).to(torch.float32) > 0)
         params = self.params_vector()
         if reset_diff:
             out, delta = _native.PixelBandwidthFunction.apply(intensity_sample, params, None, sample_ts, output_ts,
@@ -124,7 +128,8 @@ class PixelBandwidth(torch.nn.Module):
         else:
             if self.reset_delta_log_it is None:
                 raise RuntimeError("PixelBandwidth: a reset_diff=True call must precede (pixel_bandwidth.py:436-440)")
-            assert torch.all((output_ts - self.reset_ts) >= 0)
+            if CHECK_INPUTS:  # pixel_bandwidth.py:440 (a host sync)
+                assert torch.all((output_ts - self.reset_ts) >= 0)
             out, _ = _native.PixelBandwidthFunction.apply(intensity_sample, params, self.reset_delta_log_it,
                                                           sample_ts, output_ts, self.reset_ts, False)
         return out, auxiliary_output

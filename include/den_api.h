@@ -33,8 +33,10 @@
  *                       and the timestamp derivation of
  *                       deblur_e_nerf/models/deblur_e_nerf.py:418-455 training_step
  *   den_pixel_rays   <- deblur_e_nerf/models/nerf.py:206-228 NeRF.pixel_params_to_ray
+ *   den_trajectory   <- deblur_e_nerf/models/trajectories.py:30-90 LinearTrajectory.forward
  *   den_event_loss_* <- deblur_e_nerf/loss_metric/loss.py:34-96 Loss.compute
  *   den_event_target
+ *   den_image_error  <- deblur_e_nerf/loss_metric/metric.py:28-92 (L1, PSNR)
  *   den_adam_step    <- torch.optim.Adam as configured by
  *                       deblur_e_nerf/models/deblur_e_nerf.py:1055-1112
  *   den_march_* / den_visibility / den_compact / den_pack_info / den_exclusive_scan
@@ -268,12 +270,30 @@ int den_event_step_bwd(int32_t N, int32_t rd, int32_t fn_d, int32_t fn_t, int32_
  * subdiff_start_ts samples; ct (2) f32 = C+, C- and refractory (1) f64 = tau_r ns are
  * the modules' post-parametrisation values (device scalars).  render_ts (4,N) f64 is
  * the [diff start, diff end, tv start, tv end] timestamp grid the renders consume.
- * ts_diff, ts_subdiff, target may be NULL.  Forward only: the synthetic
- * configuration freezes C+/C-/tau_r (configs/train/synthetic.yaml:29-40). */
+ * ts_diff, ts_subdiff, target may be NULL.  Its reverse mode is den_event_prep_bwd (C+/C-/tau_r
+ * are learnable in configs/train/07_*.yaml: ct_freeze / refr_freeze false). */
 int den_event_prep(int32_t N, int32_t has_diff, int32_t has_tv, const int64_t* num_pos, const int64_t* num_neg,
                    const int64_t* end_ts, const int64_t* start_ts, const double* norm, const float* ct,
                    const double* refractory, const float* norm_c, float* lid, double* start_out, double* render_ts,
                    double* ts_diff, double* ts_subdiff, float* target, void* stream);
+
+/* Reverse mode of den_event_prep (gradients of ContrastThreshold / RefractoryPeriod / the
+ * timestamp derivation / the loss target, with torch's lerp / maximum / minimum derivative
+ * conventions): upstream gradients g_lid (N) f32, g_start (N) f64, g_render_ts (4,N) f64,
+ * g_ts_diff, g_ts_subdiff (N) f64, g_target (N) f32 -- each may be NULL -- give
+ * d_params (4) f64 = [dL/dC+, dL/dC-, dL/dtau_r, dL/dnorm_c].  workspace:
+ * den_event_prep_workspace_bytes(N). */
+size_t den_event_prep_workspace_bytes(int32_t N);
+int den_event_prep_bwd(int32_t N, int32_t has_diff, int32_t has_tv, const int64_t* num_pos, const int64_t* num_neg,
+                       const int64_t* end_ts, const int64_t* start_ts, const double* norm, const float* ct,
+                       const double* refractory, const float* norm_c, const float* g_lid, const double* g_start,
+                       const double* g_render_ts, const double* g_ts_diff, const double* g_ts_subdiff,
+                       const float* g_target, void* workspace, double* d_params, void* stream);
+/* Reverse mode of den_event_target: d_ts_diff (N) f64, d_lid (N) f32, d_start (N) f64 (each may be
+ * NULL, overwritten) and d_c (1) f64 = dL/dnorm_c.  workspace: den_event_prep_workspace_bytes(N). */
+int den_event_target_bwd(int32_t N, const double* ts_diff, const float* lid, const int64_t* end_ts,
+                         const double* start_ts, const float* norm_c, const float* g_target, double* d_ts_diff,
+                         float* d_lid, double* d_start, void* workspace, double* d_c, void* stream);
 
 /* Rays of M render groups x N pixels (NeRF.pixel_params_to_ray):
  *   ray_d[m,n] = normalize(t_rot[m,n] @ (k_inv @ [pixel[n], 1])),  ray_o[m,n] = t_pos[m,n]
@@ -345,6 +365,23 @@ int den_occ_update(int64_t m, const int64_t* cell_indices, const uint8_t* mask, 
                    const float* step_sizes, float step_size, float ema_decay, float occ_thre, int64_t cells,
                    float* occs, uint8_t* sampled, uint8_t* binary, void* workspace, void* stream);
 
+/* Camera poses at n timestamps (LinearTrajectory.forward, models/trajectories.py:30-90):
+ * searchsorted over the C sorted pose stamps cam_ts (i64 ns), lerp of the positions (C,3) and
+ * shortest-path slerp of the XYZW orientations (C,4) (utils/tensor_ops.py:118-184), then
+ * quaternion -> row-major rotation matrix; query_ts (n) f64 ns -> position (n,3), rotation (n,3,3)
+ * f32.  status (optional, device i32): bit 0 is OR-ed in when a query lies outside
+ * [cam_ts[0], cam_ts[C-1]] (the reference asserts; the pose is clamped to the end bins). */
+int den_trajectory(int64_t n, int32_t C, const int64_t* cam_ts, const float* cam_pos, const float* cam_quat,
+                   const double* query_ts, float* position, float* rotation, int32_t* status, void* stream);
+
+/* Evaluation image errors (Metric.compute, loss_metric/metric.py:28-92): for n_img images of
+ * `pixels` f32 values each, sse_sae (n_img, 2) f64 = [sum (pred - target)^2, sum |pred - target|]
+ * (PSNR = 10 log10(range^2 / (sse / pixels)), L1 = sae / pixels).  workspace:
+ * den_image_error_workspace_bytes(n_img). */
+size_t den_image_error_workspace_bytes(int32_t n_img);
+int den_image_error(int32_t n_img, int64_t pixels, const float* pred, const float* target, void* workspace,
+                    double* sse_sae, void* stream);
+
 /* ---------------------------------------------------------------- reductions / optimizer */
 /* out[j] = sum_b partial[j*n_blocks + b] for j < n (deterministic order). */
 int den_sum_partials(int32_t n, int32_t n_blocks, const float* partial, float* out, void* stream);
@@ -354,6 +391,9 @@ int den_sum_partials(int32_t n, int32_t n_blocks, const float* partial, float* o
 int den_adam_step(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                   float lr, float beta1, float beta2, float eps, float weight_decay,
                   int64_t step, void* stream);
+/* The same for f64 parameters (the refractory period, event_generation_params.py:196-201). */
+int den_adam_step_f64(int64_t n, double* param, const double* grad, double* exp_avg, double* exp_avg_sq, double lr,
+                      double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -31,6 +31,7 @@ import torch
 
 f32 = np.float32
 FAR = f32(1e10)
+LAST = {}  # the random draws and samples of the latest ray_marching call (fixture generation)
 
 
 class ContractionType(enum.Enum):
@@ -218,6 +219,7 @@ def ray_marching(rays_o, rays_d, t_min=None, t_max=None, scene_aabb=None, grid=N
     R = o.shape[0]
     if stratified and jitter is None:
         jitter = torch.rand(R)
+    LAST["jitter"] = None if not stratified else torch.as_tensor(jitter).clone()
     jit = None if not stratified else np.asarray(jitter, f32)
     if t_min is None or t_max is None:
         ab = None if scene_aabb is None else scene_aabb.detach().float().cpu().numpy()
@@ -232,6 +234,7 @@ def ray_marching(rays_o, rays_d, t_min=None, t_max=None, scene_aabb=None, grid=N
     else:
         g, roi, res, ctype = None, None, None, 0
     ri, a0, a1, _ = march(o, d, tmin, tmax, g, roi, res, ctype, f32(render_step_size), cone_angle)
+    LAST.update(marched=(ri.copy(), a0.copy(), a1.copy()), t_min=tmin.copy(), t_max=tmax.copy())
     ray_indices = torch.from_numpy(ri)
     t_starts = torch.from_numpy(a0)[:, None]
     t_ends = torch.from_numpy(a1)[:, None]
@@ -246,6 +249,8 @@ def ray_marching(rays_o, rays_d, t_min=None, t_max=None, scene_aabb=None, grid=N
                 keep, _ = visibility(ri, a0, a1, alphas=alp, early_stop_eps=early_stop_eps, alpha_thre=alpha_thre)
         k = torch.from_numpy(keep)
         ray_indices, t_starts, t_ends = ray_indices[k], t_starts[k], t_ends[k]
+        LAST["prepass_sigma"] = sig if sigma_fn is not None else None
+    LAST["kept"] = (ray_indices.clone(), t_starts.clone(), t_ends.clone())
     return ray_indices, t_starts, t_ends
 
 

@@ -6,19 +6,28 @@ their outputs as golden fixtures.  Nothing in the product package imports this.
 
 The reference package root (``deblur_e_nerf/__init__.py``) imports
 pytorch_lightning, which is absent here, so sub-packages are registered as bare
-namespace modules whose ``__path__`` points into the reference tree.  The
-third-party modules that the hot-path files merely *import* but never call on
-this path (``easydict``, ``cv2``, ``roma``, ``nerfacc.ContractionType``) get
-minimal import-only stand-ins.  ``easydict.EasyDict`` is the one stand-in that is
-exercised (``loss.py`` builds result dicts with it): a dict with attribute access.
+namespace modules whose ``__path__`` points into the reference tree.  Third-party
+modules the reference imports get stand-ins:
+
+* ``easydict.EasyDict``: a dict with recursive attribute access (exercised);
+* ``nerfacc``: the CPU restatement of nerfacc 0.3.1 in ``oracle/nerfacc.py``
+  (ray_marching, OccupancyGrid, render_weight_from_density,
+  accumulate_along_rays, ContractionType) -- exercised by the render fixtures,
+  which therefore pin the reference's glue around nerfacc, not nerfacc itself;
+* ``roma``: the CPU restatement of RoMa 1.2.7 in ``oracle/roma.py`` (exercised by
+  the trajectory fixture);
+* ``pytorch_lightning``: ``LightningModule`` = ``torch.nn.Module`` (the
+  DeblurENeRF fixture binds the reference's methods to a plain module);
+* ``cv2``, ``pypose``, ``tqdm``, ``tinycudann``, ``lpips``, ``torchmetrics``:
+  import-only (never called on these paths).
 """
-import enum
 import importlib
 import os
 import sys
 import types
 
 REF_ROOT = "/root/reference"
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 class _EasyDict(dict):
@@ -49,30 +58,24 @@ def install():
         return
     if not os.path.isdir(REF_ROOT):
         raise RuntimeError("reference tree not present: golden generation only runs in the build container")
+    if REPO_ROOT not in sys.path:
+        sys.path.insert(0, REPO_ROOT)
+    from oracle import nerfacc as onerfacc
+    from oracle import roma as oroma
     ed = types.ModuleType("easydict")
     ed.EasyDict = _EasyDict
     sys.modules["easydict"] = ed
-    for name in ("cv2", "roma", "pypose", "tqdm"):
+    for name in ("cv2", "pypose", "tqdm", "tinycudann", "lpips", "torchmetrics"):
         sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["roma"] = oroma.as_module()
+    pl = types.ModuleType("pytorch_lightning")
+    import torch
+    pl.LightningModule = torch.nn.Module
+    sys.modules["pytorch_lightning"] = pl
     nf = types.ModuleType("nerfacc")
-
-    class ContractionType(enum.Enum):
-        AABB = 0
-        UN_BOUNDED_TANH = 1
-        UN_BOUNDED_SPHERE = 2
-
-    nf.ContractionType = ContractionType
-
-    def _absent(*a, **k):
-        raise RuntimeError("nerfacc is not available here (import-only stand-in)")
-
-    # external/utils.py and external/vol_rendering.py import these names at
-    # module level; the functions pinned by the fixtures never call them.
-    for fn in ("OccupancyGrid", "ray_marching", "render_weight_from_density", "render_weight_from_alpha",
-               "accumulate_along_rays",
-               "render_visibility", "unpack_info", "contract", "ContractionType"):
-        if not hasattr(nf, fn):
-            setattr(nf, fn, _absent)
+    for fn in ("ContractionType", "OccupancyGrid", "ray_marching", "render_weight_from_density",
+               "render_weight_from_alpha", "accumulate_along_rays"):
+        setattr(nf, fn, getattr(onerfacc, fn))
     sys.modules["nerfacc"] = nf
     pkg_root = os.path.join(REF_ROOT, "deblur_e_nerf")
     root = types.ModuleType("deblur_e_nerf")

@@ -45,6 +45,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 import _refload  # noqa: E402
 
 # tinycudann is imported (not used) by external/ngp.py, which holds trunc_exp.
@@ -378,6 +379,323 @@ def gen_rays():
          ray_origin_1=o1.numpy(), ray_direction_1=d1.numpy())
 
 
+# ----------------------------------------------------------------------------
+RENDER_CFG = dict(aabb=[-1.5, -1.5, -1.5, 1.5, 1.5, 1.5], near=1.43, far=6.63, res=24,
+                  step=float(np.sqrt(3) * 3.0 / 1024))  # synthetic.yaml nerf section, render_step_size "auto"
+ARCH = dict(net_depth=8, net_width=256, skip_layer=4, net_depth_condition=1, net_width_condition=128,
+            hidden_activation="softplus", density_activation="shifted_trunc_exp", radiance_activation="softplus",
+            pos_encoder_max_deg=10, view_encoder_max_deg=4, weight_norm=False)
+
+
+def _chair_rays(R, seed):
+    g = torch.Generator().manual_seed(seed)
+    v = torch.randn(R, 3, generator=g)
+    o = v / v.norm(dim=-1, keepdim=True) * 4.03
+    d = -o / o.norm(dim=-1, keepdim=True) + (torch.rand(R, 3, generator=g) * 2 - 1) * np.sin(0.3)
+    d = d / d.norm(dim=-1, keepdim=True)
+    return o.float(), d.float()
+
+
+def _grad_pick(nerf, n_pick=4096, seed=77):
+    """Gradient summary small enough for a fixture: every bias, three whole weight tensors and a
+    seeded subset of the flat MLP gradient (reference named_parameters() order)."""
+    out = {}
+    flat = []
+    for k, p in nerf.radiance_field.mlp.named_parameters():
+        gr = p.grad.detach().reshape(-1)
+        flat.append(gr)
+        if k.endswith("bias") or k in ("base.hidden_layers.0.weight", "sigma_layer.output_layer.weight",
+                                       "rgb_layer.output_layer.weight"):
+            out[f"grad:{k}"] = gr.numpy()
+    flat = torch.cat(flat)
+    idx = torch.randperm(flat.numel(), generator=torch.Generator().manual_seed(seed))[:n_pick].sort().values
+    out["grad_pick_idx"] = idx.numpy()
+    out["grad_pick"] = flat[idx].numpy()
+    out["grad_norm"] = np.array(float(flat.double().norm()))
+    return out
+
+
+def _ref_nerf(rd, seed, res):
+    """The reference NeRF (models/nerf.py) in the chair configuration with the nerfacc stand-in
+    (oracle/nerfacc.py); weights = PyTorch default Linear init under torch.manual_seed(seed)."""
+    nerfm = _refload.load("models.nerf")
+    ED = sys.modules["easydict"].EasyDict
+    CT = sys.modules["nerfacc"].ContractionType
+    c = RENDER_CFG
+    torch.manual_seed(seed)
+    occ = ED(resolution=res, occ_thre=0.01, ema_decay=0.95, warmup_steps=256, n=16)
+    return nerfm.NeRF(c["aabb"], CT.AABB, occ, c["near"], c["far"], c["step"], "parameter", 0.0, 1e-4, 0.0, 16384,
+                      "mlp", ED(ARCH), 3, rd)
+
+
+def gen_render(rd=1, seed=4, R=64, sigma_bias_shift=3.5):
+    """render.npz -- the reference's NeRF.forward (models/nerf.py:230-286) -> external/utils.py
+    render_image (the sigma_fn / rgb_sigma_fn closures, chunking) -> vol_rendering.rendering
+    (weights, three accumulations, background) in the chair configuration (synthetic.yaml), with
+    nerfacc's marching / scan / grid restated by oracle/nerfacc.py: the occupancy-grid update at
+    step 0, a training-mode forward (stratified; the jitter is recorded), its backward, and an
+    eval-mode forward."""
+    nerf = _ref_nerf(rd, seed, RENDER_CFG["res"])
+    from oracle import nerfacc as onerfacc
+    out = dict(seed=seed, rd=rd, res=RENDER_CFG["res"], step=RENDER_CFG["step"], aabb=np.array(RENDER_CFG["aabb"]),
+               near=RENDER_CFG["near"], far=RENDER_CFG["far"], sigma_bias_shift=sigma_bias_shift)
+    o, d = _chair_rays(R, 31)
+    out.update(rays_o=o.numpy(), rays_d=d.numpy())
+    nerf.train()
+    torch.manual_seed(100)
+    nerf.update_occ_grid(step=0, T_wc_position=o)
+    grid = nerf.occupancy_grid
+    out.update(occ_u=grid.last_u.numpy(), occs=grid.occs.numpy(), binary=grid.binary.numpy())
+    # the renders below use a denser field (rays saturate, so the early stop T < 1e-4 drops samples)
+    # and a structured grid (a ball of occupied cells with holes), so the DDA skip is exercised
+    with torch.no_grad():
+        nerf.radiance_field.mlp.sigma_layer.output_layer.bias.add_(sigma_bias_shift)
+    r = RENDER_CFG["res"]
+    c = (torch.stack(torch.meshgrid(*[torch.arange(r)] * 3, indexing="ij"), -1).float() + 0.5) / r - 0.5
+    ball = (c.norm(dim=-1) < 0.4) & ~((c[..., 0] > 0.1) & (c[..., 1].abs() < 0.1))
+    grid._binary = ball
+    out["binary_render"] = ball.numpy()
+    g = torch.Generator().manual_seed(41)
+    g_rad, g_op, g_dp = torch.randn(R, generator=g), torch.randn(R, generator=g), torch.randn(R, generator=g)
+    if rd > 1:
+        g_rad = torch.randn(R, rd, generator=g)
+    torch.manual_seed(101)
+    rad, op, dp, mspr = nerf(o, d)
+    LAST = onerfacc.LAST
+    out.update(train_jitter=LAST["jitter"].numpy(), train_marched_ri=LAST["marched"][0],
+               train_marched_t0=LAST["marched"][1], train_marched_t1=LAST["marched"][2],
+               train_t_min=LAST["t_min"], train_t_max=LAST["t_max"],
+               train_kept_ri=LAST["kept"][0].numpy(), train_kept_t0=LAST["kept"][1][:, 0].numpy(),
+               train_kept_t1=LAST["kept"][2][:, 0].numpy(), train_prepass_sigma=LAST["prepass_sigma"],
+               train_radiance=rad.detach().numpy(), train_opacity=op.detach().numpy(),
+               train_depth=dp.detach().numpy(), train_mspr=np.array(mspr),
+               g_rad=g_rad.numpy(), g_op=g_op.numpy(), g_dp=g_dp.numpy())
+    ((rad * g_rad).sum() + (op * g_op).sum() + (dp * g_dp).sum()).backward()
+    out.update(_grad_pick(nerf))
+    out["grad_bkgd_orig"] = nerf.parametrizations.render_bkgd.original.grad.numpy()
+    nerf.eval()
+    with torch.no_grad():
+        rad, op, dp, mspr = nerf(o, d)
+    out.update(eval_radiance=rad.numpy(), eval_opacity=op.numpy(), eval_depth=dp.numpy(), eval_mspr=np.array(mspr),
+               eval_kept_ri=LAST["kept"][0].numpy(), eval_kept_t0=LAST["kept"][1][:, 0].numpy())
+    # the reference's own rendering() on explicit packed samples (vol_rendering.py:16-128)
+    vr = _refload.load("external.vol_rendering")
+    n = 300
+    ri = torch.sort(torch.randint(0, 20, (n,), generator=g)).values.int()
+    ts = torch.rand(n, 1, generator=g) * 3 + 1.5
+    te = ts + torch.rand(n, 1, generator=g) * 0.05 + 1e-3
+    sig = (torch.rand(n, 1, generator=g) * 30).requires_grad_(True)
+    rgb = torch.rand(n, rd, generator=g).requires_grad_(True)
+    bk = torch.tensor([0.7] * rd, requires_grad=True)
+    col, opa, dep = vr.rendering(ts, te, ri, 24, rgb_sigma_fn=lambda a, b, c: (rgb, sig), render_bkgd=bk)
+    gc, go, gd = torch.randn(24, rd, generator=g), torch.randn(24, 1, generator=g), torch.randn(24, 1, generator=g)
+    ((col * gc).sum() + (opa * go).sum() + (dep * gd).sum()).backward()
+    out.update(vr_ri=ri.numpy(), vr_t0=ts.numpy(), vr_t1=te.numpy(), vr_sigma=sig.detach().numpy(),
+               vr_rgb=rgb.detach().numpy(), vr_bkgd=bk.detach().numpy(), vr_color=col.detach().numpy(),
+               vr_opacity=opa.detach().numpy(), vr_depth=dep.detach().numpy(), vr_gc=gc.numpy(), vr_go=go.numpy(),
+               vr_gd=gd.numpy(), vr_dsigma=sig.grad.numpy(), vr_drgb=rgb.grad.numpy(), vr_dbkgd=bk.grad.numpy())
+    save(f"render_rd{rd}.npz", **out)
+
+
+def gen_traj():
+    """traj.npz -- models/trajectories.py LinearTrajectory (searchsorted, lerp, the shortest-path
+    full-angle slerp of utils/tensor_ops.py:118-184, quaternion -> rotation matrix) with RoMa
+    1.2.7 restated by oracle/roma.py."""
+    trm = _refload.load("models.trajectories")
+    ED = sys.modules["easydict"].EasyDict
+    g = torch.Generator().manual_seed(51)
+    C = 40
+    ts = torch.cumsum(torch.randint(1_000_000, 5_000_000, (C,), generator=g), 0) + 100_000_000   # i64 ns
+    pos = torch.cumsum(torch.randn(C, 3, generator=g) * 0.05, 0) + torch.tensor([0.0, 0.0, 4.0])
+    q = torch.randn(C, 4, generator=g)
+    q = q / q.norm(dim=-1, keepdim=True)
+    # small steps between consecutive orientations, a few sign flips (shortest path) and a near-pi pair
+    for i in range(1, C):
+        q[i] = q[i - 1] + torch.randn(4, generator=g) * 0.05
+        q[i] = q[i] / q[i].norm()
+    q[7] = -q[7]
+    q[20] = -q[20]
+    q[30] = q[29] + torch.tensor([0.0, 0.0, 0.0, 1e-5])
+    q[30] = q[30] / q[30].norm()
+    cp = ED(camera_poses=ED(T_wc_position=pos, T_wc_orientation=q, T_wc_timestamp=ts))
+    traj = trm.LinearTrajectory(cp)
+    N = 600
+    qt = ts[0].double() + torch.rand(N, generator=g, dtype=torch.float64) * float(ts[-1] - ts[0])
+    qt[:4] = torch.tensor([float(ts[0]), float(ts[-1]), float(ts[5]), float(ts[5]) + 0.5], dtype=torch.float64)
+    p_out, r_out = traj(qt)
+    qt2 = qt[:480].reshape(16, 30)
+    p2, r2 = traj(qt2)
+    save("traj.npz", T_wc_position=pos.numpy(), T_wc_orientation=q.numpy(), T_wc_timestamp=ts.numpy(),
+         query_ts=qt.numpy(), position=p_out.numpy(), rotation=r_out.numpy(), query_ts_2d=qt2.numpy(),
+         position_2d=p2.numpy(), rotation_2d=r2.numpy())
+
+
+# ----------------------------------------------------------------------------
+def synthetic_dataset_arrays(rd=1, seed=61, C=64):
+    """camera_calibration.npz + camera_poses.npz contents of a chair-like synthetic sequence:
+    EDS-assumed sensor constants, contrast thresholds 0.25 / 0.2, refractory period 1 us, an
+    800 x 800 f = 1111 camera circling the AABB at radius 4.03 (looking at the origin) over
+    [0.05 s, 1.05 s]."""
+    from scipy.spatial.transform import Rotation
+    g = torch.Generator().manual_seed(seed)
+    K = np.array([[1111.0, 0.0, 400.0], [0.0, 1111.0, 400.0], [0.0, 0.0, 1.0]], dtype=np.float32)
+    cal = {k: np.array(v, dtype=np.float32) for k, v in EDS.items()}
+    cal.update(pos_contrast_threshold=np.array(0.25, np.float32), neg_contrast_threshold=np.array(0.2, np.float32),
+               refractory_period=np.array(1000, np.int64), intrinsics=K,
+               bayer_pattern=np.array("RGGB" if rd == 3 else ""), img_height=np.array(800), img_width=np.array(800))
+    ts = np.linspace(5e7, 1.05e9, C).astype(np.int64)
+    ang = np.linspace(0.0, 1.2, C) + float(torch.rand(1, generator=g)) * 6.28
+    pos = np.stack([4.03 * np.cos(ang), 4.03 * np.sin(ang), 0.6 + 0.2 * np.sin(3 * ang)], -1).astype(np.float32)
+    rots = []
+    for p in pos:
+        z = -p / np.linalg.norm(p)
+        x = np.cross(z, [0.0, 0.0, 1.0])
+        x /= np.linalg.norm(x)
+        y = np.cross(z, x)
+        rots.append(np.stack([x, y, z], -1))
+    quat = Rotation.from_matrix(np.stack(rots)).as_quat().astype(np.float32)  # XYZW
+    poses = dict(T_wc_position=pos, T_wc_orientation=quat, T_wc_timestamp=ts)
+    return cal, poses
+
+
+def write_dataset(d, cal, poses, max_refractory_period=1_000_000):
+    np.savez(os.path.join(d, "camera_calibration.npz"), **cal)
+    np.savez(os.path.join(d, "camera_poses.npz"), **poses)
+    torch.save(torch.tensor(max_refractory_period), os.path.join(d, "max_refractory_period.pt"))
+
+
+def synthetic_event_batch(N, S, seed, img=800, ts_lo=1.5e8, ts_hi=9.5e8):
+    """A reference-shaped training batch (datamodule.py:215-247): events (1, N, ...) and the
+    normalized samples (1, N) / (1, S - 1, N)."""
+    g = torch.Generator().manual_seed(seed)
+    num_pos = (torch.rand(N, generator=g) < 0.5).long()
+    end_ts = (torch.rand(N, generator=g, dtype=torch.float64) * (ts_hi - ts_lo) + ts_lo).long()
+    start_ts = end_ts - (-torch.log(torch.rand(N, generator=g, dtype=torch.float64)) * 2e6 + 2e4).long()
+    position = torch.rand(N, 2, generator=g) * (img - 1)
+    u = torch.rand(3, N, generator=g, dtype=torch.float64)
+    ev = dict(position=position[None], start_ts=start_ts[None], end_ts=end_ts[None], num_pos=num_pos[None],
+              num_neg=(1 - num_pos)[None])
+    nz = dict(ts_diff=torch.ones(1, N, dtype=torch.float64), diff_start_ts=u[0][None],
+              ts_subdiff=(1 - torch.sqrt(1 - u[1]))[None], subdiff_start_ts=u[2][None])
+    if S:
+        nz["interval_gen"] = torch.full((1, S - 1, N), 0.5, dtype=torch.float64)
+    return dict(event=ev, normalized=nz)
+
+
+def ref_deblur_step_module(d, rd, seed, pixbw, S, ct_free, refr_free, res=24):
+    """The reference DeblurENeRF's training-path methods bound to a module assembled from the
+    reference's own components (the constructor needs eval images and Lightning)."""
+    dm = _refload.load("models.deblur_e_nerf")
+    egp = _refload.load("models.event_generation_params")
+    pbm = _refload.load("models.pixel_bandwidth")
+    trm = _refload.load("models.trajectories")
+    lossm = _refload.load("loss_metric.loss")
+    ED = sys.modules["easydict"].EasyDict
+    datasets = _refload.load("data.datasets")
+    m = dm.DeblurENeRF.__new__(dm.DeblurENeRF)
+    torch.nn.Module.__init__(m)
+    m.hparams = ED(min_modeled_intensity=0.001,
+                   contrast_threshold=ED(parameterize_mean_ct=True, freeze=not ct_free),
+                   refractory_period=ED(freeze=not refr_free),
+                   pixel_bandwidth=ED(enable=pixbw, it_sample_size=S, f_c_dominant_min=21,
+                                      target_cumprob=ED(max_sample_lifetime=0.95)),
+                   loss=ED(weight=ED(log_intensity_diff=1.0, log_intensity_tv=1e-3, nerf_mlp_weight_decay=1e-6),
+                           error_fn=ED(log_intensity_diff="huber", log_intensity_tv="l1"),
+                           normalize=ED(log_intensity_diff=True, log_intensity_tv=True)))
+    cal = datasets.Event.load_camera_calibration(d)
+    m.has_bayer_filter = str(cal["bayer_pattern"]) != ""
+    m.register_buffer("train_intrinsics_inv", torch.linalg.inv(torch.from_numpy(cal["intrinsics"])), persistent=False)
+    m.render_bkgd = "parameter"
+    m.train_ray_sample_batch_size = 131072
+    m.MODEL_COMPONENTS = ["contrast_threshold", "refractory_period", "nerf"]
+    m.MULTI_PARAM_MODEL_COMPONENTS = ["contrast_threshold"]
+    m.contrast_threshold = egp.ContrastThreshold(d, True)
+    m.refractory_period = egp.RefractoryPeriod(d)
+    cp = datasets.CameraPose(d, None)
+    if pixbw:
+        m.pixel_bandwidth = pbm.PixelBandwidth(d, cp.camera_poses.T_wc_timestamp.min(), 21,
+                                               ED(max_sample_lifetime=0.95))
+        m.MODEL_COMPONENTS.append("pixel_bandwidth")
+        m.MULTI_PARAM_MODEL_COMPONENTS.append("pixel_bandwidth")
+        for p in m.pixel_bandwidth.parameters():
+            p.requires_grad_(False)
+    m.nerf = _ref_nerf(rd, seed, res)
+    m.trajectory = trm.LinearTrajectory(cp)
+    for c, free in (("contrast_threshold", ct_free), ("refractory_period", refr_free)):
+        for p in getattr(m, c).parameters():
+            p.requires_grad_(free)
+    m.loss = lossm.Loss(m.hparams.loss.weight, m.hparams.loss.error_fn, m.hparams.loss.normalize)
+    sampler = types.SimpleNamespace(size=1)
+    m.trainer = types.SimpleNamespace(accumulate_grad_batches=1, datamodule=types.SimpleNamespace(
+        train_dataset=types.SimpleNamespace(batch_size=1),
+        train_normalized_sampler=types.SimpleNamespace(datasets=[sampler])))
+    m.global_step = 0
+    m.log = lambda *a, **k: None
+    m.all_gather = lambda t: t[None]
+    return m
+
+
+def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None):
+    """step_*.npz -- the reference DeblurENeRF.training_step (deblur_e_nerf.py:396-586) run on a
+    reference-shaped batch: event correction, supervision timestamps, the occupancy-grid update,
+    render_log_intensity x 4 (trajectory, rays, NeRF.forward through render_image with the nerfacc
+    stand-in; the pixel-bandwidth model when on), update_train_batch_size, Loss.compute; then the
+    backward.  Contrast thresholds and refractory period learnable (07_ziggy_and_fuzz_hdr.yaml:172);
+    the dtau gradient is also recorded with the trajectory's interpolation weight detached
+    (``dtau_nopose``: the part that does not flow through the camera pose)."""
+    from oracle import nerfacc as onerfacc
+    cal, poses = synthetic_dataset_arrays(rd)
+    d = tempfile.mkdtemp(prefix="den_step_")
+    write_dataset(d, cal, poses)
+    batch = synthetic_event_batch(N, S if pixbw else 0, seed + 100)
+    out = dict(rd=rd, seed=seed, N=N, S=S, pixbw=pixbw, res=24, sigma_bias_shift=2.0,
+               **{f"cal:{k}": v for k, v in cal.items()}, **{f"pose:{k}": v for k, v in poses.items()},
+               **{f"event:{k}": v.numpy() for k, v in batch["event"].items()},
+               **{f"normalized:{k}": v.numpy() for k, v in batch["normalized"].items()})
+    for variant in ("full", "nopose"):
+        m = ref_deblur_step_module(d, rd, seed, pixbw, S, True, True)
+        with torch.no_grad():
+            m.nerf.radiance_field.mlp.sigma_layer.output_layer.bias.add_(2.0)
+        m.train()
+        if variant == "nopose":
+            orig_forward = type(m.trajectory).forward
+            m.trajectory.forward = lambda ts, f=orig_forward, t=m.trajectory: f(t, ts.detach())
+        jit = []
+        real = onerfacc.ray_marching
+
+        def rec(*a, **k):
+            r = real(*a, **k)
+            jit.append(onerfacc.LAST["jitter"].clone())
+            return r
+        dmod = sys.modules["deblur_e_nerf.external.utils"]
+        dmod.ray_marching = rec
+        torch.manual_seed(200)
+        b = {k: {kk: vv.clone() for kk, vv in v.items()} for k, v in batch.items()}
+        loss = m.training_step(b, 0)
+        loss.backward()
+        dmod.ray_marching = real
+        if variant == "full":
+            grid = m.nerf.occupancy_grid
+            out.update(occ_u=grid.last_u.numpy(), occs=grid.occs.numpy(), binary=grid.binary.numpy(),
+                       loss=loss.detach().numpy(), mspr=np.array(float(m.train_batch_size) if hasattr(
+                           m, "train_batch_size") else 0.0),
+                       new_batch_size=np.array(m.trainer.datamodule.train_dataset.batch_size),
+                       **{f"jitter_{i}": j.numpy() for i, j in enumerate(jit)}, **_grad_pick(m.nerf))
+            out["grad_bkgd_orig"] = m.nerf.parametrizations.render_bkgd.original.grad.numpy()
+            ctp = m.contrast_threshold.parametrizations
+            out["d_p2n_orig"] = ctp.p2n_contrast_threshold_ratio.original.grad.numpy()
+            out["d_mean_ct_orig"] = ctp.mean_contrast_threshold.original.grad.numpy()
+            out["dtau_orig"] = m.refractory_period.parametrizations._refractory_period.original.grad.numpy()
+        else:
+            out["dtau_orig_nopose"] = m.refractory_period.parametrizations._refractory_period.original.grad.numpy()
+            out["loss_nopose"] = loss.detach().numpy()
+    save(tag or f"step_{'pixbw' if pixbw else 'nopixbw'}_rd{rd}.npz", **out)
+
+
+def gen_step_pixbw():
+    gen_step(True, 1)
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.set_num_threads(8)
     for name in sys.argv[1:]:
@@ -394,3 +712,8 @@ elif __name__ == "__main__":
     gen_ct()
     gen_events()
     gen_rays()
+    gen_render(1, 4)
+    gen_render(3, 5)
+    gen_traj()
+    gen_step(False, 1)
+    gen_step(True, 1)

@@ -1,0 +1,209 @@
+"""Parity of the packed rendering path (nerfacc 0.3.1's marching / visibility / compositing /
+occupancy grid, restated in den_march.hip) and of the trajectory kernel against fixtures the
+REFERENCE's own code produced (tests/golden/make_golden.py: models/nerf.py NeRF.forward ->
+external/utils.py render_image -> external/vol_rendering.py rendering, with nerfacc's
+primitives restated by oracle/nerfacc.py; models/trajectories.py LinearTrajectory with RoMa
+restated by oracle/roma.py).  Needs an MI355X (marked gpu).
+
+Tolerances: marching samples bit-exact (the same sequential f32 arithmetic); compositing and
+renders in F32 mode 1e-4 relative (north_star), gradients 1e-4 / 1e-3 tensor-wise relative;
+trajectory positions 1e-6, rotations 2e-6 absolute (f32 transcendentals, ulp-level).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from _util import flat_from_params, norm_rel, rel_err
+from oracle import nerf as onerf
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _mods():
+    from deblur_e_nerf import _native
+    from deblur_e_nerf.external import marching
+    from deblur_e_nerf.models import nerf as nerf_lib
+    from deblur_e_nerf.utils.easydict import EasyDict
+    return _native, marching, nerf_lib, EasyDict
+
+
+ARCH = dict(net_depth=8, net_width=256, skip_layer=4, net_depth_condition=1, net_width_condition=128,
+            hidden_activation="softplus", density_activation="shifted_trunc_exp", radiance_activation="softplus",
+            pos_encoder_max_deg=10, view_encoder_max_deg=4, weight_norm=False)
+
+
+class _Draws:
+    """Replays the U[0,1) draws a reference run recorded, in call order (marching._uniform)."""
+
+    def __init__(self, arrays):
+        self.arrays = list(arrays)
+
+    def __call__(self, *size, device=None):
+        a = torch.as_tensor(self.arrays.pop(0)).float()
+        assert tuple(a.shape) == tuple(size), (a.shape, size)
+        return a.to(device)
+
+
+def build_nerf(z, mode="f32", sigma_shift=None):
+    """Our NeRF in the fixture's configuration, weights = the reference's seeded init."""
+    nat, marching, nerf_lib, ED = _mods()
+    rd = int(z["rd"])
+    occ = ED(resolution=int(z["res"]), occ_thre=0.01, ema_decay=0.95, warmup_steps=256, n=16)
+    aabb = [float(v) for v in z["aabb"]]
+    nerf = nerf_lib.NeRF(aabb, marching.ContractionType.AABB, occ, float(z["near"]), float(z["far"]),
+                         float(z["step"]), "parameter", 0.0, 1e-4, 0.0, 16384, "mlp", ED(ARCH), 3, rd, mode=mode)
+    p = onerf.build_params(rd, int(z["seed"]))
+    nerf.radiance_field.flat_params.copy_(flat_from_params(p, rd))
+    nerf = nerf.to(DEV)
+    if sigma_shift is not None:
+        with torch.no_grad():
+            nerf.radiance_field.mlp.sigma_layer.output_layer.bias.add_(sigma_shift)
+    return nerf
+
+
+def _grad_pick(nerf):
+    grads = [p.grad.detach().reshape(-1) for _, p in nerf.radiance_field.mlp.named_parameters()]
+    return torch.cat(grads).cpu()
+
+
+@pytest.mark.parametrize("rd", [1, 3])
+def test_occupancy_grid_update_matches_reference(golden_dir, rd, monkeypatch):
+    nat, marching, _, _ = _mods()
+    z = np.load(os.path.join(golden_dir, f"render_rd{rd}.npz"))
+    nerf = build_nerf(z)
+    nerf.train()
+    monkeypatch.setattr(marching, "_uniform", _Draws([z["occ_u"]]))
+    nerf.update_occ_grid(step=0, T_wc_position=torch.from_numpy(z["rays_o"]).to(DEV))
+    occs = nerf.occupancy_grid.occs.cpu()
+    e = rel_err(occs, z["occs"])
+    binary = nerf.occupancy_grid.binary.cpu().numpy()
+    flips = int((binary != z["binary"]).sum())
+    print(f"[rd={rd}] occs err {e:.2e}, binary flips {flips} of {binary.size}, occupied {binary.mean():.3f}")
+    assert e <= 1e-4
+    # a cell flips only if its occupancy sits at the mean threshold within the f32 noise
+    thr = min(float(z["occs"].mean()), 0.01)
+    near = np.abs(z["occs"].reshape(binary.shape) - thr) <= 1e-4 * thr
+    assert ((binary != z["binary"]) & ~near).sum() == 0
+
+
+@pytest.mark.parametrize("rd", [1, 3])
+def test_marching_matches_reference_samples(golden_dir, rd):
+    """den_march_prep/count/fill against the reference run's packed samples (before and after
+    the early-stop pre-pass is applied: the marched set is bit-exact)."""
+    nat, marching, _, _ = _mods()
+    z = np.load(os.path.join(golden_dir, f"render_rd{rd}.npz"))
+    import ctypes
+    o = torch.from_numpy(z["rays_o"]).to(DEV)
+    d = torch.from_numpy(z["rays_d"]).to(DEV)
+    R = o.shape[0]
+    L = nat.lib()
+    tmin = torch.empty(R, device=DEV)
+    tmax = torch.empty(R, device=DEV)
+    jit = torch.from_numpy(z["train_jitter"]).float().to(DEV)
+    ab = marching._carr(ctypes.c_float, [float(v) for v in z["aabb"]])
+    nat._check(L.den_march_prep(R, nat._ptr(o), nat._ptr(d), ab, float(z["near"]), float(z["far"]), nat._ptr(jit),
+                                float(z["step"]), nat._ptr(tmin), nat._ptr(tmax), nat._stream()))
+    assert torch.equal(tmin.cpu(), torch.from_numpy(z["train_t_min"]))
+    assert torch.equal(tmax.cpu(), torch.from_numpy(z["train_t_max"]))
+    grid = marching.OccupancyGrid([float(v) for v in z["aabb"]], int(z["res"])).to(DEV)
+    grid._binary.copy_(torch.from_numpy(z["binary_render"]))
+    roi, res, binary, ct = marching._grid_args(grid)
+    counts = torch.empty(R, dtype=torch.int32, device=DEV)
+    args = (R, nat._ptr(o), nat._ptr(d), nat._ptr(tmin), nat._ptr(tmax), roi, res, nat._ptr(binary), ct,
+            float(z["step"]), 0.0)
+    nat._check(L.den_march_count(*args, nat._ptr(counts), nat._stream()))
+    off, n = marching._scan(counts)
+    ri = torch.empty(n, dtype=torch.int32, device=DEV)
+    t0 = torch.empty(n, device=DEV)
+    t1 = torch.empty(n, device=DEV)
+    nat._check(L.den_march_fill(*args, nat._ptr(off), nat._ptr(ri), nat._ptr(t0), nat._ptr(t1), nat._stream()))
+    print(f"[rd={rd}] marched {n} samples (reference {len(z['train_marched_ri'])})")
+    assert n == len(z["train_marched_ri"])
+    assert np.array_equal(ri.cpu().numpy(), z["train_marched_ri"])
+    assert np.array_equal(t0.cpu().numpy(), z["train_marched_t0"])
+    assert np.array_equal(t1.cpu().numpy(), z["train_marched_t1"])
+
+
+@pytest.mark.parametrize("rd", [1, 3])
+def test_vol_rendering_matches_reference(golden_dir, rd):
+    """external/vol_rendering.rendering on explicit packed samples: colours / opacities / depths
+    and the gradients to sigma, rgb and the background."""
+    nat, marching, _, _ = _mods()
+    z = np.load(os.path.join(golden_dir, f"render_rd{rd}.npz"))
+    T = lambda k: torch.from_numpy(z[k]).to(DEV)  # noqa: E731
+    sig = T("vr_sigma").requires_grad_(True)
+    rgb = T("vr_rgb").requires_grad_(True)
+    bk = T("vr_bkgd").requires_grad_(True)
+    col, op, dp = marching.rendering(T("vr_t0"), T("vr_t1"), T("vr_ri"), 24, rgb_sigma_fn=lambda a, b, c: (rgb, sig),
+                                     render_bkgd=bk)
+    for a, k in ((col, "vr_color"), (op, "vr_opacity"), (dp, "vr_depth")):
+        e = rel_err(a, z[k])
+        assert e <= 1e-5, (k, e)
+    ((col * T("vr_gc")).sum() + (op * T("vr_go")).sum() + (dp * T("vr_gd")).sum()).backward()
+    for a, k in ((sig.grad, "vr_dsigma"), (rgb.grad, "vr_drgb"), (bk.grad, "vr_dbkgd")):
+        e = norm_rel(a, z[k])
+        print(f"[rd={rd}] {k} err {e:.2e}")
+        assert e <= 1e-5, (k, e)
+
+
+@pytest.mark.parametrize("rd", [1, 3])
+def test_nerf_forward_matches_reference(golden_dir, rd, monkeypatch):
+    """NeRF.forward (sampler 'occupancy', F32): the reference's training-mode render with the
+    recorded stratified jitter (samples after the early-stop pre-pass, radiance, opacity, depth,
+    mean samples per ray), its backward (MLP and background gradients), and the eval render."""
+    nat, marching, _, _ = _mods()
+    z = np.load(os.path.join(golden_dir, f"render_rd{rd}.npz"))
+    nerf = build_nerf(z, sigma_shift=float(z["sigma_bias_shift"]))
+    nerf.occupancy_grid._binary.copy_(torch.from_numpy(z["binary_render"]).to(DEV))
+    nerf.train()
+    o = torch.from_numpy(z["rays_o"]).to(DEV)
+    d = torch.from_numpy(z["rays_d"]).to(DEV)
+    monkeypatch.setattr(marching, "_uniform", _Draws([z["train_jitter"]]))
+    rad, op, dp, mspr = nerf(o, d)
+    print(f"[rd={rd}] mean samples/ray {mspr:.3f} (reference {float(z['train_mspr']):.3f})")
+    assert abs(mspr - float(z["train_mspr"])) <= 2.0 / o.shape[0]
+    for a, k in ((rad, "train_radiance"), (op, "train_opacity"), (dp, "train_depth")):
+        e = rel_err(a, z[k])
+        print(f"[rd={rd}] {k} err {e:.2e}")
+        assert e <= 1e-4, (k, e)
+    g = lambda k: torch.from_numpy(z[k]).to(DEV)  # noqa: E731
+    ((rad * g("g_rad")).sum() + (op * g("g_op")).sum() + (dp * g("g_dp")).sum()).backward()
+    flat = _grad_pick(nerf)
+    idx = torch.from_numpy(z["grad_pick_idx"])
+    e_pick = norm_rel(flat[idx], z["grad_pick"])
+    e_norm = abs(float(flat.double().norm()) - float(z["grad_norm"])) / float(z["grad_norm"])
+    e_bk = norm_rel(nerf.parametrizations.render_bkgd.original.grad, z["grad_bkgd_orig"])
+    print(f"[rd={rd}] grad pick err {e_pick:.2e}, norm err {e_norm:.2e}, bkgd err {e_bk:.2e}")
+    assert e_pick <= 1e-3 and e_norm <= 1e-4 and e_bk <= 1e-4
+    for k, p in nerf.radiance_field.mlp.named_parameters():
+        if f"grad:{k}" in z.files:
+            e = norm_rel(p.grad, z[f"grad:{k}"])
+            assert e <= 1e-3, (k, e)
+    nerf.eval()
+    with torch.no_grad():
+        rad, op, dp, mspr = nerf(o, d)
+    for a, k in ((rad, "eval_radiance"), (op, "eval_opacity"), (dp, "eval_depth")):
+        assert rel_err(a, z[k]) <= 1e-4, k
+    assert abs(mspr - float(z["eval_mspr"])) <= 2.0 / o.shape[0]
+
+
+def test_trajectory_matches_reference(golden_dir):
+    nat = _mods()[0]
+    z = np.load(os.path.join(golden_dir, "traj.npz"))
+    from deblur_e_nerf.data.datasets import CameraPose
+    from deblur_e_nerf.models.trajectories import LinearTrajectory
+    cp = CameraPose.from_arrays(z["T_wc_position"], z["T_wc_orientation"], z["T_wc_timestamp"])
+    traj = LinearTrajectory(cp).to(DEV)
+    for q, pk, rk in (("query_ts", "position", "rotation"), ("query_ts_2d", "position_2d", "rotation_2d")):
+        p, r = traj(torch.from_numpy(z[q]).to(DEV))
+        ep = float((p.cpu() - torch.from_numpy(z[pk])).abs().max())
+        er = float((r.cpu() - torch.from_numpy(z[rk])).abs().max())
+        print(f"trajectory {q}: position err {ep:.2e}, rotation err {er:.2e}")
+        assert p.shape == z[pk].shape and ep <= 1e-6 and er <= 2e-6
+    traj.check()
+    traj(torch.tensor([float(z["T_wc_timestamp"][-1]) + 1.0], dtype=torch.float64, device=DEV))
+    with pytest.raises(AssertionError):
+        traj.check()
