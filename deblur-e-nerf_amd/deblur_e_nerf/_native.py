@@ -108,7 +108,7 @@ _SIGS = {
     "den_occ_workspace_bytes": (ctypes.c_size_t, []),
     "den_occ_points": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int32]
                        + [ctypes.c_void_p] * 4),
-    "den_occ_update": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 5 + [ctypes.c_float] * 3
+    "den_occ_update": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_float] * 3
                        + [ctypes.c_int64] + [ctypes.c_void_p] * 5),
 }
 

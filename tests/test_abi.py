@@ -73,3 +73,21 @@ def test_no_cpu_fallback():
     nat, _ = _lib()
     with pytest.raises(nat.DenError):
         nat.adam_step(torch.zeros(4), torch.zeros(4), torch.zeros(4), torch.zeros(4), 1e-3, 0.9, 0.999, 1e-8, 0.0, 1)
+
+
+def _param_counts():
+    """{function: number of parameters} from the header's prototypes."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(den_\w+)\s*\(([^)]*)\)\s*;", src):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every ctypes binding passes exactly as many arguments as the C prototype declares."""
+    nat, _ = _lib()
+    counts = _param_counts()
+    bad = {n: (len(args), counts[n]) for n, (_, args) in nat._SIGS.items() if n in counts and len(args) != counts[n]}
+    assert not bad, bad

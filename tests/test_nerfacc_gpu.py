@@ -180,7 +180,7 @@ def test_nerf_forward_matches_reference(golden_dir, rd, monkeypatch):
     assert e_pick <= 1e-3 and e_norm <= 1e-4 and e_bk <= 1e-4
     for k, p in nerf.radiance_field.mlp.named_parameters():
         if f"grad:{k}" in z.files:
-            e = norm_rel(p.grad, z[f"grad:{k}"])
+            e = norm_rel(p.grad.reshape(-1), z[f"grad:{k}"])
             assert e <= 1e-3, (k, e)
     nerf.eval()
     with torch.no_grad():
