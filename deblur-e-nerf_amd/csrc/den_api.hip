@@ -15,6 +15,7 @@
 #include "den_dw.hip"
 #include "den_events.hip"
 #include "den_hidden.hip"
+#include "den_dwstream.hip"
 #include "den_march.hip"
 #include "den_misc.hip"
 #include "den_pixbw.hip"
@@ -72,6 +73,10 @@ struct TimedLaunch {
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+#ifndef DEN_DW_STREAM
+#define DEN_DW_STREAM 1  // BF16: operand-sharing streamed weight gradients (den_dwstream.hip)
+#endif
+
 struct WsLayout {
   size_t act[NACT];
   size_t rec, bkgd_partial, dw_partial, total;
@@ -113,8 +118,9 @@ WsLayout ws_layout(const den_render_desc* d) {
   L.splits = (int)splits;
   L.per_split = per;
   L.dw_partial = off;
-  // shared by the split-K GEMMs and the layer-major hidden backward (den_hidden.hip)
-  const size_t hidden = (size_t)hidden_grid(n) * 8 * 9 * 1024;
+  // shared by the split-K GEMMs, the layer-major hidden backward (den_hidden.hip) and the streamed
+  // weight gradients (den_dwstream.hip, at most 9 x 9 tiles per workgroup)
+  const size_t hidden = (size_t)hidden_grid(n) * 9 * 9 * 1024;
   if (d->train) off += align256(std::max((size_t)splits * DW_BLOCK_MAX, hidden) * 4);
   L.total = off;
   return L;
@@ -203,6 +209,60 @@ int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, 
   R.bias = bias;
   R.grad = grad;
   const int64_t per = (int64_t)MT * (R.NT + 1) * 1024;
+  {
+    DEN_TIMED(T_DW_REDUCE, s);
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
+  }
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+// One streamed weight-gradient launch (den_dwstream.hip) over the whole sample range.
+template <int MA, int MT, int NB, int NT, int NW, int DEPTH>
+int launch_dwstream(const den_render_desc* d, const WsLayout& L, char* ws, int a0, int a1, int b0, int b1,
+                    hipStream_t s) {
+  const int64_t n = (int64_t)d->n_rays * d->n_samples;
+  DwStreamArgs P{};
+  P.a[0] = ws + L.act[a0];
+  P.a_tiles[0] = act_width(DEN_MODE_BF16, a0) / 32;
+  P.a[1] = a1 >= 0 ? ws + L.act[a1] : nullptr;
+  P.a_tiles[1] = a1 >= 0 ? act_width(DEN_MODE_BF16, a1) / 32 : 0;
+  P.b[0] = ws + L.act[b0];
+  P.b_tiles[0] = act_width(DEN_MODE_BF16, b0) / 32;
+  P.b[1] = b1 >= 0 ? ws + L.act[b1] : nullptr;
+  P.b_tiles[1] = b1 >= 0 ? act_width(DEN_MODE_BF16, b1) / 32 : 0;
+  P.partial = (float*)(ws + L.dw_partial);
+  P.n_blocks = n / 32;
+  const int64_t grid = hidden_grid(n);
+  P.per_wg = (P.n_blocks + grid - 1) / grid;
+  {
+    DEN_TIMED(T_DW_GEMM, s);
+    hipLaunchKernelGGL((dwstream_kernel<MA, MT, NB, NT, NW, DEPTH>), dim3((unsigned)grid), dim3(64 * NW), 0, s, P);
+  }
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+// Reduction of row tiles [mt0, mt0 + MT) of a streamed partial with NT_ALL column tiles into layer
+// `layer`'s gradient (red_n1 / n1_feat / bias as in launch_dw).
+int launch_dwstream_reduce(const den_render_desc* d, const WsLayout& L, char* ws, int MT_ALL, int NT_ALL, int mt0,
+                           int MT, int layer, int red_n1, int n1_feat, int bias, float* grad, hipStream_t s) {
+  DwReduceArgs R{};
+  R.partial = (float*)(ws + L.dw_partial);
+  R.splits = (int)hidden_grid((int64_t)d->n_rays * d->n_samples);
+  R.MT = MT;
+  R.NT = NT_ALL;
+  R.m_off = 0;
+  R.layer = layer;
+  R.mode = DEN_MODE_BF16;
+  R.rd = d->radiance_dim;
+  R.n1 = red_n1;
+  R.n1_feat = n1_feat;
+  R.bias = bias;
+  R.grad = grad;
+  R.split_stride = (int64_t)MT_ALL * (NT_ALL + 1) * 1024;
+  R.first = (int64_t)mt0 * (NT_ALL + 1) * 1024;
+  const int64_t per = (int64_t)MT * (NT_ALL + 1) * 1024;
   {
     DEN_TIMED(T_DW_REDUCE, s);
     hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
@@ -302,6 +362,26 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
     }
   }
   if (!(parts & 2)) return DEN_OK;
+#if DEN_DW_STREAM
+  if (hidden) {
+    // streamed, operand-sharing weight gradients (den_dwstream.hip)
+    if ((rc = launch_dwstream<8, 16, 2, 2, 4, 3>(d, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<9, 9, 8, 8, 8, 3>(d, L, ws, D_ZB, -1, A_S0 + 7, -1, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream_reduce(d, L, ws, 9, 8, 0, 9, L_B, 256, 0, 1, G, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<4, 4, 8, 9, 4, 4>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream_reduce(d, L, ws, 4, 9, 0, 4, L_G, 256, WIDTH, 1, G, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<1, 1, 4, 4, 4, 6>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream_reduce(d, L, ws, 1, 4, 0, 1, L_R, 128, 0, 1, G, s)) != DEN_OK) return rc;
+    if (g->grad_bkgd) {
+      hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(256), 0, s, d->radiance_dim, d->n_rays,
+                         (const float*)(ws + L.bkgd_partial), g->grad_bkgd);
+      DEN_LAUNCHED();
+    }
+    return DEN_OK;
+  }
+#endif
   if ((rc = launch_dw<MODE, 8, 64, 0>(d, L, ws, 0, D_Z0 + 0, A_PE, -1, 0, G, s)) != DEN_OK) return rc;
   if (hidden) {
     // pe columns of L5 (the S4 columns and the bias come from the hidden launch of layer 5)

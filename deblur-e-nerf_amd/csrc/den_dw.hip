@@ -222,14 +222,17 @@ struct DwReduceArgs {
   int n1_feat;     // chain-feature offset of the second segment (e.g. 256 for [h4, pe])
   int bias;        // 0: skip the ones tile (the bias gradient is written by another launch)
   float* grad;     // flat params layout
+  int64_t split_stride;  // floats between consecutive splits' partials (0: MT * (NT + 1) * 1024)
+  int64_t first;         // float offset of this reduction's first tile inside a split's partial
 };
 
 __global__ void dw_reduce_kernel(DwReduceArgs R) {
   const int64_t per = (int64_t)R.MT * (R.NT + 1) * 1024;
+  const int64_t stride = R.split_stride > 0 ? R.split_stride : per;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= per) return;
   float s = 0.0f;
-  for (int sp = 0; sp < R.splits; ++sp) s += R.partial[sp * per + e];
+  for (int sp = 0; sp < R.splits; ++sp) s += R.partial[sp * stride + R.first + e];
   const int reg = (int)(e & 15), lane = (int)((e >> 4) & 63);
   const int64_t tile = e >> 10;
   const int nt = (int)(tile % (R.NT + 1)), mt = (int)(tile / (R.NT + 1));

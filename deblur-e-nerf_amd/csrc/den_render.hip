@@ -81,6 +81,12 @@ __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, 
 #ifndef DEN_FWD_RING
 #define DEN_FWD_RING 3
 #endif
+#ifndef DEN_FWD_STAGGER
+#define DEN_FWD_STAGGER 0
+#endif
+#ifndef DEN_FWD_SETPRIO
+#define DEN_FWD_SETPRIO 0
+#endif
 constexpr int FWD_RING = DEN_FWD_RING;
 static_assert(FWD_RING == 2 || FWD_RING == 3, "forward weight ring: 2 or 3 slots");
 
@@ -237,11 +243,28 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
       if (i >= 2) fwd_store<MODE, EPI>(A, sample, i - 2, xo, outA);
       Acc acc;
       const float* bias = (const float*)(lds + FWD_RING * LDS_BUF) + (CB + i) * TM + grp * T::REGS;
+#if DEN_FWD_STAGGER
+      // waves 4-7 (each SIMD's second wave) run the epilogue of tile i-1 BEFORE the MFMA chain of
+      // tile i, waves 0-3 after it: within a barrier interval the two waves of a SIMD then offer
+      // the matrix pipe and the VALU complementary work instead of the same work at once
+      const bool late = (threadIdx.x >> 6) >= 4;
+      if (late) {
+        if (i > 0) fwd_epilogue<MODE, L, EPI>(A, sample, prev, i - 1, xo, outA, special);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#endif
 #pragma unroll
       for (int r = 0; r < T::REGS; ++r) acc[r] = bias[r];
       mfma_chunk<MODE, KS1>(chunk, x1, acc);
       if constexpr (KS2 > 0) mfma_chunk<MODE, KS2>(chunk + KS1 * TM * T::KI * es_of(MODE), x2, acc);
+#if DEN_FWD_STAGGER
+      if (!late) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (i > 0) fwd_epilogue<MODE, L, EPI>(A, sample, prev, i - 1, xo, outA, special);
+      }
+#else
       if (i > 0) fwd_epilogue<MODE, L, EPI>(A, sample, prev, i - 1, xo, outA, special);
+#endif
       prev = acc;
     };
     int64_t noff;
@@ -280,6 +303,9 @@ __global__ __launch_bounds__(fwd_threads(MODE), 1024 / fwd_threads(MODE)) void r
   const int c = lane % TM, grp = lane / TM;
   const int64_t sample = (int64_t)blockIdx.x * WGS + wave * TM + c;
   const int64_t ray = sample / A.n_samples;
+#if DEN_FWD_SETPRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half: static priority
+#endif
   const int k = (int)(sample - ray * A.n_samples);
 
   // prologue: whole bias table -> LDS, chunk 0 -> slot 0 (and chunk 1 -> slot 1 with the 3-slot ring)
