@@ -89,13 +89,9 @@ constexpr int64_t DW_BLOCK_MAX = 9LL * 11 * 1024;  // floats per split, bound ov
 // persistent workgroups of the layer-major hidden backward: one per CU, at most one per wave block
 inline int64_t hidden_grid(int64_t n_samples) { return std::min<int64_t>(HB_GRID_MAX, std::max<int64_t>(1, n_samples / 32)); }
 
-// BF16 backward: layer-major hidden layers (den_hidden.hip) unless DEN_BWD=sample selects the
-// sample-major chain + split-K GEMMs of the F32 mode (A/B comparisons).
-inline bool use_hidden_path(int mode) {
-  if (mode != DEN_MODE_BF16) return false;
-  const char* e = std::getenv("DEN_BWD");
-  return !(e && std::strcmp(e, "sample") == 0);
-}
+// BF16 backward: layer-major hidden layers (den_hidden.hip) unless the descriptor selects the
+// sample-major chain + split-K GEMMs of the F32 mode (bwd_path = 1, A/B comparisons).
+inline bool use_hidden_path(const den_render_desc* d) { return d->mode == DEN_MODE_BF16 && d->bwd_path == 0; }
 
 WsLayout ws_layout(const den_render_desc* d) {
   WsLayout L{};
@@ -103,6 +99,13 @@ WsLayout ws_layout(const den_render_desc* d) {
   size_t off = 0;
   const int es = es_of(d->mode);
   for (int a = 0; a < NACT; ++a) {
+    // layer-major BF16 backward: dz_l (l = 0..6) is written in place over S_l, which the hidden
+    // launch of layer l + 1 reads for the last time in the same pass (per 32-sample block, into
+    // LDS before the block's dz_l leaves): 6.4 KB of workspace per sample instead of 10 KB
+    if (use_hidden_path(d) && a >= D_Z0 && a <= D_Z0 + 6) {
+      L.act[a] = L.act[A_S0 + (a - D_Z0)];
+      continue;
+    }
     L.act[a] = off;
     if (d->train) off += align256((size_t)n * act_width(d->mode, a) * es);
   }
@@ -319,8 +322,12 @@ int render_fwd_impl(const den_render_desc* d, const den_render_io* io, hipStream
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
   {
     DEN_TIMED(T_RENDER_FWD, s);
-    hipLaunchKernelGGL(render_fwd_kernel<MODE>, dim3((unsigned)(n / fwd_wg_samples(MODE))), dim3(fwd_threads(MODE)),
-                       0, s, A);
+    if (d->train)
+      hipLaunchKernelGGL((render_fwd_kernel<MODE, true>), dim3((unsigned)(n / fwd_wg_samples(MODE))),
+                         dim3(fwd_threads(MODE)), 0, s, A);
+    else
+      hipLaunchKernelGGL((render_fwd_kernel<MODE, false>), dim3((unsigned)(n / fwd_wg_samples(MODE))),
+                         dim3(fwd_threads(MODE)), 0, s, A);
   }
   DEN_LAUNCHED();
   return DEN_OK;
@@ -338,7 +345,7 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
   char* ws = (char*)io->workspace;
   float* G = g->grad_params;
-  const bool hidden = use_hidden_path(MODE);
+  const bool hidden = use_hidden_path(d);
   int rc;
   if (parts & 1) {
     if constexpr (MODE == DEN_MODE_BF16) {
@@ -415,6 +422,14 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
 extern "C" {
 
 int den_version(void) { return DEN_VERSION; }
+
+#ifdef DEN_FWD_PROF
+// experiment builds only: per-wave cycle split of the last render_fwd launch (512 WGs x 8 waves x 4)
+int den_debug_fwd_prof(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(den_fwd_prof), sizeof(uint64_t) * 512 * 8 * 4) == hipSuccess ? DEN_OK
+                                                                                                        : DEN_EHIP;
+}
+#endif
 
 int32_t den_render_tile_samples(int32_t mode) {
   return (mode == 0 || mode == 1) ? std::max(wg_samples(mode), fwd_wg_samples(mode)) : -1;

@@ -44,12 +44,20 @@ template <> struct Tr<0> {
 template <int MODE>
 __device__ __forceinline__ void acc_to_frags(const typename Tr<MODE>::Acc& a, typename Tr<MODE>::Frag* f) {
   if constexpr (MODE == 1) {
+    // one v_cvt_pk_bf16_f32 per register pair (element-wise casts let the compiler pair them
+    // across the SLP-packed adds of the epilogue, at the cost of v_alignbit / v_perm fix-ups)
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 v;
+      uint32_t w[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)a[8 * s + j];
-      f[s] = v;
+      for (int q = 0; q < 4; ++q) {
+        const f32x2 p = {a[8 * s + 2 * q], a[8 * s + 2 * q + 1]};
+        w[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector(p, bf16x2));
+      }
+      const uint4 u = make_uint4(w[0], w[1], w[2], w[3]);
+      f[s] = __builtin_bit_cast(bf16x8, u);
     }
   } else {
 #pragma unroll

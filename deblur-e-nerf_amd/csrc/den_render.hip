@@ -73,40 +73,45 @@ __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, 
   __syncthreads();
 }
 
-// ---- forward weight ring: FWD_RING slots, chunk t+2 in flight while chunk t is computed.
-// The LDS-DMA is issued through inline asm, so the compiler does not track it (tracked, it makes
-// the first LDS read of every chunk wait vmcnt(0) -- i.e. for the deeper prefetch and for the
-// activation stores too); each step instead waits explicitly for chunk t+1 only:
-// vmcnt(<DMA ops of chunk t+2> + <stores of this step>), both issued after chunk t+1's DMA.
+// ---- forward weight ring: FWD_RING slots, chunks t+1 .. t+FWD_RING-1 in flight while chunk t is
+// computed.  The LDS-DMA is issued through inline asm, so the compiler does not track it (tracked,
+// it makes the first LDS read of every chunk wait vmcnt(0) -- i.e. for the deeper prefetch and for
+// the activation stores too).  Each step instead waits for chunk t+1 only, by count: vmcnt is
+// in-order, so "chunk t+1 landed" = at most <vector-memory ops issued after its DMA> outstanding
+// (FwdVm keeps that count).  The activation stores of a step then have FWD_RING - 2 further chunk
+// intervals to drain before a wait covers them: with the whole chip writing 5 KB per sample, an HBM
+// store outlives one interval, and a 3-slot ring made every barrier wait for the previous step's
+// stores.
 #ifndef DEN_FWD_RING
-#define DEN_FWD_RING 3
-#endif
-#ifndef DEN_FWD_STAGGER
-#define DEN_FWD_STAGGER 0
+#define DEN_FWD_RING 4
 #endif
 #ifndef DEN_FWD_SETPRIO
 #define DEN_FWD_SETPRIO 0
 #endif
 constexpr int FWD_RING = DEN_FWD_RING;
-static_assert(FWD_RING == 2 || FWD_RING == 3, "forward weight ring: 2 or 3 slots");
+static_assert(FWD_RING == 3 || FWD_RING == 4, "forward weight ring: 3 or 4 slots");
 
-// BF16 forward workgroup: DEN_FWD_WAVES_BF16 waves (32 samples each) share one weight stream.
-// Every workgroup streams the whole packed MLP (1.2 MB) through LDS, so samples per workgroup set
-// the L2 -> LDS weight traffic (78 GB per 2^24-sample step at 256 per workgroup).  Measured: 16
-// waves (half the weight traffic) take 38.4 ms against 28.0 ms for 8 waves: the 8-wave kernel holds
-// 202 VGPRs per wave (one workgroup per CU), and 16 waves per workgroup cap a wave at 128.
-#ifndef DEN_FWD_WAVES_BF16
-#define DEN_FWD_WAVES_BF16 8
+// Forward workgroup: 8 column blocks of TM samples (BF16: 256 samples) share one weight stream --
+// every workgroup streams the whole packed MLP (1.2 MB) through LDS, so samples per workgroup set
+// the L2 -> LDS weight traffic (78 GB per 2^24-sample step at 256 per workgroup).  NB column
+// blocks per wave, 8 / NB waves: NB = 2 (BF16 only; 4 waves, one per SIMD with 512 registers) feeds
+// each LDS weight fragment to two MFMAs, but measured slower than 8 waves x 1 block (the compiler
+// then serialises LDS reads and MFMAs within the single wave and moves accumulators through AGPRs;
+// profiles/fwd_prof.py cycle split).
+#ifndef DEN_FWD_NB
+#define DEN_FWD_NB 1  // r02 A/B: NB = 2 (4 waves x 64 samples) 27.7 ms vs 24.9 ms for NB = 1
 #endif
-DEN_HD constexpr int fwd_waves(int mode) { return mode == 1 ? DEN_FWD_WAVES_BF16 : 8; }
+static_assert(DEN_FWD_NB == 1 || DEN_FWD_NB == 2, "BF16 forward: 1 or 2 column blocks per wave");
+DEN_HD constexpr int fwd_nb(int mode) { return mode == 1 ? DEN_FWD_NB : 1; }
+DEN_HD constexpr int fwd_waves(int mode) { return 8 / fwd_nb(mode); }
 DEN_HD constexpr int fwd_threads(int mode) { return 64 * fwd_waves(mode); }
-DEN_HD constexpr int fwd_wg_samples(int mode) { return fwd_waves(mode) * tm_of(mode); }
-static_assert(FWD_RING == 3 || DEN_FWD_WAVES_BF16 == 8, "the 2-slot ring's tracked DMA assumes 512 threads");
+DEN_HD constexpr int fwd_wg_samples(int mode) { return 8 * tm_of(mode); }
+DEN_HD constexpr int fwd_min_waves(int mode) { return fwd_waves(mode) / 4; }  // waves per SIMD
 
 // per-wave count of DMA instructions dma_chunk_untracked<NTH> issues for `bytes` (wave-uniform)
 template <int NTH>
 __device__ __forceinline__ int dma_ops(int bytes) {
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int n = 0;
 #pragma unroll
   for (int q = 0; q < (CHUNK_MAX + NTH * 16 - 1) / (NTH * 16); ++q) n += (q * NTH * 16 + wave * 1024 < bytes) ? 1 : 0;
@@ -135,7 +140,8 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
   static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
   __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | ((VM >> 4) << 14));
 }
-__device__ __forceinline__ void wait_vm_lgkm0_rt(int n) {  // n wave-uniform, 0..7
+// n wave-uniform; counts above 15 wait for 15 (stricter than needed, never looser)
+__device__ __forceinline__ void wait_vm_lgkm0_rt(int n) {
   switch (n) {
     case 0: wait_vm_lgkm0<0>(); break;
     case 1: wait_vm_lgkm0<1>(); break;
@@ -144,40 +150,80 @@ __device__ __forceinline__ void wait_vm_lgkm0_rt(int n) {  // n wave-uniform, 0.
     case 4: wait_vm_lgkm0<4>(); break;
     case 5: wait_vm_lgkm0<5>(); break;
     case 6: wait_vm_lgkm0<6>(); break;
-    default: wait_vm_lgkm0<7>(); break;
+    case 7: wait_vm_lgkm0<7>(); break;
+    case 8: wait_vm_lgkm0<8>(); break;
+    case 9: wait_vm_lgkm0<9>(); break;
+    case 10: wait_vm_lgkm0<10>(); break;
+    case 11: wait_vm_lgkm0<11>(); break;
+    case 12: wait_vm_lgkm0<12>(); break;
+    case 13: wait_vm_lgkm0<13>(); break;
+    case 14: wait_vm_lgkm0<14>(); break;
+    default: wait_vm_lgkm0<15>(); break;
   }
 }
 
-// One forward step: issue chunk t+2 into the slot chunk t-1 used (free since the last barrier),
-// run `body` on chunk t (it issues n_st stores), wait for chunk t+1, barrier.
+// Vector-memory ops this wave issued (DMA pieces + global stores), and the count right after the
+// DMA of each chunk in the ring.  A store must be counted here or not at all: an uncounted op only
+// makes a wait stricter, an over-count would let the barrier pass before a chunk landed.
+struct FwdVm {
+  int issued;
+  int mark[FWD_RING];
+#ifdef DEN_FWD_PROF
+  uint64_t prof[4];  // experiment builds only: cycles in body / vmcnt wait / barrier / whole kernel
+#endif
+};
+#ifdef DEN_FWD_PROF
+__device__ uint64_t den_fwd_prof[512 * 8 * 4];
+#endif
+
+// One forward step: issue chunk t+FWD_RING-1 into the slot chunk t-1 used (free since the last
+// barrier), run `body` on chunk t (it issues n_st stores), wait for chunk t+1, barrier.
 template <int NTH, typename Body>
-__device__ __forceinline__ void chunk_step3(char* lds, const char* wbase, int t, int64_t off2, int bytes2, int n_st,
-                                            Body&& body) {
-  if (bytes2 > 0) dma_chunk_untracked<NTH>(wbase + off2, lds + ((t + 2) % 3) * LDS_BUF, bytes2);
-  body(lds + (t % 3) * LDS_BUF);
-  wait_vm_lgkm0_rt(dma_ops<NTH>(bytes2) + n_st);
+__device__ __forceinline__ void fwd_step(char* lds, const char* wbase, int t, int64_t off_n, int bytes_n, int n_st,
+                                         FwdVm& vm, Body&& body) {
+  constexpr int R = FWD_RING;
+#ifdef DEN_FWD_PROF
+  const uint64_t p0 = __builtin_amdgcn_s_memtime();
+#endif
+  if (bytes_n > 0) {
+    dma_chunk_untracked<NTH>(wbase + off_n, lds + ((t + R - 1) % R) * LDS_BUF, bytes_n);
+    // the DMA ops EVERY wave issues (some issue one more): an under-count, so the count stays a
+    // compile-time constant and each wait an immediate
+    vm.issued += bytes_n / (NTH * 16);
+  }
+  vm.mark[(t + R - 1) % R] = vm.issued;
+  body(lds + (t % R) * LDS_BUF);
+#ifdef DEN_FWD_PROF
+  const uint64_t p1 = __builtin_amdgcn_s_memtime();
+#endif
+  vm.issued += n_st;
+  wait_vm_lgkm0_rt(vm.issued - vm.mark[(t + 1) % R]);
+#ifdef DEN_FWD_PROF
+  const uint64_t p2 = __builtin_amdgcn_s_memtime();
+#endif
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+#ifdef DEN_FWD_PROF
+  const uint64_t p3 = __builtin_amdgcn_s_memtime();
+  vm.prof[0] += p1 - p0;
+  vm.prof[1] += p2 - p1;
+  vm.prof[2] += p3 - p2;
+#endif
 }
 
-// chunk geometry helpers (forward / backward)
+// geometry of the forward chunk k after tile i of layer l (bytes 0 past the last one)
 template <int MODE>
-__device__ __forceinline__ void fwd_next(int l, int i, int64_t* off, int* bytes) {
-  int nl = l, ni = i + 1;
-  if (ni >= fwd_tiles(MODE, l)) { nl = l + 1; ni = 0; }
-  if (nl >= NL) { *off = 0; *bytes = 0; return; }
-  *bytes = chunk_bytes_K(fwd_K(MODE, nl));
-  *off = fwd_layer_offset(MODE, nl) + (int64_t)ni * *bytes;
+__device__ __forceinline__ void fwd_ahead(int l, int i, int k, int64_t* off, int* bytes) {
+#pragma unroll
+  for (int s = 0; s < k; ++s) {
+    if (++i >= fwd_tiles(MODE, l)) { ++l; i = 0; }
+  }
+  if (l >= NL) { *off = 0; *bytes = 0; return; }
+  *bytes = chunk_bytes_K(fwd_K(MODE, l));
+  *off = fwd_layer_offset(MODE, l) + (int64_t)i * *bytes;
 }
-// geometry of the chunk two after (l, i)
-template <int MODE>
-__device__ __forceinline__ void fwd_next2(int l, int i, int64_t* off, int* bytes) {
-  int nl = l, ni = i + 1;
-  if (ni >= fwd_tiles(MODE, l)) { nl = l + 1; ni = 0; }
-  if (nl >= NL) { *off = 0; *bytes = 0; return; }
-  fwd_next<MODE>(nl, ni, off, bytes);
-}
+
 template <int MODE, int LAST_J>
 __device__ __forceinline__ void bwd_next(int j, int i, int64_t* off, int* bytes) {
   int nj = j, ni = i + 1;
@@ -188,110 +234,190 @@ __device__ __forceinline__ void bwd_next(int j, int i, int64_t* off, int* bytes)
 }
 
 // ------------------------------------------------------------------ forward layer
+// A wave carries NB = fwd_nb(MODE) column blocks of TM samples: every weight fragment read from
+// LDS feeds NB independent MFMAs (BF16: two 32-sample blocks, so a workgroup of 4 waves -- one per
+// SIMD, up to 512 registers each -- shares one weight stream over 256 samples).
+// Fragment arrays are block-major: block b's k-th fragment of an input of stride S is x[b * S + k].
 // Runs all row tiles of forward layer L with input fragments x1[0..KS1) ++ x2[0..KS2).
 // EPI: 0 = hidden softplus(100) -> xo (+store act outA), 1 = bottleneck/sigma, 2 = rgb.
-// Software pipeline: the VALU epilogue of tile i-1 is issued in the same
-// basic block as the MFMA chain of tile i, so the two interleave.
-template <int MODE, int L, int EPI, typename Frag, typename Acc>
-__device__ __forceinline__ void fwd_epilogue(const RenderArgs<MODE>& A, int64_t sample, Acc& acc, int i, Frag* xo,
-                                             int outA, Acc* special) {
+// The VALU epilogue of tile i-1 is issued in the same basic block as the MFMA chain of tile i
+// (TRAIN is a template parameter: no branch splits it), so the two interleave.
+struct FwdOut {
+  float sigma_raw;   // sigma layer output (lane group 0)
+  float rgb_raw[3];  // rgb layer outputs 0..rd-1 (lane group 0)
+};
+
+template <int MODE, int L, int EPI, int NB, typename Frag, typename Acc>
+__device__ __forceinline__ void fwd_epilogue(Acc* acc, int i, Frag* xo, FwdOut* out) {
   using T = Tr<MODE>;
-  constexpr int TM = T::TM, FPT = T::FPT;
-  if constexpr (EPI == 0) {
+  constexpr int TM = T::TM, FPT = T::FPT, KS = WIDTH / T::KI;
 #pragma unroll
-    for (int r = 0; r < T::REGS; ++r) acc[r] = hidden_act<MODE>(acc[r]);
-    acc_to_frags<MODE>(acc, xo + i * FPT);
-  } else if constexpr (EPI == 1) {
-    if (i < WIDTH / TM) {
-      acc_to_frags<MODE>(acc, xo + i * FPT);
-    } else if (i == WIDTH / TM) {
-      *special = acc;  // row 0 = sigma_raw (lane group 0, reg 0)
+  for (int b = 0; b < NB; ++b) {
+    if constexpr (EPI == 0) {
+#pragma unroll
+      for (int r = 0; r < T::REGS; ++r) acc[b][r] = hidden_act<MODE>(acc[b][r]);
+      acc_to_frags<MODE>(acc[b], xo + b * KS + i * FPT);
+    } else if constexpr (EPI == 1) {
+      if (i < WIDTH / TM) {
+        acc_to_frags<MODE>(acc[b], xo + b * KS + i * FPT);
+      } else if (i == WIDTH / TM) {
+        out[b].sigma_raw = acc[b][0];  // row 256 = sigma_raw (lane group 0, reg 0)
+      }
+    } else {
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) out[b].rgb_raw[ch] = acc[b][ch];  // rows 0..rd-1 (lane group 0)
+    }
+  }
+}
+
+// HBM store of forward tile i (train mode), issued in the chunk interval after the one that
+// computed it, so that the barrier closing an interval does not wait for it.
+template <int MODE, bool TRAIN, int EPI, int NB, typename Frag>
+__device__ __forceinline__ void fwd_store(const RenderArgs<MODE>& A, const int64_t* sample, int i, const Frag* xo,
+                                          int outA) {
+  constexpr int TM = Tr<MODE>::TM, FPT = Tr<MODE>::FPT, KS = WIDTH / Tr<MODE>::KI;
+  if constexpr (!TRAIN) return;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if constexpr (EPI == 0) {
+      store_tile_frags<MODE>(act_ptr(A, outA, sample[b], i), xo + b * KS + i * FPT);
+    } else if constexpr (EPI == 1) {
+      if (i < WIDTH / TM) store_tile_frags<MODE>(act_ptr(A, A_BT, sample[b], i), xo + b * KS + i * FPT);
+    }
+  }
+}
+
+// global store instructions fwd_store issues for tile i (store_tile_frags: 2 in BF16, 1 in F32)
+template <int MODE, bool TRAIN, int EPI, int NB>
+__device__ __forceinline__ constexpr int fwd_store_ops(int i) {
+  if (!TRAIN) return 0;
+  const int per = NB * (MODE == 1 ? 2 : 1);
+  if (EPI == 0) return per;
+  if (EPI == 1) return i < WIDTH / tm_of(MODE) ? per : 0;
+  return 0;
+}
+
+// acc[b] += W_chunk x[b * S + 0 .. KS), b < NB: one LDS read of each weight fragment per NB MFMAs.
+// BF16: the weight fragments are read FWD_PF k-steps ahead into a register ring (left alone, the
+// compiler issues each read right before its MFMAs and waits out the LDS latency every k-step).
+#ifndef DEN_FWD_PF
+#define DEN_FWD_PF 4
+#endif
+#ifndef DEN_FWD_SCHED
+#define DEN_FWD_SCHED 0  // r02 A/B: pinned schedule 25.8 ms vs 24.9 ms for the compiler's order (NB = 1)
+#endif
+template <int MODE, int KS, int NB, int S>
+__device__ __forceinline__ void mfma_chunk_nb(const char* lds_chunk, const typename Tr<MODE>::Frag* x,
+                                              typename Tr<MODE>::Acc* acc) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (MODE == 1) {
+    constexpr int PF = DEN_FWD_PF < KS ? DEN_FWD_PF : KS;
+    bf16x8 a[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) a[p] = *(const bf16x8*)(lds_chunk + p * 1024 + lane * 16);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const bf16x8 cur = a[k % PF];
+      if (k + PF < KS) a[k % PF] = *(const bf16x8*)(lds_chunk + (k + PF) * 1024 + lane * 16);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) acc[b] = Tr<1>::mfma(cur, x[b * S + k], acc[b]);
     }
   } else {
-    *special = acc;  // rows 0..rd-1 = rgb_raw (lane group 0, regs 0..rd-1)
+    static_assert(KS % 4 == 0, "f32 k-steps come in groups of 4");
+#pragma unroll
+    for (int k4 = 0; k4 < KS / 4; ++k4) {
+      const f32x4 a = *(const f32x4*)(lds_chunk + k4 * 1024 + lane * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[b] = Tr<0>::mfma(a[q], x[b * S + 4 * k4 + q], acc[b]);
+    }
   }
 }
 
-// HBM store of forward tile i (train mode), issued at the START of the chunk interval after
-// the one that computed it: the barrier closing an interval drains vmcnt(0) (it must wait for
-// the weight DMA), so a store issued there has a whole interval to complete instead of
-// stalling that barrier.
-template <int MODE, int EPI, typename Frag>
-__device__ __forceinline__ void fwd_store(const RenderArgs<MODE>& A, int64_t sample, int i, const Frag* xo,
-                                          int outA) {
-  constexpr int TM = Tr<MODE>::TM, FPT = Tr<MODE>::FPT;
-  if (!A.train) return;
-  if constexpr (EPI == 0) {
-    store_tile_frags<MODE>(act_ptr(A, outA, sample, i), xo + i * FPT);
-  } else if constexpr (EPI == 1) {
-    if (i < WIDTH / TM) store_tile_frags<MODE>(act_ptr(A, A_BT, sample, i), xo + i * FPT);
+// BF16 chunk schedule pins (DEN_FWD_SCHED): the bias and the first FWD_PF weight fragments up
+// front, then per k-step its NB MFMAs, the LDS read of fragment k + FWD_PF and V VALU instructions
+// of the previous tile's epilogue (softplus + bf16 packing).
+template <int KS1, int KS2, int NB, bool EPI_VALU>
+__device__ __forceinline__ void fwd_interleave() {
+#if DEN_FWD_SCHED
+  constexpr int V = EPI_VALU ? (NB * 90 + KS1 + KS2 - 1) / (KS1 + KS2) : 1;
+  constexpr int PF1 = DEN_FWD_PF < KS1 ? DEN_FWD_PF : KS1;
+  constexpr int PF2 = DEN_FWD_PF < KS2 ? DEN_FWD_PF : KS2;
+  __builtin_amdgcn_sched_group_barrier(0x100, 4 + PF1, 0);  // DS read: bias (4) + first fragments
+#pragma unroll
+  for (int k = 0; k < KS1; ++k) {
+    __builtin_amdgcn_sched_group_barrier(0x008, NB, 0);     // MFMA
+    if (k + PF1 < KS1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, V, 0);      // VALU
   }
+  if constexpr (KS2 > 0) {
+    __builtin_amdgcn_sched_group_barrier(0x100, PF2, 0);
+#pragma unroll
+    for (int k = 0; k < KS2; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, NB, 0);
+      if (k + PF2 < KS2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+    }
+  }
+#endif
 }
 
-template <int MODE, int L, int KS1, int KS2, int EPI, typename Frag, typename Acc>
-__device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, int64_t sample, const Frag* x1,
-                                          const Frag* x2, Frag* xo, int outA, Acc* special) {
+template <int MODE, bool TRAIN, int L, int KS1, int S1, int KS2, int S2, int EPI, int NB, typename Frag>
+__device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, const int64_t* sample,
+                                          const Frag* x1, const Frag* x2, Frag* xo, int outA, FwdOut* out,
+                                          FwdVm& vm) {
   using T = Tr<MODE>;
+  using Acc = typename T::Acc;
   constexpr int TM = T::TM;
   constexpr int NT = fwd_tiles(MODE, L);
   constexpr int CB = fwd_chunk_index(MODE, L);
   const int lane = threadIdx.x & 63, grp = lane / TM;
-  Acc prev;
+  Acc prev[NB];
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     auto body = [&](const char* chunk) {
-      if (i >= 2) fwd_store<MODE, EPI>(A, sample, i - 2, xo, outA);
-      Acc acc;
+      Acc acc[NB];
       const float* bias = (const float*)(lds + FWD_RING * LDS_BUF) + (CB + i) * TM + grp * T::REGS;
-#if DEN_FWD_STAGGER
-      // waves 4-7 (each SIMD's second wave) run the epilogue of tile i-1 BEFORE the MFMA chain of
-      // tile i, waves 0-3 after it: within a barrier interval the two waves of a SIMD then offer
-      // the matrix pipe and the VALU complementary work instead of the same work at once
-      const bool late = (threadIdx.x >> 6) >= 4;
-      if (late) {
-        if (i > 0) fwd_epilogue<MODE, L, EPI>(A, sample, prev, i - 1, xo, outA, special);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#endif
 #pragma unroll
-      for (int r = 0; r < T::REGS; ++r) acc[r] = bias[r];
-      mfma_chunk<MODE, KS1>(chunk, x1, acc);
-      if constexpr (KS2 > 0) mfma_chunk<MODE, KS2>(chunk + KS1 * TM * T::KI * es_of(MODE), x2, acc);
-#if DEN_FWD_STAGGER
-      if (!late) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (i > 0) fwd_epilogue<MODE, L, EPI>(A, sample, prev, i - 1, xo, outA, special);
+      for (int r = 0; r < T::REGS; ++r) acc[0][r] = bias[r];
+#pragma unroll
+      for (int b = 1; b < NB; ++b) acc[b] = acc[0];
+      mfma_chunk_nb<MODE, KS1, NB, S1>(chunk, x1, acc);
+      if constexpr (KS2 > 0) mfma_chunk_nb<MODE, KS2, NB, S2>(chunk + KS1 * TM * T::KI * es_of(MODE), x2, acc);
+      if (i > 0) fwd_epilogue<MODE, L, EPI, NB>(prev, i - 1, xo, out);
+      if (i >= 2) fwd_store<MODE, TRAIN, EPI, NB>(A, sample, i - 2, xo, outA);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) prev[b] = acc[b];
+      if constexpr (MODE == 1) {
+        if (i > 0) fwd_interleave<KS1, KS2, NB, EPI == 0>();  // i is unrolled: one branch survives
+        else fwd_interleave<KS1, KS2, NB, false>();
       }
-#else
-      if (i > 0) fwd_epilogue<MODE, L, EPI>(A, sample, prev, i - 1, xo, outA, special);
-#endif
-      prev = acc;
     };
     int64_t noff;
     int nbytes;
-    if constexpr (FWD_RING == 3) {
-      fwd_next2<MODE>(L, i, &noff, &nbytes);
-      // stores the body issues: fwd_store of tile i-2 (2 bf16 / 1 f32 instructions per tile)
-      const bool st = A.train && i >= 2 && (EPI == 0 || (EPI == 1 && i - 2 < WIDTH / TM));
-      chunk_step3<fwd_threads(MODE)>(lds, A.w, CB + i, noff, nbytes, st ? (MODE == 1 ? 2 : 1) : 0, body);
-    } else {
-      fwd_next<MODE>(L, i, &noff, &nbytes);
-      chunk_step(lds, A.w, CB + i, noff, nbytes, body);
-    }
+    fwd_ahead<MODE>(L, i, FWD_RING - 1, &noff, &nbytes);
+    fwd_step<fwd_threads(MODE)>(lds, A.w, CB + i, noff, nbytes,
+                                i >= 2 ? fwd_store_ops<MODE, TRAIN, EPI, NB>(i - 2) : 0, vm, body);
   }
-  fwd_epilogue<MODE, L, EPI>(A, sample, prev, NT - 1, xo, outA, special);
-  if constexpr (NT >= 2) fwd_store<MODE, EPI>(A, sample, NT - 2, xo, outA);
-  fwd_store<MODE, EPI>(A, sample, NT - 1, xo, outA);
+  fwd_epilogue<MODE, L, EPI, NB>(prev, NT - 1, xo, out);
+  if constexpr (NT >= 2) {
+    fwd_store<MODE, TRAIN, EPI, NB>(A, sample, NT - 2, xo, outA);
+    vm.issued += fwd_store_ops<MODE, TRAIN, EPI, NB>(NT - 2);
+  }
+  fwd_store<MODE, TRAIN, EPI, NB>(A, sample, NT - 1, xo, outA);
+  vm.issued += fwd_store_ops<MODE, TRAIN, EPI, NB>(NT - 1);
 }
 
 // ------------------------------------------------------------------ forward kernel
-template <int MODE>
-__global__ __launch_bounds__(fwd_threads(MODE), 1024 / fwd_threads(MODE)) void render_fwd_kernel(RenderArgs<MODE> A) {
+template <int MODE, bool TRAIN>
+__global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render_fwd_kernel(RenderArgs<MODE> A) {
   using T = Tr<MODE>;
   using Frag = typename T::Frag;
   using Acc = typename T::Acc;
   constexpr int TM = T::TM, FPT = T::FPT, REGS = T::REGS;
   constexpr bool EXACT = MODE == 0;
+  constexpr int NB = fwd_nb(MODE);
   constexpr int WGS = fwd_wg_samples(MODE);
   constexpr int NTH = fwd_threads(MODE);
   constexpr int NBIAS = (int)bias_floats(MODE);
@@ -301,119 +427,144 @@ __global__ __launch_bounds__(fwd_threads(MODE), 1024 / fwd_threads(MODE)) void r
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane % TM, grp = lane / TM;
-  const int64_t sample = (int64_t)blockIdx.x * WGS + wave * TM + c;
-  const int64_t ray = sample / A.n_samples;
+  int64_t sample[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) sample[b] = (int64_t)blockIdx.x * WGS + (wave * NB + b) * TM + c;
 #if DEN_FWD_SETPRIO
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half: static priority
 #endif
-  const int k = (int)(sample - ray * A.n_samples);
 
-  // prologue: whole bias table -> LDS, chunk 0 -> slot 0 (and chunk 1 -> slot 1 with the 3-slot ring)
+  // prologue: whole bias table -> LDS, chunks 0 .. FWD_RING-2 -> their ring slots
   for (int q = threadIdx.x; q < NBIAS; q += NTH) bias_lds[q] = A.bias[q];
-  if constexpr (FWD_RING == 3) {
-    dma_chunk_untracked<NTH>(A.w, lds, chunk_bytes_K(fwd_K(MODE, 0)));
-    int64_t off1;
-    int bytes1;
-    fwd_next<MODE>(0, 0, &off1, &bytes1);
-    dma_chunk_untracked<NTH>(A.w + off1, lds + LDS_BUF, bytes1);
-  } else {
-    dma_chunk(A.w, lds, chunk_bytes_K(fwd_K(MODE, 0)));
+#pragma unroll
+  for (int ch = 0; ch < FWD_RING - 1; ++ch) {
+    int64_t off_c;
+    int bytes_c;
+    fwd_ahead<MODE>(0, 0, ch, &off_c, &bytes_c);
+    dma_chunk_untracked<NTH>(A.w + off_c, lds + ch * LDS_BUF, bytes_c);
   }
+  FwdVm vm;
+  vm.issued = 0;
+#pragma unroll
+  for (int ch = 0; ch < FWD_RING; ++ch) vm.mark[ch] = 0;
+#ifdef DEN_FWD_PROF
+  vm.prof[0] = vm.prof[1] = vm.prof[2] = 0;
+  vm.prof[3] = __builtin_amdgcn_s_memtime();
+#endif
 
-  float o[3], d[3], xc[3], sel;
-  if (A.points == 1) {
+  // sample positions -> positional encoding as PE_PAD/TM fake accumulator tiles -> fragments
+  constexpr int PE_T = PE_PAD / TM, PE_S = PE_T * FPT;
+  float dir[NB][3], sel[NB];
+  Frag pe[NB * PE_S];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      o[a] = A.rays_o[sample * 3 + a];
-      d[a] = A.rays_d[sample * 3 + a];
-    }
-    contract_point(o, A.aabb, xc, &sel, A.contraction);
-  } else if (A.points == 2) {
-    // packed ray-marching samples: position o + d (t0 + t1)/2 of the sample's ray (utils.py:83-87)
-    const int64_t r = A.ray_idx[sample];
+  for (int b = 0; b < NB; ++b) {
+    float o[3], xc[3];
+    if (A.points == 1) {
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      o[a] = A.rays_o[r * 3 + a];
-      d[a] = A.rays_d[r * 3 + a];
-    }
-    contract(o, d, A.t_start[sample], A.t_end[sample], A.aabb, xc, &sel, A.contraction);
-  } else {
+      for (int a = 0; a < 3; ++a) {
+        o[a] = A.rays_o[sample[b] * 3 + a];
+        dir[b][a] = A.rays_d[sample[b] * 3 + a];
+      }
+      contract_point(o, A.aabb, xc, &sel[b], A.contraction);
+    } else if (A.points == 2) {
+      // packed ray-marching samples: position o + d (t0 + t1)/2 of the sample's ray (utils.py:83-87)
+      const int64_t r = A.ray_idx[sample[b]];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      o[a] = A.rays_o[ray * 3 + a];
-      d[a] = A.rays_d[ray * 3 + a];
+      for (int a = 0; a < 3; ++a) {
+        o[a] = A.rays_o[r * 3 + a];
+        dir[b][a] = A.rays_d[r * 3 + a];
+      }
+      contract(o, dir[b], A.t_start[sample[b]], A.t_end[sample[b]], A.aabb, xc, &sel[b], A.contraction);
+    } else {
+      const int64_t ray = sample[b] / A.n_samples;
+      const int k = (int)(sample[b] - ray * A.n_samples);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        o[a] = A.rays_o[ray * 3 + a];
+        dir[b][a] = A.rays_d[ray * 3 + a];
+      }
+      const float u = A.jitter[ray];
+      RayGeom g = ray_geom(o, dir[b], A.aabb, A.near_p, A.far_p);
+      float t0, t1;
+      sample_interval(g, k, u, A.n_samples, &t0, &t1);
+      contract(o, dir[b], t0, t1, A.aabb, xc, &sel[b]);
     }
-    const float u = A.jitter[ray];
-    RayGeom g = ray_geom(o, d, A.aabb, A.near_p, A.far_p);
-    float t0, t1;
-    sample_interval(g, k, u, A.n_samples, &t0, &t1);
-    contract(o, d, t0, t1, A.aabb, xc, &sel);
+#pragma unroll
+    for (int p = 0; p < PE_T; ++p) {
+      Acc a;
+#pragma unroll
+      for (int r = 0; r < REGS; ++r) a[r] = enc_feature<EXACT>(xc, p * TM + acc_row(MODE, grp, r), 10);
+      if (TRAIN) store_tile_vals<MODE>(act_ptr(A, A_PE, sample[b], p), a);
+      acc_to_frags<MODE>(a, pe + b * PE_S + p * FPT);
+    }
   }
-
-  // positional encoding as PE_PAD/TM fake accumulator tiles -> fragments
-  constexpr int PE_T = PE_PAD / TM;
-  Frag pe[PE_T * FPT];
-#pragma unroll
-  for (int p = 0; p < PE_T; ++p) {
-    Acc a;
-#pragma unroll
-    for (int r = 0; r < REGS; ++r) a[r] = enc_feature<EXACT>(xc, p * TM + acc_row(MODE, grp, r), 10);
-    if (A.train) store_tile_vals<MODE>(act_ptr(A, A_PE, sample, p), a);
-    acc_to_frags<MODE>(a, pe + p * FPT);
-  }
-  if constexpr (FWD_RING == 3) wait_vm_lgkm0<0>();  // the untracked prologue DMAs landed
+  wait_vm_lgkm0<0>();  // the untracked prologue DMAs landed (and the pe stores drained)
   __syncthreads();
 
   constexpr int KS = WIDTH / T::KI;  // k-steps of a 256-wide input
-  Frag xa[KS], xb[KS];
-  Acc sig_acc, rgb_acc;
-  fwd_layer<MODE, 0, PE_T * FPT, 0, 0>(A, lds, sample, pe, pe, xa, A_S0 + 0, &sig_acc);
-  fwd_layer<MODE, 1, KS, 0, 0>(A, lds, sample, xa, xa, xb, A_S0 + 1, &sig_acc);
-  fwd_layer<MODE, 2, KS, 0, 0>(A, lds, sample, xb, xb, xa, A_S0 + 2, &sig_acc);
-  fwd_layer<MODE, 3, KS, 0, 0>(A, lds, sample, xa, xa, xb, A_S0 + 3, &sig_acc);
-  fwd_layer<MODE, 4, KS, 0, 0>(A, lds, sample, xb, xb, xa, A_S0 + 4, &sig_acc);
-  fwd_layer<MODE, 5, KS, PE_T * FPT, 0>(A, lds, sample, xa, pe, xb, A_S0 + 5, &sig_acc);
-  fwd_layer<MODE, 6, KS, 0, 0>(A, lds, sample, xb, xb, xa, A_S0 + 6, &sig_acc);
-  fwd_layer<MODE, 7, KS, 0, 0>(A, lds, sample, xa, xa, xb, A_S0 + 7, &sig_acc);
-  fwd_layer<MODE, L_B, KS, 0, 1>(A, lds, sample, xb, xb, xa, 0, &sig_acc);  // xa <- bottleneck
+  Frag xa[NB * KS], xb[NB * KS];
+  FwdOut out[NB];
+  fwd_layer<MODE, TRAIN, 0, PE_S, PE_S, 0, 0, 0, NB>(A, lds, sample, pe, pe, xa, A_S0 + 0, out, vm);
+  fwd_layer<MODE, TRAIN, 1, KS, KS, 0, 0, 0, NB>(A, lds, sample, xa, xa, xb, A_S0 + 1, out, vm);
+  fwd_layer<MODE, TRAIN, 2, KS, KS, 0, 0, 0, NB>(A, lds, sample, xb, xb, xa, A_S0 + 2, out, vm);
+  fwd_layer<MODE, TRAIN, 3, KS, KS, 0, 0, 0, NB>(A, lds, sample, xa, xa, xb, A_S0 + 3, out, vm);
+  fwd_layer<MODE, TRAIN, 4, KS, KS, 0, 0, 0, NB>(A, lds, sample, xb, xb, xa, A_S0 + 4, out, vm);
+  fwd_layer<MODE, TRAIN, 5, KS, KS, PE_S, PE_S, 0, NB>(A, lds, sample, xa, pe, xb, A_S0 + 5, out, vm);
+  fwd_layer<MODE, TRAIN, 6, KS, KS, 0, 0, 0, NB>(A, lds, sample, xb, xb, xa, A_S0 + 6, out, vm);
+  fwd_layer<MODE, TRAIN, 7, KS, KS, 0, 0, 0, NB>(A, lds, sample, xa, xa, xb, A_S0 + 7, out, vm);
+  fwd_layer<MODE, TRAIN, L_B, KS, KS, 0, 0, 1, NB>(A, lds, sample, xb, xb, xa, 0, out, vm);  // xa <- bottleneck
 
   // view-direction encoding (mlp.py:353-355): condition * pi, degree 4
-  constexpr int VE_T = VE_PAD / TM;
-  Frag ve[VE_T * FPT];
-  {
+  constexpr int VE_T = VE_PAD / TM, VE_S = VE_T * FPT;
+  Frag ve[NB * VE_S];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
 #pragma clang fp contract(off)
     float dv[3];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) dv[a] = d[a] * 3.1415927f;
+    for (int a = 0; a < 3; ++a) dv[a] = dir[b][a] * 3.1415927f;
 #pragma unroll
     for (int p = 0; p < VE_T; ++p) {
       Acc a;
 #pragma unroll
       for (int r = 0; r < REGS; ++r) a[r] = enc_feature<EXACT>(dv, p * TM + acc_row(MODE, grp, r), 4);
-      if (A.train) store_tile_vals<MODE>(act_ptr(A, A_VE, sample, p), a);
-      acc_to_frags<MODE>(a, ve + p * FPT);
+      if (TRAIN) {
+        store_tile_vals<MODE>(act_ptr(A, A_VE, sample[b], p), a);
+        vm.issued += MODE == 1 ? 2 : 1;
+      }
+      acc_to_frags<MODE>(a, ve + b * VE_S + p * FPT);
     }
   }
-  fwd_layer<MODE, L_G, KS, VE_T * FPT, 0>(A, lds, sample, xa, ve, xb, A_G, &sig_acc);
-  fwd_layer<MODE, L_R, WIDTH_COND / T::KI, 0, 2>(A, lds, sample, xb, xb, xa, 0, &rgb_acc);
+  fwd_layer<MODE, TRAIN, L_G, KS, KS, VE_S, VE_S, 0, NB>(A, lds, sample, xa, ve, xb, A_G, out, vm);
+  fwd_layer<MODE, TRAIN, L_R, WIDTH_COND / T::KI, KS, 0, 0, 2, NB>(A, lds, sample, xb, xb, xa, 0, out, vm);
 
-  // per-sample sigma / rgb (lane group 0 holds rows 0..)
-  const int wl = wave * TM + c;  // WG-local sample
-  if (grp == 0) {
-    // select, not multiply: a sample outside the box (only zero-length samples of missed rays; nerfacc
-    // never produces one) must get sigma = 0 even where exp overflows (inf * 0 = NaN)
-    float sigma = sel != 0.0f ? expf(sig_acc[0] - 1.0f) : 0.0f;
-    float r0 = softplus_b1(rgb_acc[0]);
-    float r1 = A.rd > 1 ? softplus_b1(rgb_acc[1]) : 0.0f;
-    float r2 = A.rd > 2 ? softplus_b1(rgb_acc[2]) : 0.0f;
-    f32x4 v = {sigma, r0, r1, r2};
-    *(f32x4*)(rec_lds + wl * 4) = v;
-    if (A.train) *(f32x4*)(A.rec + sample * 4) = v;
-    if (A.points) {
-      A.out_opacity[sample] = sigma;
+#ifdef DEN_FWD_PROF
+  vm.prof[3] = __builtin_amdgcn_s_memtime() - vm.prof[3];
+  if (blockIdx.x < 512 && lane == 0) {
 #pragma unroll
-      for (int ch = 0; ch < 3; ++ch)
-        if (ch < A.rd) A.out_rgb[sample * A.rd + ch] = v[1 + ch];
+    for (int q = 0; q < 4; ++q) den_fwd_prof[(blockIdx.x * 8 + wave) * 4 + q] = vm.prof[q];
+  }
+#endif
+  // per-sample sigma / rgb (lane group 0 holds rows 0..)
+  if (grp == 0) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int wl = (wave * NB + b) * TM + c;  // WG-local sample
+      // select, not multiply: a sample outside the box (only zero-length samples of missed rays;
+      // nerfacc never produces one) must get sigma = 0 even where exp overflows (inf * 0 = NaN)
+      float sigma = sel[b] != 0.0f ? expf(out[b].sigma_raw - 1.0f) : 0.0f;
+      float r0 = softplus_b1(out[b].rgb_raw[0]);
+      float r1 = A.rd > 1 ? softplus_b1(out[b].rgb_raw[1]) : 0.0f;
+      float r2 = A.rd > 2 ? softplus_b1(out[b].rgb_raw[2]) : 0.0f;
+      f32x4 v = {sigma, r0, r1, r2};
+      *(f32x4*)(rec_lds + wl * 4) = v;
+      if (TRAIN) *(f32x4*)(A.rec + sample[b] * 4) = v;
+      if (A.points) {
+        A.out_opacity[sample[b]] = sigma;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch)
+          if (ch < A.rd) A.out_rgb[sample[b] * A.rd + ch] = v[1 + ch];
+      }
     }
   }
   if (A.points) return;
@@ -703,8 +854,10 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
   }
 }
 
-template __global__ void render_fwd_kernel<0>(RenderArgs<0>);
-template __global__ void render_fwd_kernel<1>(RenderArgs<1>);
+template __global__ void render_fwd_kernel<0, false>(RenderArgs<0>);
+template __global__ void render_fwd_kernel<0, true>(RenderArgs<0>);
+template __global__ void render_fwd_kernel<1, false>(RenderArgs<1>);
+template __global__ void render_fwd_kernel<1, true>(RenderArgs<1>);
 template __global__ void render_bwd_kernel<0, NBL - 1>(RenderArgs<0>);
 template __global__ void render_bwd_kernel<1, NBL - 1>(RenderArgs<1>);
 template __global__ void render_bwd_kernel<1, 2>(RenderArgs<1>);

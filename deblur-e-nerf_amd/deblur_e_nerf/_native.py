@@ -27,7 +27,7 @@ class RenderDesc(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("radiance_dim", ctypes.c_int32), ("n_rays", ctypes.c_int32),
                 ("n_samples", ctypes.c_int32), ("aabb", ctypes.c_float * 6), ("near_plane", ctypes.c_float),
                 ("far_plane", ctypes.c_float), ("train", ctypes.c_int32), ("has_bkgd", ctypes.c_int32),
-                ("points", ctypes.c_int32), ("contraction", ctypes.c_int32)]
+                ("points", ctypes.c_int32), ("contraction", ctypes.c_int32), ("bwd_path", ctypes.c_int32)]
 
 
 class RenderIO(ctypes.Structure):
@@ -217,6 +217,7 @@ def _desc(cfg, n_rays, n_samples, train, has_bkgd, points=0):
     d.has_bkgd = int(has_bkgd)
     d.points = int(points)
     d.contraction = int(cfg.get("contraction", 0))
+    d.bwd_path = int(cfg.get("bwd_path", 0))
     return d
 
 

@@ -104,6 +104,11 @@ typedef struct den_render_desc {
   int32_t contraction;     /* input-space contraction (mlp.py:321-335): 0 AABB, 1 tanh
                               (ngp.py:96-106), 2 unbounded sphere (ngp.py:68-93); the
                               fixed-count sampler (points = 0) needs 0 */
+  int32_t bwd_path;        /* BF16 backward: 0 layer-major hidden layers + streamed weight
+                              gradients (in place: dz_l overwrites the forward activation S_l of
+                              layers 0..6, so one train forward feeds ONE den_render_bwd);
+                              1 the F32 mode's sample-major chain + split-K GEMMs on the same bf16
+                              operands (an A/B reference path).  F32 mode ignores it. */
 } den_render_desc;
 
 /* Device buffers of one render call. */

@@ -1,0 +1,58 @@
+"""Experiment: per-wave cycle split of the BF16 render forward (s_memtime around each weight-chunk
+step: body = MFMA chain + epilogue + stores, wait = vmcnt wait for the next chunk, barrier).
+Needs a DEN_FWD_PROF build of libden (make variant NAME=prof DEFS=-DDEN_FWD_PROF), selected with
+DEN_LIB.  usage: DEN_LIB=deblur-e-nerf_amd/libden_prof.so python profiles/fwd_prof.py [train]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "deblur-e-nerf_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, ROOT)
+
+from deblur_e_nerf import _native as nat  # noqa: E402
+from _util import flat_from_params, synthetic_rays  # noqa: E402
+from oracle import nerf as onerf  # noqa: E402
+
+
+def main():
+    train = len(sys.argv) < 2 or sys.argv[1] == "train"
+    R, S, rd = 131072, 128, 1
+    o, d, u = synthetic_rays(R, seed=5, device="cuda")
+    flat = flat_from_params(onerf.build_params(rd, 1), rd).cuda().requires_grad_(train)
+    packed = nat.PackedWeights("bf16", rd, "cuda")
+    packed.pack(flat.detach())
+    cfg = dict(mode=nat.mode_id("bf16"), rd=rd, aabb=list(onerf.AABB_CHAIR), near=1.43, far=6.63)
+    lib = nat.lib()
+    lib.den_debug_fwd_prof.argtypes = [ctypes.c_void_p]
+    buf = np.zeros(512 * 8 * 4, dtype=np.uint64)
+    ms = []
+    for it in range(4):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.set_grad_enabled(train):
+            e0.record()
+            c, op, dp = nat.render(o, d, u, None, flat, cfg, packed, S)
+            e1.record()
+        torch.cuda.synchronize()
+        ms.append(e0.elapsed_time(e1))
+        del c, op, dp
+    print(f"render call ms (incl. host glue): {['%.2f' % m for m in ms]}")
+    assert lib.den_debug_fwd_prof(buf.ctypes.data) == 0
+    p = buf.reshape(512, 8, 4).astype(np.float64)
+    waves = p[:, :, 3] > 0
+    tot = p[:, :, 3][waves]
+    print(f"train={train} waves={waves.sum()} kernel cycles/wave mean {tot.mean():.0f}")
+    for q, name in enumerate(["body", "vm wait", "barrier"]):
+        v = p[:, :, q][waves]
+        print(f"  {name:8s} {v.mean():10.0f} cyc/wave ({v.mean() / tot.mean() * 100:5.1f} %)")
+    per_wave = p[:, :, 0][waves]
+    print(f"  body min/max over waves {per_wave.min():.0f} / {per_wave.max():.0f}")
+    print(f"  prologue+tail {tot.mean() - p[:, :, :3].sum(-1)[waves].mean():.0f} cyc/wave")
+
+
+if __name__ == "__main__":
+    main()

@@ -31,7 +31,7 @@ def _cfg(mode, rd, near=1.43, far=6.63):
 
 # ----------------------------------------------------------------------------- radiance field vs reference
 @pytest.mark.parametrize("rd", [3, 1])
-@pytest.mark.parametrize("mode,tol_out,tol_grad", [("f32", 1e-4, 1e-4), ("bf16", 3e-2, 5e-2)])
+@pytest.mark.parametrize("mode,tol_out,tol_grad", [("f32", 1e-4, 1e-4), ("bf16", 2e-3, 3e-2)])
 def test_field_matches_reference_golden(golden_dir, rd, mode, tol_out, tol_grad):
     nat = _nat()
     z = np.load(os.path.join(golden_dir, f"mlp_rd{rd}.npz"))
@@ -75,7 +75,8 @@ def test_field_matches_reference_golden(golden_dir, rd, mode, tol_out, tol_grad)
                                                   ("bf16", 128, 3, True), ("bf16", 64, 1, True)])
 def test_render_matches_oracle(mode, n_samples, rd, bk):
     nat = _nat()
-    tol_out, tol_grad = (1e-4, 1e-4) if mode == "f32" else (3e-2, 6e-2)
+    # BF16 measured (r02): outputs <= 1.1e-4, worst gradient 1.4e-2
+    tol_out, tol_grad = (1e-4, 1e-4) if mode == "f32" else (1e-3, 3e-2)
     R = 16 if n_samples == 128 else 24
     o, d, u = synthetic_rays(R, seed=7 + rd)
     # a ray that misses the box and a ray starting inside it
@@ -98,7 +99,7 @@ def test_render_matches_oracle(mode, n_samples, rd, bk):
     d2n = d2 / (o2 + 1e-10)
     errs = (rel_err(c2, col), rel_err(o2, op), rel_err(d2n, dep))
     print(f"[{mode} S={n_samples} rd={rd}] colour/opacity/depth err {errs}")
-    assert max(errs) <= tol_out * (1 if mode == "f32" else 4)
+    assert max(errs) <= tol_out
     ((c2 * gc.to(DEV)).sum() + (o2 * go.to(DEV)).sum() + (d2n * gd.to(DEV)).sum()).backward()
     gflat = unflat(flat.grad.cpu(), rd)
     worst = 0.0
@@ -111,7 +112,7 @@ def test_render_matches_oracle(mode, n_samples, rd, bk):
     print(f"[{mode} S={n_samples} rd={rd}] worst grad err {worst:.2e}")
 
 
-def _render_grads(mode, rd, R, n_samples, seed, env=None):
+def _render_grads(mode, rd, R, n_samples, seed, bwd_path=0):
     nat = _nat()
     o, d, u = synthetic_rays(R, seed=seed)
     p = onerf.build_params(rd, 1)
@@ -119,21 +120,13 @@ def _render_grads(mode, rd, R, n_samples, seed, env=None):
     packed = nat.PackedWeights(mode, rd, DEV)
     packed.pack(flat.detach())
     bk = torch.tensor([0.9, 0.8, 0.7][:rd], device=DEV, requires_grad=True)
-    old = os.environ.get("DEN_BWD")
-    if env is not None:
-        os.environ["DEN_BWD"] = env
-    try:
-        c, op, dp = nat.render(o.to(DEV), d.to(DEV), u.to(DEV), bk, flat, _cfg(mode, rd), packed, n_samples)
-        g = torch.Generator().manual_seed(seed + 1)
-        gc = torch.randn(c.shape, generator=g).to(DEV)
-        go = torch.randn(op.shape, generator=g).to(DEV)
-        ((c * gc).sum() + (op * go).sum()).backward()
-        torch.cuda.synchronize()
-    finally:
-        if old is None:
-            os.environ.pop("DEN_BWD", None)
-        else:
-            os.environ["DEN_BWD"] = old
+    cfg = dict(_cfg(mode, rd), bwd_path=bwd_path)
+    c, op, dp = nat.render(o.to(DEV), d.to(DEV), u.to(DEV), bk, flat, cfg, packed, n_samples)
+    g = torch.Generator().manual_seed(seed + 1)
+    gc = torch.randn(c.shape, generator=g).to(DEV)
+    go = torch.randn(op.shape, generator=g).to(DEV)
+    ((c * gc).sum() + (op * go).sum()).backward()
+    torch.cuda.synchronize()
     return c.detach(), flat.grad.detach().clone(), bk.grad.detach().clone(), p
 
 
@@ -144,7 +137,7 @@ def test_hidden_layer_major_backward_matches_sample_major(rd):
     bf16 operands -- only f32 summation order differs."""
     R = 1024  # 131072 samples = 4096 wave blocks = 16 per workgroup
     c1, g1, b1, _ = _render_grads("bf16", rd, R, 128, seed=21)
-    c2, g2, b2, _ = _render_grads("bf16", rd, R, 128, seed=21, env="sample")
+    c2, g2, b2, _ = _render_grads("bf16", rd, R, 128, seed=21, bwd_path=1)
     assert torch.equal(c1, c2)
     gf1, gf2 = unflat(g1.cpu(), rd), unflat(g2.cpu(), rd)
     worst = max(norm_rel(gf1[k], gf2[k]) for k in gf2)
@@ -166,11 +159,12 @@ def test_render_bf16_many_blocks_matches_oracle():
     gen = torch.Generator().manual_seed(34)
     gc, go = torch.randn(col.shape, generator=gen), torch.randn(op.shape, generator=gen)
     ((col * gc).sum() + (op * go).sum()).backward()
-    assert rel_err(c, col) <= 0.12
+    e_col = rel_err(c, col)
     gf = unflat(g.cpu(), rd)
     worst = max(norm_rel(gf[k], v.grad) for k, v in p.items())
-    print(f"bf16 many-block worst grad err {worst:.2e}")
-    assert worst <= 6e-2
+    print(f"bf16 many-block colour err {e_col:.2e}, worst grad err {worst:.2e}")
+    assert e_col <= 1e-3  # measured (r02): 1e-4-level
+    assert worst <= 2e-2  # measured (r02): 6.9e-3
 
 
 def test_render_rejects_bad_shapes():
@@ -206,6 +200,6 @@ def test_render_survives_density_overflow(mode):
     assert torch.isfinite(ref_c).all()  # the oracle's composite handles inf as nerfacc does
     assert torch.isfinite(c).all() and torch.isfinite(op).all()
     assert torch.allclose(op.cpu(), torch.ones(R), atol=1e-6)
-    tol = 1e-4 if mode == "f32" else 3e-2
+    tol = 1e-4 if mode == "f32" else 1e-3
     assert rel_err(c, ref_c) <= tol
     assert torch.isfinite(flat.grad).all()
