@@ -225,6 +225,94 @@ def cpu_baseline(rd, threads, legs=((4096, 64, 2, 5), (4096, 128, 1, 3))):
                 legs=out, **_cpu_info(threads))
 
 
+def _view_rays(n_px, radius=4.03, focal_px=None, direction=(0.62, -0.55, 0.56)):
+    """Held-out camera: n_px x n_px pixel rays of a pinhole at `radius` along `direction`,
+    looking at the origin (the synthetic chair's AABB centre)."""
+    c = torch.tensor(direction)
+    c = c / c.norm() * radius
+    z = -c / c.norm()
+    x = torch.linalg.cross(z, torch.tensor([0.0, 0.0, 1.0]))
+    x = x / x.norm()
+    y = torch.linalg.cross(z, x)
+    f = focal_px or 1.2 * n_px
+    j, i = torch.meshgrid(torch.arange(n_px) + 0.5, torch.arange(n_px) + 0.5, indexing="ij")
+    d = ((i - n_px / 2) / f)[..., None] * x + ((j - n_px / 2) / f)[..., None] * y + z
+    d = d.reshape(-1, 3)
+    d = d / d.norm(dim=-1, keepdim=True)
+    return c.expand(d.shape[0], 3).contiguous(), d.contiguous()
+
+
+def psnr_vs_oracle(rd, threads, dev, steps=8, n_events=1024, n_samples=64, view=64, modes=("f32", "bf16")):
+    """The second half of BASELINE's metric ("PSNR vs ref"; north_star: rendered PSNR within 0.1 dB
+    of the reference).  A teacher scene (a differently seeded MLP, density raised) supervises a
+    configs[0]-shaped batch (1024 events = 4096 rays x 64 samples): each event's measured
+    log-intensity change is the teacher's.  The HIP TrainStep and the oracle (the reference path
+    restated, parity-pinned by tests/) train from the SAME init on that batch for `steps` Adam
+    steps; both render a held-out 64x64 view (deblur_e_nerf.py:602-652 eval render), scored against
+    the teacher's render with the reference's PSNR (metric.py:68-72, data range 1)."""
+    from oracle import nerf as onerf
+    from oracle.train import step_loss
+    from deblur_e_nerf import _native as nat
+    from deblur_e_nerf.loss_metric.metric import psnr
+    from deblur_e_nerf.train import TrainStep, synthetic_batch
+    torch.set_num_threads(threads)
+    teacher = onerf.build_params(rd, 77)
+    teacher["mlp.sigma_layer.output_layer.bias"] += 3.0
+    ones = torch.ones(rd)
+    b = synthetic_batch(n_events, seed=21)
+    with torch.no_grad():
+        col, _, _, _ = onerf.render_rays(teacher, b["rays_o"], b["rays_d"], b["jitter"], n_samples=n_samples,
+                                         bkgd=ones)
+        y = torch.log(col[:, 0] + 1e-3).view(4, n_events)
+        b["lid"] = (y[1] - y[0]).float().contiguous()
+        vo, vd = _view_rays(view)
+        vu = torch.full((vo.shape[0],), 0.5)
+        target, _, _, _ = onerf.render_rays(teacher, vo, vd, vu, n_samples=n_samples, bkgd=ones)
+    out = {}
+    oracle_view = None
+    for mode in modes:
+        ts = TrainStep(n_events, n_samples=n_samples, radiance_dim=rd, mode=mode, device=dev, seed=0)
+        ts.load_batch(**b)
+        if oracle_view is None:  # the oracle student: the same init, torch.optim.Adam as TrainStep's
+            flat0 = ts.flat.detach().cpu()
+            names = [n for n, _, _ in onerf.layer_specs(rd)]
+            p, off = {}, 0
+            for n, fin, fout in onerf.layer_specs(rd):
+                p[n + ".weight"] = flat0[off:off + fin * fout].view(fout, fin).clone().requires_grad_(True)
+                off += fin * fout
+                p[n + ".bias"] = flat0[off:off + fout].clone().requires_grad_(True)
+                off += fout
+            bk = ts.bkgd_orig.detach().cpu().clone().requires_grad_(True)
+            leaves = [p[n + s] for n in names for s in (".weight", ".bias")]
+            opt = torch.optim.Adam([{"params": leaves, "weight_decay": ts.wd}, {"params": [bk], "weight_decay": 0.0}],
+                                   lr=ts.lr)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                opt.zero_grad()
+                total, _, _ = step_loss(p, torch.nn.functional.softplus(bk), b, n_samples)
+                total.backward()
+                opt.step()
+            oracle_s = time.perf_counter() - t0
+            with torch.no_grad():
+                oracle_view, _, _, _ = onerf.render_rays(p, vo, vd, vu, n_samples=n_samples,
+                                                         bkgd=torch.nn.functional.softplus(bk))
+            out["oracle"] = {"psnr_db": round(psnr(oracle_view.to(dev), target.to(dev), 1.0), 3),
+                             "train_s": round(oracle_s, 2)}
+        for _ in range(steps):
+            ts.step()
+        with torch.no_grad():
+            cfg = dict(ts.cfg)
+            hv, _, _ = nat.render(vo.to(dev), vd.to(dev), vu.to(dev),
+                                  torch.nn.functional.softplus(ts.bkgd_orig.detach()), ts.flat.detach(), cfg,
+                                  ts.packed, n_samples)
+        ph = psnr(hv, target.to(dev), 1.0)
+        out[mode] = {"psnr_db": round(ph, 3), "delta_db": round(ph - out["oracle"]["psnr_db"], 4),
+                     "psnr_vs_oracle_render_db": round(psnr(hv, oracle_view.to(dev), 1.0), 2)}
+    return dict(out, steps=steps, setup=f"teacher-scene supervision, {n_events} events = {4 * n_events} rays x "
+                                        f"{n_samples} samples, {steps} Adam steps from one init, held-out "
+                                        f"{view}x{view} view, PSNR vs the teacher render (data range 1)")
+
+
 def cpu_baseline_pixbw(n_rays, n_samples, rd, S, threads):
     """Bounded CPU sample of the pixel-bandwidth-on step (oracle): median of 3 after 1 warm-up."""
     from oracle import nerf as onerf
@@ -351,6 +439,7 @@ def main():
     roofline["phases_ms"] = {k: round(v, 3) for k, v in phases.items()}
 
     cpu = None
+    psnr_info = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
             threads = cpu_threads()
@@ -358,6 +447,11 @@ def main():
                    else cpu_baseline(a.rd, threads))
         except Exception as e:  # pragma: no cover - reported, not fatal
             cpu = {"error": repr(e)}
+        if not a.pixbw:
+            try:  # the oracle leg's second product: ΔPSNR of the HIP-trained render vs the oracle-trained one
+                psnr_info = psnr_vs_oracle(a.rd, cpu_threads(), dev)
+            except Exception as e:  # pragma: no cover - reported, not fatal
+                psnr_info = {"error": repr(e)}
     if rank == 0:
         out = {
             "metric": "train-step rays/sec at 131072 rays x 128 samples",
@@ -373,6 +467,7 @@ def main():
             "loss": [round(x, 6) for x in loss],
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "psnr": psnr_info,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

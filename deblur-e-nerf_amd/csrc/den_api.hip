@@ -141,6 +141,8 @@ int check_desc(const den_render_desc* d) {
     return fail(DEN_EUNSUPPORTED, "n_rays * n_samples must be a multiple of the workgroup tile "
                                   "(den_render_tile_samples)");
   if (d->points < 0 || d->points > 2) return fail(DEN_EINVAL, "points must be 0, 1 or 2");
+  if (d->points == 0 && fwd_wg_samples(d->mode) % d->n_samples != 0)
+    return fail(DEN_EUNSUPPORTED, "the fused compositing needs whole rays per forward workgroup");
   if (d->contraction < 0 || d->contraction > 2) return fail(DEN_EINVAL, "contraction must be 0 (AABB), 1 (tanh) or 2 (sphere)");
   if (d->points == 0 && d->contraction != 0)
     return fail(DEN_EUNSUPPORTED, "the fixed-count sampler (points = 0) marches the AABB: contraction must be 0");

@@ -102,11 +102,16 @@ static_assert(FWD_RING == 3 || FWD_RING == 4, "forward weight ring: 3 or 4 slots
 #define DEN_FWD_NB 1  // r02 A/B: NB = 2 (4 waves x 64 samples) 27.7 ms vs 24.9 ms for NB = 1
 #endif
 static_assert(DEN_FWD_NB == 1 || DEN_FWD_NB == 2, "BF16 forward: 1 or 2 column blocks per wave");
+#ifndef DEN_FWD_WAVES_BF16
+#define DEN_FWD_WAVES_BF16 (8 / DEN_FWD_NB)
+#endif
 DEN_HD constexpr int fwd_nb(int mode) { return mode == 1 ? DEN_FWD_NB : 1; }
-DEN_HD constexpr int fwd_waves(int mode) { return 8 / fwd_nb(mode); }
+DEN_HD constexpr int fwd_waves(int mode) { return mode == 1 ? DEN_FWD_WAVES_BF16 : 8; }
 DEN_HD constexpr int fwd_threads(int mode) { return 64 * fwd_waves(mode); }
-DEN_HD constexpr int fwd_wg_samples(int mode) { return 8 * tm_of(mode); }
-DEN_HD constexpr int fwd_min_waves(int mode) { return fwd_waves(mode) / 4; }  // waves per SIMD
+DEN_HD constexpr int fwd_wg_samples(int mode) { return fwd_waves(mode) * fwd_nb(mode) * tm_of(mode); }
+// waves per SIMD the register budget is sized for: 1 with two blocks per wave (512 registers),
+// else 2 (256 registers; 4-wave workgroups then run two per CU)
+DEN_HD constexpr int fwd_min_waves(int mode) { return fwd_nb(mode) == 2 ? 1 : 2; }
 
 // per-wave count of DMA instructions dma_chunk_untracked<NTH> issues for `bytes` (wave-uniform)
 template <int NTH>
