@@ -92,13 +92,34 @@ def contract_aabb(x, aabb):
     return 2 * math.pi * (xh - 0.5), sel
 
 
+def contract_unbounded(x, aabb, kind):
+    """The unbounded input-space contractions of VanillaNeRFRadianceField.contract_input_space
+    (mlp.py:321-335): "sphere" = ngp.py:68-93 contract_to_unisphere (box at [-1, 1], outside the unit
+    ball x -> (2 - 1/|x|) x/|x|, then /4 + 1/2), "tanh" = ngp.py:96-106 contract_tanh; then the same
+    selector and [-pi, pi] map as the AABB case."""
+    lo = torch.tensor(aabb[:3], dtype=x.dtype)
+    hi = torch.tensor(aabb[3:], dtype=x.dtype)
+    xh = (x - lo) / (hi - lo)
+    if kind == "sphere":
+        xh = xh * 2 - 1
+        mag = xh.norm(dim=-1, keepdim=True)
+        xh = torch.where(mag > 1, (2 - 1 / mag) * (xh / mag), xh)
+        xh = xh / 4 + 0.5
+    elif kind == "tanh":
+        xh = (torch.tanh(xh - 0.5) + 1) / 2
+    else:
+        raise ValueError(kind)
+    sel = ((xh > 0.0) & (xh < 1.0)).all(dim=-1)
+    return 2 * math.pi * (xh - 0.5), sel
+
+
 def _lin(p, name, h):
     return torch.nn.functional.linear(h, p[name + ".weight"], p[name + ".bias"])
 
 
-def radiance_field(p, x, d, aabb=AABB_CHAIR, depth=8, skip=4):
+def radiance_field(p, x, d, aabb=AABB_CHAIR, depth=8, skip=4, contraction="aabb"):
     """VanillaNeRFRadianceField.forward(x, d) -> (rgb (n, rd), sigma (n, 1))."""
-    xc, sel = contract_aabb(x, aabb)
+    xc, sel = contract_aabb(x, aabb) if contraction == "aabb" else contract_unbounded(x, aabb, contraction)
     pe = encode(xc, 10)
     h = pe
     for i in range(depth):

@@ -92,23 +92,30 @@ def save(name, **arrays):
 
 
 # ----------------------------------------------------------------------------
-def gen_mlp(rd, seed):
+def gen_mlp(rd, seed, contraction="aabb"):
+    """VanillaNeRFRadianceField forward/backward; contraction "aabb" (mlp_rd{rd}.npz) or the
+    unbounded "sphere" / "tanh" input-space contractions (mlp_rd{rd}_{contraction}.npz: mlp.py:321-335,
+    ngp.py:68-106), whose positions reach 4x the box so the contracted shells are exercised."""
     mlp = _refload.load("external.mlp")
     ngp = _refload.load("external.ngp")
     ContractionType = sys.modules["nerfacc"].ContractionType
+    ctype = {"aabb": ContractionType.AABB, "sphere": ContractionType.UN_BOUNDED_SPHERE,
+             "tanh": ContractionType.UN_BOUNDED_TANH}[contraction]
     torch.manual_seed(seed)
     field = mlp.VanillaNeRFRadianceField(
         aabb=[-1.5, -1.5, -1.5, 1.5, 1.5, 1.5], net_depth=8, net_width=256,
         skip_layer=4, net_depth_condition=1, net_width_condition=128, num_dim=3,
-        contraction_type=ContractionType.AABB, radiance_dim=rd,
+        contraction_type=ctype, radiance_dim=rd,
         hidden_activation=torch.nn.Softplus(beta=100),
         density_activation=ngp.shifted_trunc_exp,
         radiance_activation=torch.nn.Softplus(beta=1),
         pos_encoder_max_deg=10, view_encoder_max_deg=4, weight_norm=False)
     g = torch.Generator().manual_seed(1000 + seed)
     n = 512
-    # positions: mostly inside the AABB, some outside (selector = 0)
-    x = (torch.rand(n, 3, generator=g) * 3.6 - 1.8).float()
+    # positions: mostly inside the AABB, some outside (selector = 0); unbounded contractions: up to
+    # 4x the box, the sphere's |x| > 1 shell and the tanh tails
+    span = 1.8 if contraction == "aabb" else 6.0
+    x = (torch.rand(n, 3, generator=g) * 2 * span - span).float()
     d = torch.randn(n, 3, generator=g)
     d = d / d.norm(dim=-1, keepdim=True)
     g_rgb = torch.randn(n, rd, generator=g)
@@ -130,7 +137,8 @@ def gen_mlp(rd, seed):
                 out[f"grad:{k}"] = gr
     field.float()
     wsum = {f"wsum:{k}": np.array(p.detach().double().sum().item()) for k, p in field.named_parameters()}
-    save(f"mlp_rd{rd}.npz", seed=seed, x=x.numpy(), d=d.numpy(), g_rgb=g_rgb.numpy(),
+    name = f"mlp_rd{rd}.npz" if contraction == "aabb" else f"mlp_rd{rd}_{contraction}.npz"
+    save(name, seed=seed, contraction=np.array(contraction), x=x.numpy(), d=d.numpy(), g_rgb=g_rgb.numpy(),
          g_sigma=g_sig.numpy(), param_names=np.array(names), **out, **wsum)
 
 
@@ -696,6 +704,11 @@ def gen_step_pixbw():
     gen_step(True, 1)
 
 
+def gen_mlp_unbounded():
+    gen_mlp(3, seed=2, contraction="sphere")
+    gen_mlp(1, seed=3, contraction="tanh")
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.set_num_threads(8)
     for name in sys.argv[1:]:
@@ -704,6 +717,7 @@ elif __name__ == "__main__":
     torch.set_num_threads(8)
     gen_mlp(3, seed=0)
     gen_mlp(1, seed=1)
+    gen_mlp_unbounded()
     gen_foh()
     gen_pixbw(16, EDS, "eds")
     gen_pixbw(30, EDS, "eds")

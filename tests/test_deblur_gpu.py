@@ -128,3 +128,74 @@ def test_configure_optimizers_and_fit_step(golden_dir, monkeypatch):
     assert torch.isfinite(loss) and float(step.max()) > 0
     # Adam's first step moves every parameter with a non-zero gradient by ~lr
     assert float(step.max()) <= 1.01e-3
+
+
+def _event_batch(N, seed, img=800, ts_lo=1.5e8, ts_hi=9.5e8):
+    """A reference-shaped batch (datamodule.py:215-247) of N events, as tests/golden/make_golden.py
+    builds them: events (1, N, ...) and the normalized samples (1, N)."""
+    g = torch.Generator().manual_seed(seed)
+    num_pos = (torch.rand(N, generator=g) < 0.5).long()
+    end_ts = (torch.rand(N, generator=g, dtype=torch.float64) * (ts_hi - ts_lo) + ts_lo).long()
+    start_ts = end_ts - (-torch.log(torch.rand(N, generator=g, dtype=torch.float64)) * 2e6 + 2e4).long()
+    position = torch.rand(N, 2, generator=g) * (img - 1)
+    u = torch.rand(3, N, generator=g, dtype=torch.float64)
+    ev = dict(position=position[None], start_ts=start_ts[None], end_ts=end_ts[None], num_pos=num_pos[None],
+              num_neg=(1 - num_pos)[None])
+    nz = dict(ts_diff=torch.ones(1, N, dtype=torch.float64), diff_start_ts=u[0][None],
+              ts_subdiff=(1 - torch.sqrt(1 - u[1]))[None], subdiff_start_ts=u[2][None])
+    return dict(event=ev, normalized=nz)
+
+
+def _slice(batch, a, b):
+    return {grp: {k: v[:, a:b].contiguous().to(DEV) for k, v in d.items()} for grp, d in batch.items()}
+
+
+def test_gradient_accumulation_equals_one_big_batch(golden_dir, monkeypatch):
+    """PL accumulate_grad_batches semantics (configs[3]: 07_ziggy_and_fuzz_hdr.yaml:203,
+    accumulate_grad_batches 8; deblur_e_nerf.py:465 occupancy update on the first micro-batch only,
+    :1286-1291 batch-size update on the second-to-last): 8 micro-batches of n events through
+    fit_step (loss / 8 accumulated, one optimizer step on the last) give the gradient of ONE
+    training_step on the 8n-event batch -- the same marching draws, split per micro-batch -- and
+    leave the parameters untouched until the 8th.  F32 at the north-star 1e-4 (measured 2.7e-5: the
+    loss gradient is a difference of nearby renders, so f32 summation order shows at ~1e-5)."""
+    from deblur_e_nerf.external import marching
+    z = np.load(os.path.join(golden_dir, "step_nopixbw_rd1.npz"))
+    n, acc = 40, 8
+    big = _event_batch(n * acc, seed=31)
+    jit = torch.rand(4, n * acc, generator=torch.Generator().manual_seed(32))
+    occ_u = z["occ_u"]
+
+    m_big = build_model(z)
+    m_big.train()
+    monkeypatch.setattr(marching, "_uniform", _Draws([occ_u, jit.reshape(-1).numpy()]))
+    loss_big = m_big.training_step(_slice(big, 0, n * acc), 0)
+    loss_big.backward()
+    g_big = torch.cat([p.grad.detach().reshape(-1) for p in m_big.parameters() if p.grad is not None]).cpu()
+
+    m_acc = build_model(z)
+    m_acc.train()
+    m_acc.trainer.accumulate_grad_batches = acc
+    opt = m_acc.configure_optimizers()["optimizer"]
+    before = m_acc.nerf.radiance_field.flat_params.detach().clone()
+    g_acc = None
+    for k in range(acc):
+        draws = ([occ_u] if k == 0 else []) + [jit[:, k * n:(k + 1) * n].reshape(-1).numpy()]
+        monkeypatch.setattr(marching, "_uniform", _Draws(draws))
+        if k == acc - 1:
+            # fit_step's last micro-batch, spelled out to read the accumulated gradient before
+            # the optimizer step consumes it
+            loss = m_acc.training_step(_slice(big, k * n, (k + 1) * n), k)
+            (loss / acc).backward()
+            g_acc = torch.cat([p.grad.detach().reshape(-1) for p in m_acc.parameters()
+                               if p.grad is not None]).cpu()
+            opt.step()
+            torch.cuda.synchronize()
+            assert not torch.equal(m_acc.nerf.radiance_field.flat_params, before)
+            break
+        m_acc.fit_step(_slice(big, k * n, (k + 1) * n), k, opt)
+        torch.cuda.synchronize()
+        assert torch.equal(m_acc.nerf.radiance_field.flat_params, before)  # no step before the 8th
+    e = norm_rel(g_acc, g_big)
+    print(f"8 accumulated micro-batches vs one 8x batch: gradient rel err {e:.2e} "
+          f"(loss {float(loss_big):.6f})")
+    assert g_acc.shape == g_big.shape and e <= 1e-4

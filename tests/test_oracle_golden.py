@@ -23,9 +23,10 @@ def rel_err(a, b):
 
 
 # --------------------------------------------------------------------------- radiance field
-@pytest.mark.parametrize("rd", [1, 3])
-def test_radiance_field_matches_reference(golden_dir, rd):
-    z = _load(golden_dir, f"mlp_rd{rd}.npz")
+@pytest.mark.parametrize("fixture,rd", [("mlp_rd1", 1), ("mlp_rd3", 3), ("mlp_rd3_sphere", 3), ("mlp_rd1_tanh", 1)])
+def test_radiance_field_matches_reference(golden_dir, fixture, rd):
+    z = _load(golden_dir, fixture + ".npz")
+    contraction = str(z["contraction"]) if "contraction" in z.files else "aabb"
     p = onerf.build_params(rd, int(z["seed"]))
     # same weights as the reference's construction under the same seed
     for name in z["param_names"]:
@@ -34,7 +35,7 @@ def test_radiance_field_matches_reference(golden_dir, rd):
         p[k].requires_grad_(True)
     x = torch.from_numpy(z["x"])
     d = torch.from_numpy(z["d"])
-    rgb, sig = onerf.radiance_field(p, x, d)
+    rgb, sig = onerf.radiance_field(p, x, d, contraction=contraction)
     # bitwise-level agreement with the reference's fp32 forward (same torch ops on CPU)
     assert rel_err(rgb.detach(), z["rgb_f32"]) < 1e-6
     assert rel_err(sig.detach(), z["sigma_f32"]) < 1e-6

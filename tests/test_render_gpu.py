@@ -30,21 +30,27 @@ def _cfg(mode, rd, near=1.43, far=6.63):
 
 
 # ----------------------------------------------------------------------------- radiance field vs reference
-@pytest.mark.parametrize("rd", [3, 1])
+CONTRACTION_ID = {"aabb": 0, "tanh": 1, "sphere": 2}  # den_render_desc.contraction
+
+
+@pytest.mark.parametrize("fixture,rd", [("mlp_rd3", 3), ("mlp_rd1", 1), ("mlp_rd3_sphere", 3), ("mlp_rd1_tanh", 1)])
 @pytest.mark.parametrize("mode,tol_out,tol_grad", [("f32", 1e-4, 1e-4), ("bf16", 2e-3, 3e-2)])
-def test_field_matches_reference_golden(golden_dir, rd, mode, tol_out, tol_grad):
+def test_field_matches_reference_golden(golden_dir, fixture, rd, mode, tol_out, tol_grad):
+    """VanillaNeRFRadianceField.forward/backward against the reference run (make_golden.gen_mlp),
+    with the AABB contraction and the unbounded sphere / tanh contractions of configs[3]/[4]."""
     nat = _nat()
-    z = np.load(os.path.join(golden_dir, f"mlp_rd{rd}.npz"))
+    z = np.load(os.path.join(golden_dir, fixture + ".npz"))
+    contraction = str(z["contraction"]) if "contraction" in z.files else "aabb"
     p = onerf.build_params(rd, int(z["seed"]))
     flat = flat_from_params(p, rd).to(DEV).requires_grad_(True)
     packed = nat.PackedWeights(mode, rd, DEV)
     packed.pack(flat.detach())
     x = torch.from_numpy(z["x"]).to(DEV)
     d = torch.from_numpy(z["d"]).to(DEV)
-    rgb, sig = nat.field(x, d, flat, _cfg(mode, rd), packed)
+    rgb, sig = nat.field(x, d, flat, dict(_cfg(mode, rd), contraction=CONTRACTION_ID[contraction]), packed)
     e_rgb = rel_err(rgb, z["rgb_f32"])
     e_sig = rel_err(sig, z["sigma_f32"][:, 0])
-    print(f"[{mode} rd={rd}] field rgb err {e_rgb:.2e} sigma err {e_sig:.2e}")
+    print(f"[{mode} {fixture}] field rgb err {e_rgb:.2e} sigma err {e_sig:.2e}")
     assert e_rgb <= tol_out and e_sig <= tol_out
     loss = (rgb * torch.from_numpy(z["g_rgb"]).to(DEV)).sum() + (sig * torch.from_numpy(z["g_sigma"][:, 0]).to(DEV)).sum()
     loss.backward()
