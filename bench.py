@@ -74,8 +74,10 @@ def flop_per_sample(rd):
 # hidden_bwd: 7 launches (L7..L1), each reading dz_l + a_(l-1) and writing dz_(l-1), 256 bf16 each =
 # 1536 B; render_fwd: the activations + record it stores for the backward; render_bwd: head
 # activations read + dz written; dw_gemm: the dz/x operand streams of the split-K GEMMs.
+# dw_gemm_kernel (the streamed weight-gradient kernels, den_dwstream.hip): dz_0 + dz_5 + pe, dz_b + S7,
+# dz_g + bottleneck + ve, dz_r + g = 1152 + 1088 + 832 + 320 B per sample
 BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "render_fwd_kernel": 5072, "render_bwd_kernel": 2192,
-                    "dw_gemm_kernel": 4032}
+                    "dw_gemm_kernel": 3392}
 
 
 def pmc_traffic(kernel, a):

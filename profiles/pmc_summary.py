@@ -15,8 +15,8 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("render_fwd_kernel", "render_bwd_kernel", "hidden_bwd_kernel", "dw_gemm_kernel", "dw_reduce_kernel",
-           "pack_kernel", "adam_kernel")
+KERNELS = ("render_fwd_kernel", "render_bwd_kernel", "hidden_bwd_kernel", "dwstream_kernel", "dw_gemm_kernel",
+           "dw_reduce_kernel", "pack_kernel", "adam_kernel")
 
 
 def short(name):
@@ -105,7 +105,7 @@ def main(out_dir, tag):
             rows.append(r)
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
              "Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python bench.py --steps 5 --warmup 2 "
-             "--no-cpu-baseline --no-gemm-peak` (profiles/gpu_r02a.sh); 7 train steps + 3 phase-timing reps per kernel.", "",
+             "--no-cpu-baseline --no-gemm-peak` (profiles/gpu_r02a.sh, gpu_r02g.sh); 7 train steps + 3 phase-timing reps per kernel.", "",
              "| kernel | calls | avg ms | total % |", "|---|---|---|---|"]
     for r in rows[:20]:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | "
