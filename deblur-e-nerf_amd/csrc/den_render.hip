@@ -82,14 +82,28 @@ __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, 
 // intervals to drain before a wait covers them: with the whole chip writing 5 KB per sample, an HBM
 // store outlives one interval, and a 3-slot ring made every barrier wait for the previous step's
 // stores.
+#ifndef DEN_FWD_G
+#define DEN_FWD_G 2  // r02 A/B/A/B: 25.05 / 25.08 ms vs 25.28 / 25.46 ms for one tile per chunk
+#endif
 #ifndef DEN_FWD_RING
-#define DEN_FWD_RING 4
+#define DEN_FWD_RING (DEN_FWD_G == 2 ? 3 : 4)
 #endif
 #ifndef DEN_FWD_SETPRIO
 #define DEN_FWD_SETPRIO 0
 #endif
 constexpr int FWD_RING = DEN_FWD_RING;
 static_assert(FWD_RING == 3 || FWD_RING == 4, "forward weight ring: 3 or 4 slots");
+// row tiles per forward chunk (one barrier per chunk): G = 2 halves the barriers and DMA batches
+constexpr int FWD_G = DEN_FWD_G;
+static_assert(FWD_G == 1 || FWD_G == 2, "forward chunk: 1 or 2 row tiles");
+constexpr int FWD_SLOT = FWD_G * CHUNK_MAX;  // bytes per forward ring slot
+static_assert(FWD_RING * FWD_SLOT <= 128 * 1024, "forward ring exceeds the LDS budget");
+DEN_HD constexpr int fwd_nchunks_l(int mode, int l) { return (fwd_tiles(mode, l) + FWD_G - 1) / FWD_G; }
+DEN_HD constexpr int fwd_gchunk_index(int mode, int l) {
+  int c = 0;
+  for (int i = 0; i < l; ++i) c += fwd_nchunks_l(mode, i);
+  return c;
+}
 
 // Forward workgroup: 8 column blocks of TM samples (BF16: 256 samples) share one weight stream --
 // every workgroup streams the whole packed MLP (1.2 MB) through LDS, so samples per workgroup set
@@ -119,7 +133,7 @@ __device__ __forceinline__ int dma_ops(int bytes) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int n = 0;
 #pragma unroll
-  for (int q = 0; q < (CHUNK_MAX + NTH * 16 - 1) / (NTH * 16); ++q) n += (q * NTH * 16 + wave * 1024 < bytes) ? 1 : 0;
+  for (int q = 0; q < (FWD_SLOT + NTH * 16 - 1) / (NTH * 16); ++q) n += (q * NTH * 16 + wave * 1024 < bytes) ? 1 : 0;
   return n;
 }
 
@@ -127,7 +141,7 @@ template <int NTH>
 __device__ __forceinline__ void dma_chunk_untracked(const char* g, char* lds_slot, int bytes) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int q = 0; q < (CHUNK_MAX + NTH * 16 - 1) / (NTH * 16); ++q) {
+  for (int q = 0; q < (FWD_SLOT + NTH * 16 - 1) / (NTH * 16); ++q) {
     // wave-uniform offset (readfirstlane is 32-bit: never pass it a 64-bit pointer)
     const int off = __builtin_amdgcn_readfirstlane(q * NTH * 16 + wave * 1024);
     if (off < bytes) {
@@ -191,13 +205,13 @@ __device__ __forceinline__ void fwd_step(char* lds, const char* wbase, int t, in
   const uint64_t p0 = __builtin_amdgcn_s_memtime();
 #endif
   if (bytes_n > 0) {
-    dma_chunk_untracked<NTH>(wbase + off_n, lds + ((t + R - 1) % R) * LDS_BUF, bytes_n);
+    dma_chunk_untracked<NTH>(wbase + off_n, lds + ((t + R - 1) % R) * FWD_SLOT, bytes_n);
     // the DMA ops EVERY wave issues (some issue one more): an under-count, so the count stays a
     // compile-time constant and each wait an immediate
     vm.issued += bytes_n / (NTH * 16);
   }
   vm.mark[(t + R - 1) % R] = vm.issued;
-  body(lds + (t % R) * LDS_BUF);
+  body(lds + (t % R) * FWD_SLOT);
 #ifdef DEN_FWD_PROF
   const uint64_t p1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -217,16 +231,19 @@ __device__ __forceinline__ void fwd_step(char* lds, const char* wbase, int t, in
 #endif
 }
 
-// geometry of the forward chunk k after tile i of layer l (bytes 0 past the last one)
+// geometry of the forward chunk k after chunk c of layer l (bytes 0 past the last one): FWD_G
+// consecutive row tiles of one layer (fewer at a layer's end), contiguous in the packed layout
 template <int MODE>
-__device__ __forceinline__ void fwd_ahead(int l, int i, int k, int64_t* off, int* bytes) {
+__device__ __forceinline__ void fwd_ahead(int l, int c, int k, int64_t* off, int* bytes) {
 #pragma unroll
   for (int s = 0; s < k; ++s) {
-    if (++i >= fwd_tiles(MODE, l)) { ++l; i = 0; }
+    if (++c >= fwd_nchunks_l(MODE, l)) { ++l; c = 0; }
   }
   if (l >= NL) { *off = 0; *bytes = 0; return; }
-  *bytes = chunk_bytes_K(fwd_K(MODE, l));
-  *off = fwd_layer_offset(MODE, l) + (int64_t)i * *bytes;
+  const int tile = chunk_bytes_K(fwd_K(MODE, l));
+  const int left = fwd_tiles(MODE, l) - c * FWD_G;
+  *bytes = (left < FWD_G ? left : FWD_G) * tile;
+  *off = fwd_layer_offset(MODE, l) + (int64_t)c * FWD_G * tile;
 }
 
 template <int MODE, int LAST_J>
@@ -378,32 +395,47 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
   constexpr int NT = fwd_tiles(MODE, L);
   constexpr int CB = fwd_chunk_index(MODE, L);
   const int lane = threadIdx.x & 63, grp = lane / TM;
+  constexpr int NC = fwd_nchunks_l(MODE, L);
+  constexpr int GB = fwd_gchunk_index(MODE, L);
+  constexpr int TILE_BYTES = chunk_bytes_K(fwd_K(MODE, L));
   Acc prev[NB];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) {
+  for (int c = 0; c < NC; ++c) {
     auto body = [&](const char* chunk) {
-      Acc acc[NB];
-      const float* bias = (const float*)(lds + FWD_RING * LDS_BUF) + (CB + i) * TM + grp * T::REGS;
 #pragma unroll
-      for (int r = 0; r < T::REGS; ++r) acc[0][r] = bias[r];
+      for (int j = 0; j < FWD_G; ++j) {
+        const int i = c * FWD_G + j;
+        if (i < NT) {
+          const char* tile = chunk + j * TILE_BYTES;
+          Acc acc[NB];
+          const float* bias = (const float*)(lds + FWD_RING * FWD_SLOT) + (CB + i) * TM + grp * T::REGS;
 #pragma unroll
-      for (int b = 1; b < NB; ++b) acc[b] = acc[0];
-      mfma_chunk_nb<MODE, KS1, NB, S1>(chunk, x1, acc);
-      if constexpr (KS2 > 0) mfma_chunk_nb<MODE, KS2, NB, S2>(chunk + KS1 * TM * T::KI * es_of(MODE), x2, acc);
-      if (i > 0) fwd_epilogue<MODE, L, EPI, NB>(prev, i - 1, xo, out);
-      if (i >= 2) fwd_store<MODE, TRAIN, EPI, NB>(A, sample, i - 2, xo, outA);
+          for (int r = 0; r < T::REGS; ++r) acc[0][r] = bias[r];
 #pragma unroll
-      for (int b = 0; b < NB; ++b) prev[b] = acc[b];
-      if constexpr (MODE == 1) {
-        if (i > 0) fwd_interleave<KS1, KS2, NB, EPI == 0>();  // i is unrolled: one branch survives
-        else fwd_interleave<KS1, KS2, NB, false>();
+          for (int b = 1; b < NB; ++b) acc[b] = acc[0];
+          mfma_chunk_nb<MODE, KS1, NB, S1>(tile, x1, acc);
+          if constexpr (KS2 > 0) mfma_chunk_nb<MODE, KS2, NB, S2>(tile + KS1 * TM * T::KI * es_of(MODE), x2, acc);
+          if (i > 0) fwd_epilogue<MODE, L, EPI, NB>(prev, i - 1, xo, out);
+          if (i >= 2) fwd_store<MODE, TRAIN, EPI, NB>(A, sample, i - 2, xo, outA);
+#pragma unroll
+          for (int b = 0; b < NB; ++b) prev[b] = acc[b];
+          if constexpr (MODE == 1 && FWD_G == 1) {
+            if (i > 0) fwd_interleave<KS1, KS2, NB, EPI == 0>();  // i is unrolled: one branch survives
+            else fwd_interleave<KS1, KS2, NB, false>();
+          }
+        }
       }
     };
     int64_t noff;
     int nbytes;
-    fwd_ahead<MODE>(L, i, FWD_RING - 1, &noff, &nbytes);
-    fwd_step<fwd_threads(MODE)>(lds, A.w, CB + i, noff, nbytes,
-                                i >= 2 ? fwd_store_ops<MODE, TRAIN, EPI, NB>(i - 2) : 0, vm, body);
+    fwd_ahead<MODE>(L, c, FWD_RING - 1, &noff, &nbytes);
+    int n_st = 0;
+#pragma unroll
+    for (int j = 0; j < FWD_G; ++j) {
+      const int i = c * FWD_G + j;
+      if (i < NT && i >= 2) n_st += fwd_store_ops<MODE, TRAIN, EPI, NB>(i - 2);
+    }
+    fwd_step<fwd_threads(MODE)>(lds, A.w, GB + c, noff, nbytes, n_st, vm, body);
   }
   fwd_epilogue<MODE, L, EPI, NB>(prev, NT - 1, xo, out);
   if constexpr (NT >= 2) {
@@ -426,8 +458,8 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
   constexpr int WGS = fwd_wg_samples(MODE);
   constexpr int NTH = fwd_threads(MODE);
   constexpr int NBIAS = (int)bias_floats(MODE);
-  __shared__ __attribute__((aligned(16))) char lds[FWD_RING * LDS_BUF + NBIAS * 4 + WGS * 16];
-  float* bias_lds = (float*)(lds + FWD_RING * LDS_BUF);
+  __shared__ __attribute__((aligned(16))) char lds[FWD_RING * FWD_SLOT + NBIAS * 4 + WGS * 16];
+  float* bias_lds = (float*)(lds + FWD_RING * FWD_SLOT);
   float* rec_lds = bias_lds + NBIAS;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -446,7 +478,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
     int64_t off_c;
     int bytes_c;
     fwd_ahead<MODE>(0, 0, ch, &off_c, &bytes_c);
-    dma_chunk_untracked<NTH>(A.w + off_c, lds + ch * LDS_BUF, bytes_c);
+    dma_chunk_untracked<NTH>(A.w + off_c, lds + ch * FWD_SLOT, bytes_c);
   }
   FwdVm vm;
   vm.issued = 0;
