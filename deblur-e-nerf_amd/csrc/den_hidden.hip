@@ -31,6 +31,10 @@ constexpr int HB_GRID_MAX = 256;
 #ifndef DEN_HB_DEPTH
 #define DEN_HB_DEPTH 3
 #endif
+#ifndef DEN_HB_PF
+#define DEN_HB_PF 4  // dz_l fragments read ahead of the chain MFMAs
+#endif
+constexpr int HB_PF = DEN_HB_PF;
 constexpr int HB_DEPTH = DEN_HB_DEPTH;                   // blocks in flight ahead of the computed one
 constexpr int HB_RING = HB_DEPTH + 1;                    // LDS slots (32 KiB each; <= 5 fit in 160 KiB)
 constexpr int HB_DMA_OPS = 2 * (16 / 4);                 // LDS-DMA instructions per wave per block
@@ -135,16 +139,30 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const char* dzb = cur;
   const char* sb = cur + HB_BLOCK;
-  // chain: two row tiles, K = 256 (16 k-steps); then the activation derivative
+  // chain: both row tiles of this wave share each dz_l fragment (K = 256, 16 k-steps): one LDS read
+  // feeds two independent MFMAs, and the reads run HB_PF k-steps ahead of their use (issued
+  // one per k-step, the compiler waited out the LDS latency before every MFMA)
+  f32x16 accs[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accs[t][r] = 0.0f;
+  {
+    bf16x8 bq[HB_PF];
+#pragma unroll
+    for (int p = 0; p < HB_PF; ++p) bq[p] = hb_frag(dzb + (p >> 1) * HB_TILE, p & 1);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const bf16x8 cur = bq[k % HB_PF];
+      if (k + HB_PF < 16) bq[k % HB_PF] = hb_frag(dzb + ((k + HB_PF) >> 1) * HB_TILE, (k + HB_PF) & 1);
+      accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[0][k], cur, accs[0], 0, 0, 0);
+      accs[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[1][k], cur, accs[1], 0, 0, 0);
+    }
+  }
+  // then the activation derivative
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[t][k], hb_frag(dzb + (k >> 1) * HB_TILE, k & 1), acc, 0, 0,
-                                                     0);
+    f32x16 acc = accs[t];
     const char* st = sb + (2 * wave + t) * HB_TILE;
     const bf16x8 s0 = hb_frag(st, 0), s1 = hb_frag(st, 1);
 #pragma unroll

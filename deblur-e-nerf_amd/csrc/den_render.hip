@@ -363,7 +363,8 @@ __device__ __forceinline__ void mfma_chunk_nb(const char* lds_chunk, const typen
 template <int KS1, int KS2, int NB, bool EPI_VALU>
 __device__ __forceinline__ void fwd_interleave() {
 #if DEN_FWD_SCHED
-  constexpr int V = EPI_VALU ? (NB * 90 + KS1 + KS2 - 1) / (KS1 + KS2) : 1;
+  // DEN_FWD_SCHED 2: LDS reads and MFMAs only (the VALU epilogue left to the scheduler)
+  constexpr int V = DEN_FWD_SCHED == 2 ? 0 : EPI_VALU ? (NB * 90 + KS1 + KS2 - 1) / (KS1 + KS2) : 1;
   constexpr int PF1 = DEN_FWD_PF < KS1 ? DEN_FWD_PF : KS1;
   constexpr int PF2 = DEN_FWD_PF < KS2 ? DEN_FWD_PF : KS2;
   __builtin_amdgcn_sched_group_barrier(0x100, 4 + PF1, 0);  // DS read: bias (4) + first fragments
@@ -371,7 +372,7 @@ __device__ __forceinline__ void fwd_interleave() {
   for (int k = 0; k < KS1; ++k) {
     __builtin_amdgcn_sched_group_barrier(0x008, NB, 0);     // MFMA
     if (k + PF1 < KS1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, V, 0);      // VALU
+    if (V > 0) __builtin_amdgcn_sched_group_barrier(0x002, V, 0);  // VALU
   }
   if constexpr (KS2 > 0) {
     __builtin_amdgcn_sched_group_barrier(0x100, PF2, 0);
@@ -379,7 +380,7 @@ __device__ __forceinline__ void fwd_interleave() {
     for (int k = 0; k < KS2; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, NB, 0);
       if (k + PF2 < KS2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+      if (V > 0) __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
     }
   }
 #endif
@@ -419,7 +420,7 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
           if (i >= 2) fwd_store<MODE, TRAIN, EPI, NB>(A, sample, i - 2, xo, outA);
 #pragma unroll
           for (int b = 0; b < NB; ++b) prev[b] = acc[b];
-          if constexpr (MODE == 1 && FWD_G == 1) {
+          if constexpr (MODE == 1) {
             if (i > 0) fwd_interleave<KS1, KS2, NB, EPI == 0>();  // i is unrolled: one branch survives
             else fwd_interleave<KS1, KS2, NB, false>();
           }
