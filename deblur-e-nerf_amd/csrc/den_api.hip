@@ -216,7 +216,7 @@ int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, 
   const int64_t per = (int64_t)MT * (R.NT + 1) * 1024;
   {
     DEN_TIMED(T_DW_REDUCE, s);
-    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + DWR_EL - 1) / DWR_EL)), dim3(DWR_THREADS), 0, s, R);
   }
   DEN_LAUNCHED();
   return DEN_OK;
@@ -270,7 +270,7 @@ int launch_dwstream_reduce(const den_render_desc* d, const WsLayout& L, char* ws
   const int64_t per = (int64_t)MT * (NT_ALL + 1) * 1024;
   {
     DEN_TIMED(T_DW_REDUCE, s);
-    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + DWR_EL - 1) / DWR_EL)), dim3(DWR_THREADS), 0, s, R);
   }
   DEN_LAUNCHED();
   return DEN_OK;
@@ -310,7 +310,7 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   const int64_t per = 8LL * 9 * 1024;
   {
     DEN_TIMED(T_DW_REDUCE, s);
-    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, R);
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + DWR_EL - 1) / DWR_EL)), dim3(DWR_THREADS), 0, s, R);
   }
   DEN_LAUNCHED();
   return DEN_OK;
@@ -384,7 +384,7 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
     if ((rc = launch_dwstream<1, 1, 4, 4, 4, 6>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 1, 4, 0, 1, L_R, 128, 0, 1, G, s)) != DEN_OK) return rc;
     if (g->grad_bkgd) {
-      hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(256), 0, s, d->radiance_dim, d->n_rays,
+      hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(1024), 0, s, d->radiance_dim, d->n_rays,
                          (const float*)(ws + L.bkgd_partial), g->grad_bkgd);
       DEN_LAUNCHED();
     }
@@ -412,7 +412,7 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
   // rgb output (M = 32): 4 waves split the 4 column tiles
   if ((rc = launch_dw<MODE, 1, 128, 0, 4>(d, L, ws, L_R, D_ZR, A_G, -1, 0, G, s)) != DEN_OK) return rc;
   if (g->grad_bkgd) {
-    hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(256), 0, s, d->radiance_dim, d->n_rays,
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(1024), 0, s, d->radiance_dim, d->n_rays,
                        (const float*)(ws + L.bkgd_partial), g->grad_bkgd);
     DEN_LAUNCHED();
   }

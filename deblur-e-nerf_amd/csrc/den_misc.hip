@@ -111,15 +111,27 @@ __global__ void adam_kernel(int64_t n, T* p, const T* g, T* m, T* v, T step_size
 }
 
 // ------------------------------------------------------------------ partial sums
-__global__ void sum_partials_kernel(int n, int nb, const float* part, float* out) {
+// out[j] = sum_b part[j * nb + b], one workgroup per j (any blockDim.x <= 1024, a multiple of 64):
+// 8 loads in flight per lane, then a fixed-order tree -- deterministic for a given launch shape.
+__global__ __launch_bounds__(1024) void sum_partials_kernel(int n, int nb, const float* part, float* out) {
   const int j = blockIdx.x;
   if (j >= n) return;
-  float s = 0.0f;
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) s += part[(int64_t)j * nb + b];
-  __shared__ float red[256];
+  const float* p = part + (int64_t)j * nb;
+  const int T = blockDim.x;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int b = threadIdx.x;
+  for (; b + 7 * T < nb; b += 8 * T) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += p[b + u * T];
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (b + u * T < nb) a[u] += p[b + u * T];
+  float s = ((a[0] + a[4]) + (a[1] + a[5])) + ((a[2] + a[6]) + (a[3] + a[7]));
+  __shared__ float red[1024];
   red[threadIdx.x] = s;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = T / 2; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }

@@ -319,6 +319,21 @@ __device__ __forceinline__ constexpr int fwd_store_ops(int i) {
   return 0;
 }
 
+// The last row tile's epilogue of layer L and the stores of its last two tiles.
+template <int MODE, bool TRAIN, int L, int EPI, int NB, typename Frag, typename Acc>
+__device__ __forceinline__ void fwd_layer_tail(const RenderArgs<MODE>& A, const int64_t* sample, Acc* last, Frag* xo,
+                                               int outA, FwdOut* out) {
+  constexpr int NT = fwd_tiles(MODE, L);
+  fwd_epilogue<MODE, L, EPI, NB>(last, NT - 1, xo, out);
+  if constexpr (NT >= 2) fwd_store<MODE, TRAIN, EPI, NB>(A, sample, NT - 2, xo, outA);
+  fwd_store<MODE, TRAIN, EPI, NB>(A, sample, NT - 1, xo, outA);
+}
+template <int MODE, bool TRAIN, int L, int EPI, int NB>
+__device__ __forceinline__ constexpr int fwd_tail_store_ops() {
+  constexpr int NT = fwd_tiles(MODE, L);
+  return (NT >= 2 ? fwd_store_ops<MODE, TRAIN, EPI, NB>(NT - 2) : 0) + fwd_store_ops<MODE, TRAIN, EPI, NB>(NT - 1);
+}
+
 // acc[b] += W_chunk x[b * S + 0 .. KS), b < NB: one LDS read of each weight fragment per NB MFMAs.
 // BF16: the weight fragments are read FWD_PF k-steps ahead into a register ring (left alone, the
 // compiler issues each read right before its MFMAs and waits out the LDS latency every k-step).
@@ -328,26 +343,29 @@ __device__ __forceinline__ constexpr int fwd_store_ops(int i) {
 #ifndef DEN_FWD_SCHED
 #define DEN_FWD_SCHED 0  // r02 A/B: pinned schedule 25.8 ms vs 24.9 ms for the compiler's order (NB = 1)
 #endif
-template <int MODE, int KS, int NB, int S>
+template <int MODE, int K0, int K1, int NB, int S>
 __device__ __forceinline__ void mfma_chunk_nb(const char* lds_chunk, const typename Tr<MODE>::Frag* x,
                                               typename Tr<MODE>::Acc* acc) {
   const int lane = threadIdx.x & 63;
-  if constexpr (MODE == 1) {
+  constexpr int KS = K1 - K0;
+  if constexpr (KS <= 0) {
+    return;
+  } else if constexpr (MODE == 1) {
     constexpr int PF = DEN_FWD_PF < KS ? DEN_FWD_PF : KS;
     bf16x8 a[PF];
 #pragma unroll
-    for (int p = 0; p < PF; ++p) a[p] = *(const bf16x8*)(lds_chunk + p * 1024 + lane * 16);
+    for (int p = 0; p < PF; ++p) a[p] = *(const bf16x8*)(lds_chunk + (K0 + p) * 1024 + lane * 16);
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
       const bf16x8 cur = a[k % PF];
-      if (k + PF < KS) a[k % PF] = *(const bf16x8*)(lds_chunk + (k + PF) * 1024 + lane * 16);
+      if (k + PF < KS) a[k % PF] = *(const bf16x8*)(lds_chunk + (K0 + k + PF) * 1024 + lane * 16);
 #pragma unroll
-      for (int b = 0; b < NB; ++b) acc[b] = Tr<1>::mfma(cur, x[b * S + k], acc[b]);
+      for (int b = 0; b < NB; ++b) acc[b] = Tr<1>::mfma(cur, x[b * S + K0 + k], acc[b]);
     }
   } else {
-    static_assert(KS % 4 == 0, "f32 k-steps come in groups of 4");
+    static_assert(K0 % 4 == 0 && K1 % 4 == 0, "f32 k-steps come in groups of 4");
 #pragma unroll
-    for (int k4 = 0; k4 < KS / 4; ++k4) {
+    for (int k4 = K0 / 4; k4 < K1 / 4; ++k4) {
       const f32x4 a = *(const f32x4*)(lds_chunk + k4 * 1024 + lane * 16);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -386,19 +404,30 @@ __device__ __forceinline__ void fwd_interleave() {
 #endif
 }
 
-template <int MODE, bool TRAIN, int L, int KS1, int S1, int KS2, int S2, int EPI, int NB, typename Frag>
+// Layer transitions: the epilogue of a layer's last row tile (and its last two tile stores) does not
+// run on its own between two layers -- every wave would then be in VALU at once, the MFMAs idle.
+// With DEFER the layer leaves its last accumulators in `tail`; the next layer runs them (`pend`,
+// PEND_ST stores) inside the body of its first tile, between the MFMAs that do not read the last
+// input tile (k-steps [0, KS1 - FPT)) and the FPT that do.
+struct NoPend {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+template <int MODE, bool TRAIN, int L, int KS1, int S1, int KS2, int S2, int EPI, int NB, bool DEFER, int PEND_ST,
+          typename Frag, typename Acc, typename Pend>
 __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, const int64_t* sample,
                                           const Frag* x1, const Frag* x2, Frag* xo, int outA, FwdOut* out,
-                                          FwdVm& vm) {
+                                          FwdVm& vm, Pend&& pend, Acc* tail) {
   using T = Tr<MODE>;
-  using Acc = typename T::Acc;
-  constexpr int TM = T::TM;
+  constexpr int TM = T::TM, FPT = T::FPT;
   constexpr int NT = fwd_tiles(MODE, L);
   constexpr int CB = fwd_chunk_index(MODE, L);
   const int lane = threadIdx.x & 63, grp = lane / TM;
   constexpr int NC = fwd_nchunks_l(MODE, L);
   constexpr int GB = fwd_gchunk_index(MODE, L);
   constexpr int TILE_BYTES = chunk_bytes_K(fwd_K(MODE, L));
+  constexpr int KSPLIT = PEND_ST >= 0 ? KS1 - FPT : KS1;  // PEND_ST < 0: no pending epilogue
+  static_assert(KSPLIT >= 0, "pending epilogue split");
   Acc prev[NB];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -414,8 +443,15 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
           for (int r = 0; r < T::REGS; ++r) acc[0][r] = bias[r];
 #pragma unroll
           for (int b = 1; b < NB; ++b) acc[b] = acc[0];
-          mfma_chunk_nb<MODE, KS1, NB, S1>(tile, x1, acc);
-          if constexpr (KS2 > 0) mfma_chunk_nb<MODE, KS2, NB, S2>(tile + KS1 * TM * T::KI * es_of(MODE), x2, acc);
+          if (i == 0 && PEND_ST >= 0) {
+            mfma_chunk_nb<MODE, 0, KSPLIT, NB, S1>(tile, x1, acc);
+            pend();
+            mfma_chunk_nb<MODE, KSPLIT, KS1, NB, S1>(tile, x1, acc);
+          } else {
+            mfma_chunk_nb<MODE, 0, KS1, NB, S1>(tile, x1, acc);
+          }
+          if constexpr (KS2 > 0)
+            mfma_chunk_nb<MODE, 0, KS2, NB, S2>(tile + KS1 * TM * T::KI * es_of(MODE), x2, acc);
           if (i > 0) fwd_epilogue<MODE, L, EPI, NB>(prev, i - 1, xo, out);
           if (i >= 2) fwd_store<MODE, TRAIN, EPI, NB>(A, sample, i - 2, xo, outA);
 #pragma unroll
@@ -430,7 +466,7 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
     int64_t noff;
     int nbytes;
     fwd_ahead<MODE>(L, c, FWD_RING - 1, &noff, &nbytes);
-    int n_st = 0;
+    int n_st = (c == 0 && PEND_ST > 0) ? PEND_ST : 0;
 #pragma unroll
     for (int j = 0; j < FWD_G; ++j) {
       const int i = c * FWD_G + j;
@@ -438,13 +474,13 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
     }
     fwd_step<fwd_threads(MODE)>(lds, A.w, GB + c, noff, nbytes, n_st, vm, body);
   }
-  fwd_epilogue<MODE, L, EPI, NB>(prev, NT - 1, xo, out);
-  if constexpr (NT >= 2) {
-    fwd_store<MODE, TRAIN, EPI, NB>(A, sample, NT - 2, xo, outA);
-    vm.issued += fwd_store_ops<MODE, TRAIN, EPI, NB>(NT - 2);
+  if constexpr (DEFER) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) tail[b] = prev[b];
+  } else {
+    fwd_layer_tail<MODE, TRAIN, L, EPI, NB>(A, sample, prev, xo, outA, out);
+    vm.issued += fwd_tail_store_ops<MODE, TRAIN, L, EPI, NB>();
   }
-  fwd_store<MODE, TRAIN, EPI, NB>(A, sample, NT - 1, xo, outA);
-  vm.issued += fwd_store_ops<MODE, TRAIN, EPI, NB>(NT - 1);
 }
 
 // ------------------------------------------------------------------ forward kernel
@@ -542,15 +578,29 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
   constexpr int KS = WIDTH / T::KI;  // k-steps of a 256-wide input
   Frag xa[NB * KS], xb[NB * KS];
   FwdOut out[NB];
-  fwd_layer<MODE, TRAIN, 0, PE_S, PE_S, 0, 0, 0, NB>(A, lds, sample, pe, pe, xa, A_S0 + 0, out, vm);
-  fwd_layer<MODE, TRAIN, 1, KS, KS, 0, 0, 0, NB>(A, lds, sample, xa, xa, xb, A_S0 + 1, out, vm);
-  fwd_layer<MODE, TRAIN, 2, KS, KS, 0, 0, 0, NB>(A, lds, sample, xb, xb, xa, A_S0 + 2, out, vm);
-  fwd_layer<MODE, TRAIN, 3, KS, KS, 0, 0, 0, NB>(A, lds, sample, xa, xa, xb, A_S0 + 3, out, vm);
-  fwd_layer<MODE, TRAIN, 4, KS, KS, 0, 0, 0, NB>(A, lds, sample, xb, xb, xa, A_S0 + 4, out, vm);
-  fwd_layer<MODE, TRAIN, 5, KS, KS, PE_S, PE_S, 0, NB>(A, lds, sample, xa, pe, xb, A_S0 + 5, out, vm);
-  fwd_layer<MODE, TRAIN, 6, KS, KS, 0, 0, 0, NB>(A, lds, sample, xb, xb, xa, A_S0 + 6, out, vm);
-  fwd_layer<MODE, TRAIN, 7, KS, KS, 0, 0, 0, NB>(A, lds, sample, xa, xa, xb, A_S0 + 7, out, vm);
-  fwd_layer<MODE, TRAIN, L_B, KS, KS, 0, 0, 1, NB>(A, lds, sample, xb, xb, xa, 0, out, vm);  // xa <- bottleneck
+  Acc tl[NB];  // last row tile of the previous layer, finished inside the next one (fwd_layer DEFER)
+  // the previous layer's tail, run by the next layer inside its first tile (xo: where it writes)
+#define DEN_PEND(LP, EPIP, XO, OUTA) \
+  [&]() { fwd_layer_tail<MODE, TRAIN, LP, EPIP, NB>(A, sample, tl, XO, OUTA, out); }
+#define DEN_PST(LP, EPIP) fwd_tail_store_ops<MODE, TRAIN, LP, EPIP, NB>()
+  fwd_layer<MODE, TRAIN, 0, PE_S, PE_S, 0, 0, 0, NB, true, -1>(A, lds, sample, pe, pe, xa, A_S0 + 0, out, vm, NoPend{}, tl);
+  fwd_layer<MODE, TRAIN, 1, KS, KS, 0, 0, 0, NB, true, DEN_PST(0, 0)>(A, lds, sample, xa, xa, xb, A_S0 + 1, out, vm,
+                                                                      DEN_PEND(0, 0, xa, A_S0 + 0), tl);
+  fwd_layer<MODE, TRAIN, 2, KS, KS, 0, 0, 0, NB, true, DEN_PST(1, 0)>(A, lds, sample, xb, xb, xa, A_S0 + 2, out, vm,
+                                                                      DEN_PEND(1, 0, xb, A_S0 + 1), tl);
+  fwd_layer<MODE, TRAIN, 3, KS, KS, 0, 0, 0, NB, true, DEN_PST(2, 0)>(A, lds, sample, xa, xa, xb, A_S0 + 3, out, vm,
+                                                                      DEN_PEND(2, 0, xa, A_S0 + 2), tl);
+  fwd_layer<MODE, TRAIN, 4, KS, KS, 0, 0, 0, NB, true, DEN_PST(3, 0)>(A, lds, sample, xb, xb, xa, A_S0 + 4, out, vm,
+                                                                      DEN_PEND(3, 0, xb, A_S0 + 3), tl);
+  fwd_layer<MODE, TRAIN, 5, KS, KS, PE_S, PE_S, 0, NB, true, DEN_PST(4, 0)>(A, lds, sample, xa, pe, xb, A_S0 + 5, out,
+                                                                            vm, DEN_PEND(4, 0, xa, A_S0 + 4), tl);
+  fwd_layer<MODE, TRAIN, 6, KS, KS, 0, 0, 0, NB, true, DEN_PST(5, 0)>(A, lds, sample, xb, xb, xa, A_S0 + 6, out, vm,
+                                                                      DEN_PEND(5, 0, xb, A_S0 + 5), tl);
+  fwd_layer<MODE, TRAIN, 7, KS, KS, 0, 0, 0, NB, true, DEN_PST(6, 0)>(A, lds, sample, xa, xa, xb, A_S0 + 7, out, vm,
+                                                                      DEN_PEND(6, 0, xa, A_S0 + 6), tl);
+  // xa <- bottleneck; its tail (the sigma row tile) runs inside L_G
+  fwd_layer<MODE, TRAIN, L_B, KS, KS, 0, 0, 1, NB, true, DEN_PST(7, 0)>(A, lds, sample, xb, xb, xa, 0, out, vm,
+                                                                        DEN_PEND(7, 0, xb, A_S0 + 7), tl);
 
   // view-direction encoding (mlp.py:353-355): condition * pi, degree 4
   constexpr int VE_T = VE_PAD / TM, VE_S = VE_T * FPT;
@@ -573,8 +623,12 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
       acc_to_frags<MODE>(a, ve + b * VE_S + p * FPT);
     }
   }
-  fwd_layer<MODE, TRAIN, L_G, KS, KS, VE_S, VE_S, 0, NB>(A, lds, sample, xa, ve, xb, A_G, out, vm);
-  fwd_layer<MODE, TRAIN, L_R, WIDTH_COND / T::KI, KS, 0, 0, 2, NB>(A, lds, sample, xb, xb, xa, 0, out, vm);
+  fwd_layer<MODE, TRAIN, L_G, KS, KS, VE_S, VE_S, 0, NB, true, DEN_PST(L_B, 1)>(A, lds, sample, xa, ve, xb, A_G, out,
+                                                                                vm, DEN_PEND(L_B, 1, xa, 0), tl);
+  fwd_layer<MODE, TRAIN, L_R, WIDTH_COND / T::KI, KS, 0, 0, 2, NB, false, DEN_PST(L_G, 0)>(
+      A, lds, sample, xb, xb, xa, 0, out, vm, DEN_PEND(L_G, 0, xb, A_G), tl);
+#undef DEN_PEND
+#undef DEN_PST
 
 #ifdef DEN_FWD_PROF
   vm.prof[3] = __builtin_amdgcn_s_memtime() - vm.prof[3];
