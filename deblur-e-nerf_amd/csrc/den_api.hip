@@ -374,14 +374,15 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
 #if DEN_DW_STREAM
   if (hidden) {
     // streamed, operand-sharing weight gradients (den_dwstream.hip)
-    if ((rc = launch_dwstream<8, 16, 2, 2, 4, 3>(d, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<8, 16, 2, 2, DEN_DWS_NW1, 3>(d, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK)
+      return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream<9, 9, 8, 8, 8, 3>(d, L, ws, D_ZB, -1, A_S0 + 7, -1, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<9, 9, 8, 8, DEN_DWS_NW2, 3>(d, L, ws, D_ZB, -1, A_S0 + 7, -1, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 9, 8, 0, 9, L_B, 256, 0, 1, G, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream<4, 4, 8, 9, 4, 4>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<4, 4, 8, 9, DEN_DWS_NW3, 4>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 4, 9, 0, 4, L_G, 256, WIDTH, 1, G, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream<1, 1, 4, 4, 4, 6>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 1, 4, 0, 1, L_R, 128, 0, 1, G, s)) != DEN_OK) return rc;
     if (g->grad_bkgd) {
       hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(1024), 0, s, d->radiance_dim, d->n_rays,

@@ -18,6 +18,23 @@
 // bottleneck_layer, rgb_layer.* (external/mlp.py:99-113, 193-205).
 // Included by den_api.hip after den_hidden.hip (hb_slot, hb_tr_frag, hb_wait_vm_lgkm0, HB_TILE).
 
+// waves per workgroup of the streamed weight-gradient launches {L0 + L5 pe}, Lg, Lr
+#ifndef DEN_DWS_NW1
+#define DEN_DWS_NW1 16  // r02 A/B: streamed dW 13.0-13.35 ms per step (4 waves), 11.2 (8), 10.8 (16, with NW3)
+#endif
+#ifndef DEN_DWS_NW2
+#define DEN_DWS_NW2 8
+#endif
+#ifndef DEN_DWS_NW3
+#define DEN_DWS_NW3 16
+#endif
+#ifndef DEN_DWS_NW4
+#define DEN_DWS_NW4 4
+#endif
+#ifndef DEN_DWS_D4
+#define DEN_DWS_D4 6  // blocks in flight of the Lr launch (10 KiB each)
+#endif
+
 namespace den {
 
 struct DwStreamArgs {
@@ -157,9 +174,9 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
 }
 
 // the four launches of a BF16 backward
-template __global__ void dwstream_kernel<8, 16, 2, 2, 4, 3>(DwStreamArgs);   // L0 + L5 pe
-template __global__ void dwstream_kernel<9, 9, 8, 8, 8, 3>(DwStreamArgs);    // Lb + sigma
-template __global__ void dwstream_kernel<4, 4, 8, 9, 4, 4>(DwStreamArgs);    // Lg
-template __global__ void dwstream_kernel<1, 1, 4, 4, 4, 6>(DwStreamArgs);    // Lr
+template __global__ void dwstream_kernel<8, 16, 2, 2, DEN_DWS_NW1, 3>(DwStreamArgs);  // L0 + L5 pe
+template __global__ void dwstream_kernel<9, 9, 8, 8, DEN_DWS_NW2, 3>(DwStreamArgs);    // Lb + sigma
+template __global__ void dwstream_kernel<4, 4, 8, 9, DEN_DWS_NW3, 4>(DwStreamArgs);    // Lg
+template __global__ void dwstream_kernel<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4>(DwStreamArgs);  // Lr
 
 }  // namespace den
