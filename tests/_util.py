@@ -45,3 +45,38 @@ def norm_rel(a, b):
     a = torch.as_tensor(a).detach().cpu().double()
     b = torch.as_tensor(b).detach().cpu().double()
     return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+# ----------------------------------------------------------------------------- ngp fixtures
+NGP_CTYPE = {"aabb": 0, "tanh": 1, "sphere": 2}
+
+
+def ngp_fixture(z):
+    """(params {name: tensor}, pos_encoding cfg, base cfg, head cfg, rd, ctype) of a
+    tests/golden/ngp_*.npz fixture; the default-size hash table is regenerated from the seed
+    (oracle/ngp.build_params, x 1e3 as make_golden.gen_ngp) and checked against its stored sum."""
+    import json
+    from oracle import ngp as ongp
+    pos = json.loads(str(z["pos_encoding"]))
+    rd = int(z["rd"])
+    if "table" in z.files:
+        table = torch.from_numpy(z["table"])
+    else:
+        table = ongp.build_params(rd, int(z["seed"]), pos)["mlp_base.0.params"] * 1e3
+        assert abs(table.double().sum().item() - float(z["table_sum"])) <= 1e-6 * max(1.0, abs(float(z["table_sum"])))
+    p = {"mlp_base.0.params": table}
+    for k in z.files:
+        if k.startswith("param:"):
+            p[k[len("param:"):]] = torch.from_numpy(z[k])
+    base = dict(ongp.MLP_BASE, hidden_activation=str(z["hidden"]))
+    head = dict(ongp.MLP_HEAD, hidden_activation=str(z["hidden"]), radiance_activation=str(z["radiance"]))
+    return p, pos, base, head, rd, NGP_CTYPE[str(z["contraction"])]
+
+
+def ngp_table_grad(z, n):
+    """The fixture's hash-table gradient as a dense (n,) tensor."""
+    if "grad:mlp_base.0.params" in z.files:
+        return torch.from_numpy(z["grad:mlp_base.0.params"])
+    g = torch.zeros(n)
+    g[torch.from_numpy(z["table_grad_idx"]).long()] = torch.from_numpy(z["table_grad_val"])
+    return g

@@ -35,6 +35,7 @@ enum/tinycudann).  What each fixture pins:
                            ray origin / unit direction), with and without the
                            leading render-group dimension.
 """
+import json
 import os
 import sys
 import tempfile
@@ -709,6 +710,81 @@ def gen_mlp_unbounded():
     gen_mlp(1, seed=3, contraction="tanh")
 
 
+# ----------------------------------------------------------------------------
+NGP_SMALL = dict(otype="HashGrid", n_levels=8, n_features_per_level=2, log2_hashmap_size=12, base_resolution=16,
+                 per_level_scale=1.4472692012786865, interpolation="Linear")
+
+
+def gen_ngp(rd=1, seed=21, cfg="small", contraction="aabb", hidden="softplus", radiance="softplus", n=512):
+    """ngp_*.npz -- the reference's NGPradianceField (external/ngp.py:109-280: contraction, the
+    mlp_base / mlp_head MLPs of external/mlp.py, SHEncoder, shifted_trunc_exp, the configured
+    activations of models/nerf.py:17-29) forward + backward, with oracle/tcnn.py standing in for
+    tcnn.Encoding (tiny-cuda-nn is absent: the grid encoding itself is parity unpinned).
+    cfg "small": 8 levels of 2^12 entries (dense level 0, hashed levels 1..7; the table and its
+    whole gradient are stored); cfg "default": configs/train/synthetic.yaml's 16 levels of 2^19
+    (the table is regenerated from the seed by oracle/ngp.build_params, the fixture keeps its
+    f64 sum and the gradient's nonzero entries)."""
+    sys.path.insert(0, os.path.join(HERE, "..", ".."))
+    from oracle import ngp as ongp
+    from oracle import tcnn as otcnn
+    ngp = _refload.load("external.ngp")
+    sys.modules["tinycudann"].Encoding = otcnn.Encoding
+    ContractionType = sys.modules["nerfacc"].ContractionType
+    ctype = {"aabb": ContractionType.AABB, "sphere": ContractionType.UN_BOUNDED_SPHERE,
+             "tanh": ContractionType.UN_BOUNDED_TANH}[contraction]
+    pos = dict(NGP_SMALL) if cfg == "small" else dict(ongp.POS_ENCODING)
+    act = {"softplus": torch.nn.Softplus(beta=100), "relu": torch.nn.ReLU()}
+    ract = {"softplus": torch.nn.Softplus(beta=1), "sigmoid": torch.nn.Sigmoid()}
+    base = dict(ongp.MLP_BASE, hidden_activation=act[hidden], density_activation=ngp.shifted_trunc_exp)
+    head = dict(ongp.MLP_HEAD, hidden_activation=act[hidden], radiance_activation=ract[radiance], output_dim=rd)
+    aabb = [-1.5, -1.5, -1.5, 1.5, 1.5, 1.5]
+    field = ngp.NGPradianceField(aabb=aabb, num_dim=3, use_viewdirs=True, contraction_type=ctype,
+                                 pos_encoding_config=pos, dir_encoding_config={"degree": 4},
+                                 mlp_base_config=base, mlp_head_config=head)
+    p = ongp.build_params(rd, seed, pos)
+    # a larger table scale than tcnn's 1e-4 init so the encoding dominates the MLP inputs
+    p["mlp_base.0.params"] = p["mlp_base.0.params"] * 1e3
+    names = [k for k, _ in field.named_parameters()]
+    assert set(names) == set(p), (names, list(p))
+    field.load_state_dict(dict(p, aabb=field.aabb), strict=True)
+    g = torch.Generator().manual_seed(2000 + seed)
+    span = 1.8 if contraction == "aabb" else 6.0
+    x = (torch.rand(n, 3, generator=g) * 2 * span - span).float()
+    d = torch.randn(n, 3, generator=g)
+    d = d / d.norm(dim=-1, keepdim=True)
+    g_rgb = torch.randn(n, rd, generator=g)
+    g_sig = torch.randn(n, 1, generator=g)
+    field.zero_grad()
+    rgb, sig = field(x, d)
+    (rgb * g_rgb).sum().add_((sig * g_sig).sum()).backward()
+    out = dict(rgb=rgb.detach().numpy(), sigma=sig.detach().numpy())
+    for k, prm in field.named_parameters():
+        gr = prm.grad.detach()
+        if k == "mlp_base.0.params" and cfg != "small":
+            nz = torch.nonzero(gr).flatten()
+            out["table_grad_idx"] = nz.numpy()
+            out["table_grad_val"] = gr[nz].numpy()
+        else:
+            out[f"grad:{k}"] = gr.numpy()
+    # the default-size table is regenerated in the test from the seed (oracle/ngp.build_params x 1e3)
+    extra = dict(table=p["mlp_base.0.params"].numpy()) if cfg == "small" else {}
+    mlp_w = {f"param:{k}": v.numpy() for k, v in p.items() if k != "mlp_base.0.params"}
+    tag = f"ngp_rd{rd}_{cfg}" + ("" if contraction == "aabb" else f"_{contraction}") + \
+        ("" if hidden == "softplus" and radiance == "softplus" else f"_{hidden}_{radiance}")
+    save(tag + ".npz", seed=seed, rd=rd, cfg=np.array(cfg), contraction=np.array(contraction),
+         hidden=np.array(hidden), radiance=np.array(radiance), pos_encoding=np.array(json.dumps(pos)),
+         table_sum=np.array(p["mlp_base.0.params"].double().sum().item()), aabb=np.array(aabb, np.float32),
+         x=x.numpy(), d=d.numpy(), g_rgb=g_rgb.numpy(), g_sigma=g_sig.numpy(), param_names=np.array(names),
+         **out, **extra, **mlp_w)
+
+
+def gen_ngp_all():
+    gen_ngp(1, 21, "small")
+    gen_ngp(3, 22, "small", "sphere", "relu", "sigmoid")
+    gen_ngp(3, 23, "small", "tanh")
+    gen_ngp(3, 24, "default", n=256)
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.set_num_threads(8)
     for name in sys.argv[1:]:
@@ -731,3 +807,4 @@ elif __name__ == "__main__":
     gen_traj()
     gen_step(False, 1)
     gen_step(True, 1)
+    gen_ngp_all()

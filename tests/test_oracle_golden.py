@@ -217,3 +217,42 @@ def test_pixel_rays_match_reference(golden_dir):
     o1, d1 = oev.pixel_params_to_ray(K, px, pos[0], rot[0])
     assert rel_err(d1, z["ray_direction_1"]) < 1e-7
     assert np.allclose(np.linalg.norm(z["ray_direction"], axis=-1), 1.0, atol=1e-6)
+
+
+# --------------------------------------------------------------------------- ngp radiance field
+NGP_FIXTURES = ["ngp_rd1_small", "ngp_rd3_small_sphere_relu_sigmoid", "ngp_rd3_small_tanh", "ngp_rd3_default"]
+
+
+@pytest.mark.parametrize("fixture", NGP_FIXTURES)
+def test_ngp_field_matches_reference(golden_dir, fixture):
+    """oracle/ngp.py (contraction, SH, MLPs, activations around oracle/tcnn.py) against the
+    reference's NGPradianceField run with the same encoding: outputs 1e-6, gradients 1e-5."""
+    from _util import ngp_fixture, ngp_table_grad
+    from oracle import ngp as ongp
+    z = _load(golden_dir, fixture + ".npz")
+    p, pos, base, head, rd, ctype = ngp_fixture(z)
+    for k in p:
+        p[k].requires_grad_(True)
+    rgb, sig = ongp.field(p, torch.from_numpy(z["x"]), torch.from_numpy(z["d"]), rd, torch.from_numpy(z["aabb"]),
+                          ctype, pos, base, head)
+    assert rel_err(rgb.detach(), z["rgb"]) < 1e-6 and rel_err(sig.detach(), z["sigma"]) < 1e-6
+    ((rgb * torch.from_numpy(z["g_rgb"])).sum() + (sig * torch.from_numpy(z["g_sigma"])).sum()).backward()
+    for k, v in p.items():
+        ref = ngp_table_grad(z, v.numel()) if k == "mlp_base.0.params" else torch.from_numpy(z[f"grad:{k}"])
+        e = (v.grad - ref).abs().max().item() / max(ref.abs().max().item(), 1e-12)
+        assert e < 1e-5, (k, e)
+
+
+def test_tcnn_grid_levels_follow_tcnn_sizing():
+    """synthetic.yaml's HashGrid: level 0..4 dense (res 16, 24, 34, 49, 71 -> entries rounded to 8),
+    levels 5..15 hashed at 2^19: 6,299,960 entries x 2 = 12,599,920 parameters."""
+    from oracle import ngp as ongp
+    from oracle import tcnn as otcnn
+    c = ongp.POS_ENCODING
+    levels, total = otcnn.grid_levels(c["n_levels"], c["log2_hashmap_size"], c["base_resolution"],
+                                      c["per_level_scale"])
+    res = [r for _, r, _, _ in levels]
+    assert res[:5] == [16, 24, 34, 49, 71]
+    assert [e for _, _, e, _ in levels[:5]] == [4096, 13824, 39304, 117656, 357912]
+    assert all(e == 1 << 19 for _, _, e, _ in levels[5:])
+    assert total * 2 == otcnn.n_params(c) == 12599920
