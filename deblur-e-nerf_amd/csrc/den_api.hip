@@ -18,6 +18,7 @@
 #include "den_dwstream.hip"
 #include "den_march.hip"
 #include "den_misc.hip"
+#include "den_ngp.hip"
 #include "den_pixbw.hip"
 #include "den_render.hip"
 
@@ -1096,6 +1097,204 @@ int den_image_error(int32_t n_img, int64_t pixels, const float* pred, const floa
   DEN_LAUNCHED();
   hipLaunchKernelGGL(sum_partials_f64_kernel, dim3(2 * n_img), dim3(256), 0, st, 2 * n_img, IMG_SLICES,
                      (const double*)workspace, sse_sae);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- ngp radiance field
+namespace {
+// tcnn's GridEncodingTemplated sizing, float32 host arithmetic (oracle/tcnn.py grid_levels)
+bool ngp_grid(const den_ngp_desc* d, NgpGrid* G, int64_t* table_floats) {
+  if (!d || d->n_levels < 1 || d->n_levels > NGP_MAX_LEVELS || d->n_features_per_level != NGP_F ||
+      d->log2_hashmap_size < 1 || d->log2_hashmap_size > 30 || d->base_resolution < 1 || !(d->per_level_scale >= 1.0f) ||
+      (d->grid_type != 0 && d->grid_type != 1) || (d->radiance_dim != 1 && d->radiance_dim != 3) ||
+      d->hidden_activation < 0 || d->hidden_activation > 1 || d->radiance_activation < 0 ||
+      d->radiance_activation > 1 || d->contraction < 0 || d->contraction > 2)
+    return false;
+  NgpGrid g{};
+  g.n_levels = d->n_levels;
+  g.hashed = d->grid_type == 0;
+  // f32 steps as tcnn's grid_scale, exp2 / log2 evaluated in double and rounded once (the oracle,
+  // oracle/tcnn.py grid_levels, does the same)
+  const float log2_pls = (float)std::log2((double)d->per_level_scale);
+  uint64_t off = 0;
+  for (int l = 0; l < d->n_levels; ++l) {
+    const float e = (float)l * log2_pls;
+    const float scale = (float)std::exp2((double)e) * (float)d->base_resolution - 1.0f;
+    const uint32_t res = (uint32_t)std::ceil(scale) + 1;
+    const uint32_t max_params = 0xFFFFFFFFu / 2;
+    uint64_t entries = std::pow((float)res, 3.0f) > (float)max_params ? max_params : (uint64_t)res * res * res;
+    entries = (entries + 7) / 8 * 8;
+    if (g.hashed) entries = std::min<uint64_t>(entries, 1ull << d->log2_hashmap_size);
+    if (off + entries > 0x7FFFFFFFull) return false;
+    g.scale[l] = scale;
+    g.res[l] = res;
+    g.entries[l] = (uint32_t)entries;
+    g.offset[l] = (uint32_t)off;
+    off += entries;
+  }
+  *G = g;
+  *table_floats = (int64_t)off * NGP_F;
+  return true;
+}
+
+struct NgpWs {
+  size_t save, dz, partial, total;
+  int splits;
+  int64_t per_split;
+};
+NgpWs ngp_ws(int64_t n) {
+  NgpWs w{};
+  size_t off = 0;
+  w.save = off;
+  off += align256((size_t)NS_ROWS * n * 4);
+  w.dz = off;
+  off += align256((size_t)ND_ROWS * n * 4);
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(256, (n + 4095) / 4096));
+  int64_t per = (n + splits - 1) / splits;
+  per = (per + NGP_DW_CHUNK - 1) / NGP_DW_CHUNK * NGP_DW_CHUNK;
+  w.splits = (int)((n + per - 1) / per);
+  w.per_split = per;
+  w.partial = off;
+  off += align256((size_t)5 * w.splits * NGP_DW_PM * NGP_DW_PK * 4);
+  w.total = off;
+  return w;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t den_ngp_table_params(const den_ngp_desc* desc) {
+  NgpGrid g;
+  int64_t t;
+  return ngp_grid(desc, &g, &t) ? t : -1;
+}
+
+int64_t den_ngp_param_count(const den_ngp_desc* desc) {
+  const int64_t t = den_ngp_table_params(desc);
+  return t < 0 ? -1 : t + ngp_mlp_params(2 * desc->n_levels, desc->radiance_dim);
+}
+
+size_t den_ngp_workspace_bytes(const den_ngp_desc* desc, int64_t n, int32_t train) {
+  if (!train || n <= 0 || den_ngp_table_params(desc) < 0) return 0;
+  return ngp_ws(n).total;
+}
+
+int den_ngp_fwd(const den_ngp_desc* desc, int64_t n, int32_t points, const float* x, const float* d,
+                const int32_t* ray_idx, const float* t0, const float* t1, const float* params, int32_t density_only,
+                int32_t train, void* workspace, float* out_rgb, float* out_sigma, void* stream) {
+  NgpGrid g;
+  int64_t tfl;
+  if (!ngp_grid(desc, &g, &tfl)) return fail(DEN_EUNSUPPORTED, "unsupported ngp descriptor");
+  if (n < 0 || (points != 1 && points != 2) || !params || !out_sigma || (!density_only && !out_rgb) ||
+      (train && (!workspace || density_only)) || (n > 0 && (!x || !d)) ||
+      (points == 2 && n > 0 && (!ray_idx || !t0 || !t1)))
+    return fail(DEN_EINVAL, "bad arguments");
+  if (n == 0) return DEN_OK;
+  NgpArgs A{};
+  A.n = n;
+  A.rd = desc->radiance_dim;
+  A.points = points;
+  A.contraction = desc->contraction;
+  A.hidden_relu = desc->hidden_activation;
+  A.rad_sigmoid = desc->radiance_activation;
+  A.density_only = density_only ? 1 : 0;
+  for (int i = 0; i < 6; ++i) A.aabb[i] = desc->aabb[i];
+  A.x = x;
+  A.d = d;
+  A.ray_idx = ray_idx;
+  A.t0 = t0;
+  A.t1 = t1;
+  A.table = params;
+  A.mlp = params + tfl;
+  A.off = ngp_offsets(2 * g.n_levels, desc->radiance_dim);
+  A.enc = 2 * g.n_levels;
+  A.grid = g;
+  A.out_rgb = out_rgb;
+  A.out_sigma = out_sigma;
+  A.save = train ? (float*)((char*)workspace + ngp_ws(n).save) : nullptr;
+  hipLaunchKernelGGL(ngp_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* workspace, const float* d_rgb,
+                const float* d_sigma, float* grad_params, void* stream) {
+  NgpGrid g;
+  int64_t tfl;
+  if (!ngp_grid(desc, &g, &tfl)) return fail(DEN_EUNSUPPORTED, "unsupported ngp descriptor");
+  if (n < 0 || !params || !workspace || !grad_params) return fail(DEN_EINVAL, "bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  DEN_HIP(hipMemsetAsync(grad_params, 0, (size_t)tfl * 4, st));
+  if (n == 0) {
+    DEN_HIP(hipMemsetAsync(grad_params + tfl, 0, (size_t)ngp_mlp_params(2 * g.n_levels, desc->radiance_dim) * 4, st));
+    return DEN_OK;
+  }
+  const NgpWs W = ngp_ws(n);
+  char* ws = (char*)workspace;
+  NgpArgs A{};
+  A.n = n;
+  A.rd = desc->radiance_dim;
+  A.hidden_relu = desc->hidden_activation;
+  A.rad_sigmoid = desc->radiance_activation;
+  A.mlp = params + tfl;
+  A.off = ngp_offsets(2 * g.n_levels, desc->radiance_dim);
+  A.enc = 2 * g.n_levels;
+  A.grid = g;
+  A.save = (float*)(ws + W.save);
+  A.d_rgb = d_rgb;
+  A.d_sigma = d_sigma;
+  A.d_table = grad_params;
+  A.dz = (float*)(ws + W.dz);
+  hipLaunchKernelGGL(ngp_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
+  DEN_LAUNCHED();
+  const int rd = desc->radiance_dim;
+  NgpDwArgs P{};
+  P.dz = A.dz;
+  P.save = A.save;
+  P.n = n;
+  P.per_split = W.per_split;
+  P.splits = W.splits;
+  P.partial = (float*)(ws + W.partial);
+  P.grad = grad_params + tfl;
+  const NgpOff& O = A.off;
+  P.L[0] = NgpDwLayer{ND_Z0, NGP_W, NS_FEAT, A.enc, O.w[0], O.b[0]};
+  P.L[1] = NgpDwLayer{ND_O, 1 + NGP_GEO, NS_H0, NGP_W, O.w[1], O.b[1]};
+  P.L[2] = NgpDwLayer{ND_Z2, NGP_W, NS_HIN, NGP_HIN, O.w[2], O.b[2]};
+  P.L[3] = NgpDwLayer{ND_Z3, NGP_W, NS_H1, NGP_W, O.w[3], O.b[3]};
+  P.L[4] = NgpDwLayer{ND_R, rd, NS_H2, NGP_W, O.w[4], O.b[4]};
+  hipLaunchKernelGGL(ngp_dw_kernel, dim3((unsigned)W.splits, 5), dim3(256), 0, st, P);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(ngp_dw_reduce_kernel, dim3((NGP_DW_PM * NGP_DW_PK + 255) / 256, 5), dim3(256), 0, st, P);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_hashgrid_fwd(const den_ngp_desc* desc, int64_t n, const float* x, const float* table, float* out,
+                     void* stream) {
+  NgpGrid g;
+  int64_t tfl;
+  if (!ngp_grid(desc, &g, &tfl)) return fail(DEN_EUNSUPPORTED, "unsupported grid descriptor");
+  if (n < 0 || (n > 0 && (!x || !table || !out))) return fail(DEN_EINVAL, "bad arguments");
+  if (n == 0) return DEN_OK;
+  NgpEncArgs E{n, g, x, table, out, nullptr, nullptr};
+  hipLaunchKernelGGL(ngp_encode_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, E);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_hashgrid_bwd(const den_ngp_desc* desc, int64_t n, const float* x, const float* d_out, float* d_table,
+                     void* stream) {
+  NgpGrid g;
+  int64_t tfl;
+  if (!ngp_grid(desc, &g, &tfl)) return fail(DEN_EUNSUPPORTED, "unsupported grid descriptor");
+  if (n < 0 || (n > 0 && (!x || !d_out || !d_table))) return fail(DEN_EINVAL, "bad arguments");
+  if (n == 0) return DEN_OK;
+  NgpEncArgs E{n, g, x, nullptr, nullptr, d_out, d_table};
+  hipLaunchKernelGGL(ngp_encode_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     E);
   DEN_LAUNCHED();
   return DEN_OK;
 }

@@ -244,10 +244,11 @@ __device__ __forceinline__ void sample_interval(const RayGeom& g, int k, float u
 // then selector = all(0 < x < 1) and x' = 2*pi*(x - 0.5).
 enum { CONTRACT_AABB = 0, CONTRACT_TANH = 1, CONTRACT_SPHERE = 2 };
 
-__device__ __forceinline__ void contract_point(const float* pos, const float* aabb, float* xc, float* sel,
-                                               int type = CONTRACT_AABB) {
+// the contracted position x in [0,1]^3 (for the interior) and the selector; the ngp field
+// (ngp.py:230-238) encodes x itself, the mlp field x' = 2 pi (x - 0.5) (contract_point)
+__device__ __forceinline__ void contract_unit(const float* pos, const float* aabb, float* x, float* sel,
+                                              int type = CONTRACT_AABB) {
 #pragma clang fp contract(off)
-  float x[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) x[a] = __fdiv_rn(pos[a] - aabb[a], aabb[3 + a] - aabb[a]);
   if (type == CONTRACT_SPHERE) {
@@ -267,11 +268,17 @@ __device__ __forceinline__ void contract_point(const float* pos, const float* aa
   }
   bool in = true;
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    in = in && (x[a] > 0.0f) && (x[a] < 1.0f);
-    xc[a] = 6.2831855f * (x[a] - 0.5f);
-  }
+  for (int a = 0; a < 3; ++a) in = in && (x[a] > 0.0f) && (x[a] < 1.0f);
   *sel = in ? 1.0f : 0.0f;
+}
+
+__device__ __forceinline__ void contract_point(const float* pos, const float* aabb, float* xc, float* sel,
+                                               int type = CONTRACT_AABB) {
+#pragma clang fp contract(off)
+  float x[3];
+  contract_unit(pos, aabb, x, sel, type);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) xc[a] = 6.2831855f * (x[a] - 0.5f);
 }
 
 // sample position o + d*(t0 + t1)/2 (external/utils.py:83-87), then the contraction

@@ -1,0 +1,620 @@
+// den_ngp.hip -- the `ngp` radiance field (reference external/ngp.py NGPradianceField, the shipped
+// default arch of configs/train/*.yaml): tiny-cuda-nn's multiresolution hash-grid encoding, the
+// mlp_base / mlp_head MLPs (external/mlp.py MLP with the configured activations), the degree-4
+// SH view encoding (external/sh_encoder.py) and shifted_trunc_exp density -- forward, backward
+// (hash-table scatter + per-sample layer gradients) and the weight-gradient GEMMs.
+//
+// One sample per lane.  The work per sample is latency-bound gathers (16 levels x 8 corners of
+// float2 from a <= 50 MB table, resident in the 256 MB MALL) plus 9.3 K f32 MACs of tiny MLPs,
+// so the field is laid out for occupancy, not for MFMA: the MLP weights are wave-uniform
+// (kernel-argument pointer + compile-time offsets), so they come through the scalar cache into
+// SGPR operands of v_fmac_f32 and cost no VGPRs or LDS; activations stay in VGPRs.  f32
+// throughout, in torch's operation order where it matters (softplus threshold, SH products),
+// so parity is at the f32-rounding level against the reference.
+//
+// Saved state (train) and per-layer gradients are FEATURE-major ([row][n]): a wave's stores and
+// loads of one feature are 256 contiguous bytes, and the weight-gradient GEMM dW = dZ^T X reads
+// rows that are contiguous over samples (k = samples).
+#include "den_device.h"
+
+namespace den {
+
+constexpr int NGP_MAX_LEVELS = 16;
+constexpr int NGP_F = 2;                         // features per level
+constexpr int NGP_ENC = NGP_MAX_LEVELS * NGP_F;  // encoding width (32)
+constexpr int NGP_W = 64;                        // n_neurons (base and head)
+constexpr int NGP_GEO = 15;                      // geo_feat_dim
+constexpr int NGP_SH = 16;                       // SH degree 4
+constexpr int NGP_HIN = NGP_SH + NGP_GEO;        // head input (31)
+
+// MLP parameter offsets (floats) after the hash table, reference named_parameters() order:
+// mlp_base.1.hidden_layers.0 (64 x E, E = 2 n_levels), mlp_base.1.output_layer (16 x 64),
+// mlp_head.hidden_layers.0 (64 x 31), .1 (64 x 64), mlp_head.output_layer (rd x 64); weight then
+// bias, torch (out, in) layout.
+struct NgpOff {
+  int w[5], b[5];
+};
+DEN_HD inline NgpOff ngp_offsets(int enc, int rd) {
+  NgpOff o{};
+  const int in[5] = {enc, NGP_W, NGP_HIN, NGP_W, NGP_W};
+  const int out[5] = {NGP_W, 1 + NGP_GEO, NGP_W, NGP_W, rd};
+  int off = 0;
+  for (int l = 0; l < 5; ++l) {
+    o.w[l] = off;
+    off += in[l] * out[l];
+    o.b[l] = off;
+    off += out[l];
+  }
+  return o;
+}
+DEN_HD inline int ngp_mlp_params(int enc, int rd) {
+  const NgpOff o = ngp_offsets(enc, rd);
+  return o.b[4] + rd;
+}
+
+// saved rows (train): encoding, pre-activation and output of each hidden layer, head input,
+// radiance pre-activation, density pre-activation, selector, contracted position
+enum {
+  NS_FEAT = 0,
+  NS_H0P = NS_FEAT + NGP_ENC,
+  NS_H0 = NS_H0P + NGP_W,
+  NS_HIN = NS_H0 + NGP_W,
+  NS_H1P = NS_HIN + 32,
+  NS_H1 = NS_H1P + NGP_W,
+  NS_H2P = NS_H1 + NGP_W,
+  NS_H2 = NS_H2P + NGP_W,
+  NS_R = NS_H2 + NGP_W,
+  NS_O0 = NS_R + 4,
+  NS_SEL = NS_O0 + 1,
+  NS_X = NS_SEL + 1,
+  NS_ROWS = NS_X + 3
+};
+// per-layer pre-activation gradients (rows): layer 0 (64), base output (16), head 0 (64), head 1 (64), rgb (rd)
+enum { ND_Z0 = 0, ND_O = ND_Z0 + NGP_W, ND_Z2 = ND_O + 1 + NGP_GEO, ND_Z3 = ND_Z2 + NGP_W, ND_R = ND_Z3 + NGP_W,
+       ND_ROWS = ND_R + 4 };
+
+struct NgpGrid {
+  int n_levels;
+  int hashed;                      // HashGrid (tcnn GridType::Hash) vs DenseGrid
+  float scale[NGP_MAX_LEVELS];     // exp2f(l * log2f(per_level_scale)) * base_resolution - 1
+  uint32_t res[NGP_MAX_LEVELS];    // ceilf(scale) + 1
+  uint32_t entries[NGP_MAX_LEVELS];
+  uint32_t offset[NGP_MAX_LEVELS];  // entry offset of the level
+};
+
+struct NgpArgs {
+  int64_t n;
+  int rd;
+  int points;        // 1: positions x (n,3) + directions (n,3); 2: packed samples of rays
+  int contraction;   // CONTRACT_*
+  int hidden_relu;   // hidden activation: 0 softplus(beta = 100), 1 relu
+  int rad_sigmoid;   // radiance activation: 0 softplus(beta = 1), 1 sigmoid
+  int density_only;  // sigma_fn of the marching pre-pass: skip the head
+  float aabb[6];
+  const float* x;    // points 1: positions; points 2: ray origins (R,3)
+  const float* d;    // points 1: directions; points 2: ray directions (R,3)
+  const int* ray_idx;
+  const float* t0;
+  const float* t1;
+  const float* table;  // hash-grid parameters
+  const float* mlp;    // MLP parameters (offsets: off)
+  NgpOff off;
+  int enc;             // encoding width 2 n_levels (<= NGP_ENC)
+  NgpGrid grid;
+  float* out_rgb;      // (n, rd)
+  float* out_sigma;    // (n)
+  float* save;         // train: [NS_ROWS][n]
+  // backward
+  const float* d_rgb;
+  const float* d_sigma;
+  float* d_table;
+  float* dz;           // [ND_ROWS][n]
+};
+
+// ------------------------------------------------------------------ elementwise pieces
+// torch.nn.Softplus(beta, threshold = 20): x if beta x > 20 else log1p(exp(beta x)) / beta
+__device__ __forceinline__ float ngp_sp100(float x) {
+  const float bx = x * 100.0f;
+  return bx > 20.0f ? x : __fdiv_rn(log1pf(expf(bx)), 100.0f);
+}
+// its backward from the input: z = exp(beta x); beta x > 20 ? g : g z / (z + 1)
+__device__ __forceinline__ float ngp_dsp100(float x) {
+  const float bx = x * 100.0f;
+  if (bx > 20.0f) return 1.0f;
+  const float z = expf(bx);
+  return __fdiv_rn(z, z + 1.0f);
+}
+__device__ __forceinline__ float ngp_act(float x, int relu) { return relu ? fmaxf(x, 0.0f) : ngp_sp100(x); }
+__device__ __forceinline__ float ngp_dact(float pre, float out, int relu) {
+  return relu ? (out > 0.0f ? 1.0f : 0.0f) : ngp_dsp100(pre);
+}
+
+// The MLP weights are read through the constant address space: wave-uniform addresses there become
+// scalar loads into SGPR operands (through the generic / global space the compiler cannot prove the
+// stores of the kernel leave them unchanged, emits vector loads and runs out of VGPRs).
+typedef const __attribute__((address_space(4))) float* ngp_cptr;
+__device__ __forceinline__ ngp_cptr ngp_const(const float* p) { return (ngp_cptr)p; }
+
+// y = W x + b, W row-major (OUT, LD), first IN columns (uniform weights: scalar loads)
+template <int OUT, int IN, int LD>
+__device__ __forceinline__ void ngp_linear(ngp_cptr W, ngp_cptr b, const float* x, float* y) {
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < IN; ++i) acc = fmaf(W[o * LD + i], x[i], acc);
+    y[o] = acc + b[o];
+  }
+}
+// layer 0: the encoding width E = 2 n_levels <= NGP_ENC is a runtime (wave-uniform) row length
+__device__ __forceinline__ void ngp_linear_enc(ngp_cptr W, ngp_cptr b, const float* x, float* y, int E) {
+#pragma unroll
+  for (int o = 0; o < NGP_W; ++o) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NGP_ENC; ++i)
+      if (i < E) acc = fmaf(W[o * E + i], x[i], acc);
+    y[o] = acc + b[o];
+  }
+}
+__device__ __forceinline__ void ngp_linear_enc_t(ngp_cptr W, const float* dy, float* dx, int E) {
+#pragma unroll
+  for (int i = 0; i < NGP_ENC; ++i) dx[i] = 0.0f;
+#pragma unroll
+  for (int o = 0; o < NGP_W; ++o)
+#pragma unroll
+    for (int i = 0; i < NGP_ENC; ++i)
+      if (i < E) dx[i] = fmaf(W[o * E + i], dy[o], dx[i]);
+}
+
+// dx = W^T dy (OUT rows of W, first IN columns), rows streamed in order
+template <int OUT, int IN, int LD>
+__device__ __forceinline__ void ngp_linear_t(ngp_cptr W, const float* dy, float* dx) {
+#pragma unroll
+  for (int i = 0; i < IN; ++i) dx[i] = 0.0f;
+#pragma unroll
+  for (int o = 0; o < OUT; ++o)
+#pragma unroll
+    for (int i = 0; i < IN; ++i) dx[i] = fmaf(W[o * LD + i], dy[o], dx[i]);
+}
+
+// SHEncoder (external/sh_encoder.py:27-80), degree 4, the reference's f32 operation order
+__device__ __forceinline__ void ngp_sh4(const float* dv, float* out) {
+#pragma clang fp contract(off)
+  const float x = dv[0], y = dv[1], z = dv[2];
+  const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+  out[0] = 0.28209479177387814f;
+  out[1] = -0.48860251190291987f * y;
+  out[2] = 0.48860251190291987f * z;
+  out[3] = -0.48860251190291987f * x;
+  out[4] = 1.0925484305920792f * xy;
+  out[5] = -1.0925484305920792f * yz;
+  out[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+  out[7] = -1.0925484305920792f * xz;
+  out[8] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+  out[9] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
+  out[10] = 2.8906114426405538f * xy * z;
+  out[11] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
+  out[12] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
+  out[13] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
+  out[14] = 1.4453057213202769f * z * (x2 - y2);
+  out[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+}
+
+// ------------------------------------------------------------------ grid encoding (tcnn grid.h)
+// cell / fractional position of one coordinate: pos = fmaf(scale, x, 0.5) (pos_fract)
+struct NgpCorner {
+  uint32_t idx[8];
+  float w[8];
+};
+
+__device__ __forceinline__ uint32_t ngp_index(const NgpGrid& G, int l, uint32_t cx, uint32_t cy, uint32_t cz) {
+  // grid_index: dense strides while the stride stays <= the level size, else the prime hash
+  const uint32_t size = G.entries[l], res = G.res[l];
+  uint32_t stride = 1, index = 0;
+  const uint32_t c[3] = {cx, cy, cz};
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    if (stride <= size) {
+      index += c[d] * stride;
+      stride *= res;
+    } else {
+      stride = 0xFFFFFFFFu;  // the loop has ended (stride > size stays true)
+    }
+  }
+  if (G.hashed && size < stride) index = cx ^ (cy * 2654435761u) ^ (cz * 805459861u);
+  return index % size;
+}
+
+__device__ __forceinline__ void ngp_corners(const NgpGrid& G, int l, const float* x, NgpCorner& C) {
+  float frac[3];
+  uint32_t cell[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float pos = fmaf(G.scale[l], x[d], 0.5f);
+    const float fl = floorf(pos);
+    cell[d] = (uint32_t)(int)fl;
+    frac[d] = pos - fl;
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float w = 1.0f;
+    uint32_t p[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      if ((c >> d) & 1) {
+        w *= frac[d];
+        p[d] = cell[d] + 1;
+      } else {
+        w *= 1.0f - frac[d];
+        p[d] = cell[d];
+      }
+    }
+    C.w[c] = w;
+    C.idx[c] = G.offset[l] + ngp_index(G, l, p[0], p[1], p[2]);
+  }
+}
+
+__device__ __forceinline__ void ngp_encode(const NgpGrid& G, const float* __restrict__ table, const float* x,
+                                           float* feat) {
+#pragma unroll
+  for (int l = 0; l < NGP_MAX_LEVELS; ++l) {
+    float f0 = 0.0f, f1 = 0.0f;
+    if (l < G.n_levels) {
+      NgpCorner C;
+      ngp_corners(G, l, x, C);
+      float2 v[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = *(const float2*)(table + 2 * (int64_t)C.idx[c]);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        f0 = fmaf(C.w[c], v[c].x, f0);
+        f1 = fmaf(C.w[c], v[c].y, f1);
+      }
+    }
+    feat[2 * l] = f0;
+    feat[2 * l + 1] = f1;
+  }
+}
+
+// position (points 1: given; points 2: o + d (t0 + t1)/2 of the sample's ray) -> contracted x in
+// [0,1]^3 + selector (ngp.py:230-238), and the view direction
+__device__ __forceinline__ void ngp_point(const NgpArgs& A, int64_t i, float* xn, float* sel, float* dir) {
+  float pos[3];
+  if (A.points == 2) {
+    const int64_t r = A.ray_idx[i];
+    float o[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      o[a] = A.x[r * 3 + a];
+      dir[a] = A.d[r * 3 + a];
+    }
+    {
+#pragma clang fp contract(off)
+      const float tt = A.t0[i] + A.t1[i];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) pos[a] = o[a] + __fdiv_rn(dir[a] * tt, 2.0f);
+    }
+  } else {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      pos[a] = A.x[i * 3 + a];
+      dir[a] = A.d[i * 3 + a];
+    }
+  }
+  contract_unit(pos, A.aabb, xn, sel, A.contraction);
+}
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n) return;
+  const ngp_cptr P = ngp_const(A.mlp);
+  float xn[3], sel, dir[3];
+  ngp_point(A, i, xn, &sel, dir);
+  float feat[NGP_ENC];
+  ngp_encode(A.grid, A.table, xn, feat);
+  const int relu = A.hidden_relu;
+  float* S = A.save;
+  const int64_t n = A.n;
+  if (S) {
+#pragma unroll
+    for (int f = 0; f < NGP_ENC; ++f)
+      if (f < A.enc) S[(NS_FEAT + f) * n + i] = feat[f];
+  }
+  float h0[NGP_W];
+  {
+    float h0p[NGP_W];
+    ngp_linear_enc(P + A.off.w[0], P + A.off.b[0], feat, h0p, A.enc);
+#pragma unroll
+    for (int o = 0; o < NGP_W; ++o) h0[o] = ngp_act(h0p[o], relu);
+    if (S) {
+#pragma unroll
+      for (int o = 0; o < NGP_W; ++o) {
+        S[(NS_H0P + o) * n + i] = h0p[o];
+        S[(NS_H0 + o) * n + i] = h0[o];
+      }
+    }
+  }
+  float ob[1 + NGP_GEO];
+  ngp_linear<1 + NGP_GEO, NGP_W, NGP_W>(P + A.off.w[1], P + A.off.b[1], h0, ob);
+  // shifted_trunc_exp(o0) * selector; selected (not multiplied) so an overflow outside the box is 0
+  const float sigma = sel != 0.0f ? expf(ob[0] - 1.0f) : 0.0f;
+  A.out_sigma[i] = sigma;
+  if (S) {
+    S[NS_O0 * n + i] = ob[0];
+    S[NS_SEL * n + i] = sel;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) S[(NS_X + a) * n + i] = xn[a];
+  }
+  if (A.density_only) return;
+  float hin[NGP_HIN];
+  ngp_sh4(dir, hin);
+#pragma unroll
+  for (int g = 0; g < NGP_GEO; ++g) hin[NGP_SH + g] = ob[1 + g];
+  if (S) {
+#pragma unroll
+    for (int f = 0; f < NGP_HIN; ++f) S[(NS_HIN + f) * n + i] = hin[f];
+  }
+  // each layer's saved rows are stored as soon as it is computed (keeps them out of VGPRs)
+  float h1[NGP_W];
+  {
+    float h1p[NGP_W];
+    ngp_linear<NGP_W, NGP_HIN, NGP_HIN>(P + A.off.w[2], P + A.off.b[2], hin, h1p);
+#pragma unroll
+    for (int o = 0; o < NGP_W; ++o) h1[o] = ngp_act(h1p[o], relu);
+    if (S) {
+#pragma unroll
+      for (int o = 0; o < NGP_W; ++o) {
+        S[(NS_H1P + o) * n + i] = h1p[o];
+        S[(NS_H1 + o) * n + i] = h1[o];
+      }
+    }
+  }
+  float h2[NGP_W];
+  {
+    float h2p[NGP_W];
+    ngp_linear<NGP_W, NGP_W, NGP_W>(P + A.off.w[3], P + A.off.b[3], h1, h2p);
+#pragma unroll
+    for (int o = 0; o < NGP_W; ++o) h2[o] = ngp_act(h2p[o], relu);
+    if (S) {
+#pragma unroll
+      for (int o = 0; o < NGP_W; ++o) {
+        S[(NS_H2P + o) * n + i] = h2p[o];
+        S[(NS_H2 + o) * n + i] = h2[o];
+      }
+    }
+  }
+  float r[3] = {0.f, 0.f, 0.f};
+  if (A.rd == 3) ngp_linear<3, NGP_W, NGP_W>(P + A.off.w[4], P + A.off.b[4], h2, r);
+  else ngp_linear<1, NGP_W, NGP_W>(P + A.off.w[4], P + A.off.b[4], h2, r);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (c < A.rd) {
+      const float v = A.rad_sigmoid ? __fdiv_rn(1.0f, 1.0f + expf(-r[c])) : (r[c] > 20.0f ? r[c] : log1pf(expf(r[c])));
+      A.out_rgb[i * A.rd + c] = v;
+    }
+    if (S) S[(NS_R + c) * n + i] = r[c];
+  }
+}
+
+// ------------------------------------------------------------------ backward (per sample)
+// -> the pre-activation gradient of every layer (rows of A.dz) and the hash-table gradient
+// (tcnn kernel_grid_backward: atomicAdd of weight * dy per corner and feature)
+__global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpArgs A) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n) return;
+  const ngp_cptr P = ngp_const(A.mlp);
+  const float* S = A.save;
+  const int64_t n = A.n;
+  const int relu = A.hidden_relu;
+  float* D = A.dz;
+  // radiance activation
+  float dr[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (c >= A.rd) break;
+    const float g = A.d_rgb ? A.d_rgb[i * A.rd + c] : 0.0f;
+    const float rv = S[(NS_R + c) * n + i];
+    if (A.rad_sigmoid) {
+      const float s = __fdiv_rn(1.0f, 1.0f + expf(-rv));
+      dr[c] = g * (s * (1.0f - s));
+    } else {
+      const float z = expf(rv);
+      dr[c] = rv > 20.0f ? g : g * __fdiv_rn(z, z + 1.0f);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) D[(ND_R + c) * n + i] = dr[c];
+  // head output layer -> h2 -> h1 -> head input
+  float dh[NGP_W], dz[NGP_W];
+  if (A.rd == 3) ngp_linear_t<3, NGP_W, NGP_W>(P + A.off.w[4], dr, dh);
+  else ngp_linear_t<1, NGP_W, NGP_W>(P + A.off.w[4], dr, dh);
+#pragma unroll
+  for (int o = 0; o < NGP_W; ++o) {
+    dz[o] = dh[o] * ngp_dact(S[(NS_H2P + o) * n + i], S[(NS_H2 + o) * n + i], relu);
+    D[(ND_Z3 + o) * n + i] = dz[o];
+  }
+  ngp_linear_t<NGP_W, NGP_W, NGP_W>(P + A.off.w[3], dz, dh);
+#pragma unroll
+  for (int o = 0; o < NGP_W; ++o) {
+    dz[o] = dh[o] * ngp_dact(S[(NS_H1P + o) * n + i], S[(NS_H1 + o) * n + i], relu);
+    D[(ND_Z2 + o) * n + i] = dz[o];
+  }
+  float dhin[NGP_HIN];
+  ngp_linear_t<NGP_W, NGP_HIN, NGP_HIN>(P + A.off.w[2], dz, dhin);
+  // base output: density (trunc_exp backward clamps the exponent at 15) and the geo features
+  float dob[1 + NGP_GEO];
+  {
+    const float gs = A.d_sigma ? A.d_sigma[i] : 0.0f;
+    const float sel = S[NS_SEL * n + i];
+    const float o0 = S[NS_O0 * n + i];
+    dob[0] = sel != 0.0f ? gs * expf(fminf(o0 - 1.0f, 15.0f)) : 0.0f;
+  }
+#pragma unroll
+  for (int g = 0; g < NGP_GEO; ++g) dob[1 + g] = dhin[NGP_SH + g];
+#pragma unroll
+  for (int o = 0; o < 1 + NGP_GEO; ++o) D[(ND_O + o) * n + i] = dob[o];
+  ngp_linear_t<1 + NGP_GEO, NGP_W, NGP_W>(P + A.off.w[1], dob, dh);
+#pragma unroll
+  for (int o = 0; o < NGP_W; ++o) {
+    dz[o] = dh[o] * ngp_dact(S[(NS_H0P + o) * n + i], S[(NS_H0 + o) * n + i], relu);
+    D[(ND_Z0 + o) * n + i] = dz[o];
+  }
+  float dfeat[NGP_ENC];
+  ngp_linear_enc_t(P + A.off.w[0], dz, dfeat, A.enc);
+  // hash-table scatter
+  float xn[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) xn[a] = S[(NS_X + a) * n + i];
+  for (int l = 0; l < A.grid.n_levels; ++l) {
+    NgpCorner C;
+    ngp_corners(A.grid, l, xn, C);
+    const float g0 = dfeat[2 * l], g1 = dfeat[2 * l + 1];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float* t = A.d_table + 2 * (int64_t)C.idx[c];
+      unsafeAtomicAdd(t, C.w[c] * g0);
+      unsafeAtomicAdd(t + 1, C.w[c] * g1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ standalone encoding (tcnn.Encoding)
+struct NgpEncArgs {
+  int64_t n;
+  NgpGrid grid;
+  const float* x;      // (n, 3) in [0,1]
+  const float* table;
+  float* out;          // (n, 2 L)
+  const float* d_out;  // backward
+  float* d_table;
+};
+
+__global__ __launch_bounds__(256) void ngp_encode_kernel(NgpEncArgs E) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E.n) return;
+  float x[3] = {E.x[i * 3], E.x[i * 3 + 1], E.x[i * 3 + 2]};
+  float feat[NGP_ENC];
+  ngp_encode(E.grid, E.table, x, feat);
+  const int w = 2 * E.grid.n_levels;
+  for (int f = 0; f < w; ++f) E.out[i * w + f] = feat[f];
+}
+
+__global__ __launch_bounds__(256) void ngp_encode_bwd_kernel(NgpEncArgs E) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E.n) return;
+  float x[3] = {E.x[i * 3], E.x[i * 3 + 1], E.x[i * 3 + 2]};
+  const int w = 2 * E.grid.n_levels;
+  for (int l = 0; l < E.grid.n_levels; ++l) {
+    NgpCorner C;
+    ngp_corners(E.grid, l, x, C);
+    const float g0 = E.d_out[i * w + 2 * l], g1 = E.d_out[i * w + 2 * l + 1];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float* t = E.d_table + 2 * (int64_t)C.idx[c];
+      unsafeAtomicAdd(t, C.w[c] * g0);
+      unsafeAtomicAdd(t + 1, C.w[c] * g1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ weight gradients
+// dW[o][k] = sum_s dZ[o][s] X[k][s], db[o] = sum_s dZ[o][s] for the five layers, split-K over
+// samples: workgroup (split, layer) stages 64-sample chunks of its dZ and X rows sample-major in
+// LDS ([s][row], 4-row groups contiguous for ds_read_b128; a ones row gives the bias) and each lane
+// accumulates 4 x 4 output blocks.  Partials [layer][split][64][65] reduced in a fixed order.
+constexpr int NGP_DW_CHUNK = 64, NGP_DW_LD = 68, NGP_DW_PM = 64, NGP_DW_PK = 65;
+
+struct NgpDwLayer {
+  int a_row, m;   // dZ rows
+  int b_row, k;   // X rows (saved activations)
+  int64_t w_off;  // weight / bias offsets in the flat gradient
+  int64_t b_off;
+};
+struct NgpDwArgs {
+  const float* dz;
+  const float* save;
+  int64_t n;
+  int64_t per_split;
+  int splits;
+  NgpDwLayer L[5];
+  float* partial;  // [5][splits][64][65]
+  float* grad;
+};
+
+__global__ __launch_bounds__(256) void ngp_dw_kernel(NgpDwArgs P) {
+  __shared__ __attribute__((aligned(16))) float sa[NGP_DW_CHUNK * NGP_DW_LD];
+  __shared__ __attribute__((aligned(16))) float sb[NGP_DW_CHUNK * NGP_DW_LD];
+  const NgpDwLayer L = P.L[blockIdx.y];
+  const int tid = threadIdx.x;
+  const int MG = (L.m + 3) / 4, KG = (L.k + 1 + 3) / 4;  // + the ones column
+  const int T = MG * KG;
+  float acc[2][16];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[u][e] = 0.0f;
+  const int64_t s0 = (int64_t)blockIdx.x * P.per_split;
+  const int64_t s1 = s0 + P.per_split < P.n ? s0 + P.per_split : P.n;
+  for (int64_t c0 = s0; c0 < s1; c0 += NGP_DW_CHUNK) {
+    __syncthreads();
+    // stage: lane (s = tid & 63) of row group (tid >> 6) -- coalesced over samples
+    for (int r = tid >> 6; r < NGP_DW_LD; r += 4) {
+      const int s = tid & 63;
+      const int64_t si = c0 + s;
+      const bool ok = si < s1;
+      float va = 0.0f, vb = 0.0f;
+      if (r < L.m && ok) va = P.dz[(int64_t)(L.a_row + r) * P.n + si];
+      if (r < L.k && ok) vb = P.save[(int64_t)(L.b_row + r) * P.n + si];
+      else if (r == L.k && ok) vb = 1.0f;
+      sa[s * NGP_DW_LD + r] = va;
+      sb[s * NGP_DW_LD + r] = vb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = tid + u * 256;
+      if (t < T) {
+        const int og = t / KG, kg = t % KG;
+        for (int s = 0; s < NGP_DW_CHUNK; ++s) {
+          const f32x4 a = *(const f32x4*)(sa + s * NGP_DW_LD + 4 * og);
+          const f32x4 b = *(const f32x4*)(sb + s * NGP_DW_LD + 4 * kg);
+#pragma unroll
+          for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[u][4 * p + q] = fmaf(a[p], b[q], acc[u][4 * p + q]);
+        }
+      }
+    }
+  }
+  float* out = P.partial + ((int64_t)blockIdx.y * P.splits + blockIdx.x) * NGP_DW_PM * NGP_DW_PK;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = tid + u * 256;
+    if (t < T) {
+      const int og = t / KG, kg = t % KG;
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int o = 4 * og + p, k = 4 * kg + q;
+          if (o < L.m && k <= L.k) out[o * NGP_DW_PK + k] = acc[u][4 * p + q];
+        }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void ngp_dw_reduce_kernel(NgpDwArgs P) {
+  const NgpDwLayer L = P.L[blockIdx.y];
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= L.m * (L.k + 1)) return;
+  const int o = e / (L.k + 1), k = e % (L.k + 1);
+  const float* src = P.partial + (int64_t)blockIdx.y * P.splits * NGP_DW_PM * NGP_DW_PK + o * NGP_DW_PK + k;
+  float s = 0.0f;
+  for (int sp = 0; sp < P.splits; ++sp) s += src[(int64_t)sp * NGP_DW_PM * NGP_DW_PK];
+  if (k < L.k) P.grad[L.w_off + (int64_t)o * L.k + k] = s;
+  else P.grad[L.b_off + o] = s;
+}
+
+}  // namespace den

@@ -36,6 +36,15 @@ class RenderIO(ctypes.Structure):
                                                "t_starts", "t_ends")]
 
 
+class NgpDesc(ctypes.Structure):
+    _fields_ = [("radiance_dim", ctypes.c_int32), ("n_levels", ctypes.c_int32),
+                ("n_features_per_level", ctypes.c_int32), ("log2_hashmap_size", ctypes.c_int32),
+                ("base_resolution", ctypes.c_int32), ("per_level_scale", ctypes.c_float),
+                ("grid_type", ctypes.c_int32), ("hidden_activation", ctypes.c_int32),
+                ("radiance_activation", ctypes.c_int32), ("contraction", ctypes.c_int32),
+                ("aabb", ctypes.c_float * 6)]
+
+
 class RenderGrad(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("d_rgb", "d_opacity", "d_depth", "grad_params", "grad_bkgd")]
 
@@ -105,6 +114,14 @@ _SIGS = {
     "den_adam_step_f64": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_double] * 5
                           + [ctypes.c_int64, ctypes.c_void_p]),
     "den_trajectory": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 8),
+    "den_ngp_table_params": (ctypes.c_int64, [ctypes.POINTER(NgpDesc)]),
+    "den_ngp_param_count": (ctypes.c_int64, [ctypes.POINTER(NgpDesc)]),
+    "den_ngp_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(NgpDesc), ctypes.c_int64, ctypes.c_int32]),
+    "den_ngp_fwd": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 6
+                    + [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 4),
+    "den_ngp_bwd": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64] + [ctypes.c_void_p] * 6),
+    "den_hashgrid_fwd": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64] + [ctypes.c_void_p] * 4),
+    "den_hashgrid_bwd": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64] + [ctypes.c_void_p] * 4),
     "den_occ_workspace_bytes": (ctypes.c_size_t, []),
     "den_occ_points": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int32]
                        + [ctypes.c_void_p] * 4),
@@ -328,6 +345,115 @@ def field_packed(rays_o, rays_d, ray_indices, t_starts, t_ends, flat, cfg, packe
     rgb, sig, _ = RenderFunction.apply(rays_o.float().contiguous(), rays_d.float().contiguous(), None, None, flat,
                                        cfg, packed, group, 2, (ri.contiguous(), t0.contiguous(), t1.contiguous()))
     return rgb[:n], sig[:n]
+
+
+# ----------------------------------------------------------------------------- ngp radiance field
+def ngp_desc(rd, pos_encoding, hidden_activation, radiance_activation, contraction, aabb):
+    """den_ngp_desc of an NGPradianceField configuration (external/ngp.py:112-145 with the
+    configs/train/*.yaml nerf.ngp entries); unsupported settings raise DenError."""
+    pe = dict(pos_encoding)
+    if pe.get("interpolation", "Linear") != "Linear" or pe.get("otype", "HashGrid") not in ("HashGrid", "DenseGrid"):
+        raise DenError(f"ngp position encoding {pe} unsupported (Linear HashGrid / DenseGrid only)")
+    d = NgpDesc()
+    d.radiance_dim = int(rd)
+    d.n_levels = int(pe["n_levels"])
+    d.n_features_per_level = int(pe["n_features_per_level"])
+    d.log2_hashmap_size = int(pe.get("log2_hashmap_size", 19))
+    d.base_resolution = int(pe["base_resolution"])
+    d.per_level_scale = float(pe["per_level_scale"])
+    d.grid_type = 0 if pe.get("otype", "HashGrid") == "HashGrid" else 1
+    d.hidden_activation = {"softplus": 0, "relu": 1}[hidden_activation]
+    d.radiance_activation = {"softplus": 0, "sigmoid": 1}[radiance_activation]
+    d.contraction = int(contraction)
+    for i, v in enumerate(aabb):
+        d.aabb[i] = float(v)
+    if lib().den_ngp_table_params(ctypes.byref(d)) < 0:
+        raise DenError(f"unsupported ngp descriptor: {pe}")
+    return d
+
+
+def ngp_table_params(desc):
+    return int(lib().den_ngp_table_params(ctypes.byref(desc)))
+
+
+def ngp_param_count(desc):
+    return int(lib().den_ngp_param_count(ctypes.byref(desc)))
+
+
+class NgpFieldFunction(torch.autograd.Function):
+    """NGPradianceField forward at points (points = 1: x, d (n,3)) or packed ray samples
+    (points = 2: rays_o / rays_d (R,3) + ray_indices, t_starts, t_ends) -> rgb (n, rd), sigma (n)
+    (den_ngp_fwd); backward -> the flat-parameter gradient (den_ngp_bwd)."""
+
+    @staticmethod
+    def forward(ctx, flat, desc, points, x, d, ri, t0, t1, density_only):
+        _require_device(flat, x, d, ri, t0, t1)
+        n = (ri.numel() if points == 2 else x.shape[0])
+        dev = flat.device
+        # (grad mode is off inside Function.forward: needs_input_grad says whether a backward follows)
+        train = bool(ctx.needs_input_grad[0]) and not density_only
+        ws = (torch.empty(lib().den_ngp_workspace_bytes(ctypes.byref(desc), n, 1), dtype=torch.uint8, device=dev)
+              if train and n > 0 else None)
+        rgb = torch.empty(n, desc.radiance_dim, dtype=torch.float32, device=dev)
+        sig = torch.empty(n, dtype=torch.float32, device=dev)
+        _check(lib().den_ngp_fwd(ctypes.byref(desc), n, points, _ptr(x), _ptr(d), _ptr(ri), _ptr(t0), _ptr(t1),
+                                 _ptr(flat), int(bool(density_only)), int(train), _ptr(ws), _ptr(rgb), _ptr(sig),
+                                 _stream(dev)))
+        ctx.keep = (desc, n, flat, ws)
+        return rgb, sig
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_sig):
+        desc, n, flat, ws = ctx.keep
+        grad = torch.empty_like(flat)
+        g_rgb = None if g_rgb is None else g_rgb.contiguous()
+        g_sig = None if g_sig is None else g_sig.contiguous()
+        if ws is None:
+            grad.zero_()
+        else:
+            _check(lib().den_ngp_bwd(ctypes.byref(desc), n, _ptr(flat), _ptr(ws), _ptr(g_rgb), _ptr(g_sig),
+                                     _ptr(grad), _stream(flat.device)))
+        ctx.keep = None
+        return grad, None, None, None, None, None, None, None, None
+
+
+def ngp_field(flat, desc, x, d, density_only=False):
+    """-> rgb (n, rd), sigma (n) at positions x (n,3) viewed along d (n,3)."""
+    return NgpFieldFunction.apply(flat, desc, 1, x.float().contiguous(), d.float().contiguous(), None, None, None,
+                                  density_only)
+
+
+def ngp_field_packed(flat, desc, rays_o, rays_d, ray_indices, t_starts, t_ends, density_only=False):
+    """-> rgb (n, rd), sigma (n) at packed ray-marching samples (external/utils.py:83-96)."""
+    return NgpFieldFunction.apply(flat, desc, 2, rays_o.float().contiguous(), rays_d.float().contiguous(),
+                                  ray_indices.reshape(-1).to(torch.int32).contiguous(),
+                                  t_starts.reshape(-1).float().contiguous(), t_ends.reshape(-1).float().contiguous(),
+                                  density_only)
+
+
+class HashGridFunction(torch.autograd.Function):
+    """tcnn.Encoding (HashGrid / DenseGrid, Linear): x (n,3) in [0,1] -> (n, 2 n_levels)."""
+
+    @staticmethod
+    def forward(ctx, table, desc, x):
+        _require_device(table, x)
+        n = x.shape[0]
+        out = torch.empty(n, 2 * desc.n_levels, dtype=torch.float32, device=x.device)
+        _check(lib().den_hashgrid_fwd(ctypes.byref(desc), n, _ptr(x), _ptr(table), _ptr(out), _stream(x.device)))
+        ctx.keep = (desc, x, table.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        desc, x, shape = ctx.keep
+        d_table = torch.zeros(shape, dtype=torch.float32, device=x.device)
+        _check(lib().den_hashgrid_bwd(ctypes.byref(desc), x.shape[0], _ptr(x), _ptr(g.contiguous()), _ptr(d_table),
+                                      _stream(x.device)))
+        return d_table, None, None
+
+
+def hashgrid(table, desc, x):
+    return HashGridFunction.apply(table, desc, x.float().contiguous())
 
 
 # ----------------------------------------------------------------------------- reductions / adam

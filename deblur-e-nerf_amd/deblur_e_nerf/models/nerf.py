@@ -64,8 +64,11 @@ class NeRF(torch.nn.Module):
         assert cone_angle >= 0 and 0 <= early_stop_eps <= 1 and 0 <= alpha_thre <= 1
         assert test_chunk_size > 0 and num_dim > 0 and radiance_dim > 0 and opacity_eps > 0
         assert sampler in ("occupancy", "fixed")
-        if arch != "mlp":
-            raise NotImplementedError("the ngp arch (tcnn HashGrid) is out of scope; use arch: mlp")
+        if arch not in ("mlp", "ngp"):
+            raise NotImplementedError(f"unknown arch {arch!r} (nerf.py:105-164: ngp or mlp)")
+        if arch == "ngp" and sampler != "occupancy":
+            raise NotImplementedError("the fixed-count sampler runs the fused `mlp` arch; the ngp field marches "
+                                      "with the occupancy grid (the reference's sampler)")
         if sampler == "fixed" and contraction_id(contraction_type) != 0:
             raise NotImplementedError("the fixed-count sampler marches the AABB: use contraction_type AABB")
         self.register_buffer("aabb", torch.tensor(aabb), persistent=False)
@@ -91,6 +94,21 @@ class NeRF(torch.nn.Module):
         # the occupancy grid (nerf.py:98-102)
         resolution = occ_grid_config.resolution if occ_grid_config is not None else 128
         self.occupancy_grid = OccupancyGrid(roi_aabb=aabb, resolution=resolution, contraction_type=contraction_type)
+        if arch == "ngp":
+            # nerf.py:105-142: the activation names resolved, the radiance dim from the sensor
+            base = dict(arch_config.mlp_base)
+            base["hidden_activation"] = self.HIDDEN_ACTIVATION_NAME_TO_FN[arch_config.mlp_base.hidden_activation]
+            base["density_activation"] = self.DENSITY_ACTIVATION_NAME_TO_FN[arch_config.mlp_base.density_activation]
+            head = dict(arch_config.mlp_head)
+            head["hidden_activation"] = self.HIDDEN_ACTIVATION_NAME_TO_FN[arch_config.mlp_head.hidden_activation]
+            head["radiance_activation"] = self.RADIANCE_ACTIVATION_NAME_TO_FN[
+                arch_config.mlp_head.radiance_activation]
+            head["output_dim"] = radiance_dim
+            self.radiance_field = ngp.NGPradianceField(
+                aabb=aabb, num_dim=num_dim, use_viewdirs=True, contraction_type=contraction_type,
+                pos_encoding_config=dict(arch_config.pos_encoding), dir_encoding_config=dict(arch_config.dir_encoding),
+                mlp_base_config=base, mlp_head_config=head)
+            return
         self.radiance_field = mlp.VanillaNeRFRadianceField(
             aabb=aabb,
             net_depth=arch_config.net_depth,

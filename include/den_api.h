@@ -46,6 +46,9 @@
  *                       render_weight_from_density + accumulate_along_rays)
  *   den_occ_*        <- nerfacc OccupancyGrid.every_n_step, called at
  *                       deblur_e_nerf/models/nerf.py:170-204
+ *   den_ngp_* / den_hashgrid_*
+ *                    <- deblur_e_nerf/external/ngp.py:109-280 NGPradianceField (tcnn.Encoding
+ *                       HashGrid + MLP + SHEncoder) forward / backward
  */
 #ifndef DEN_API_H
 #define DEN_API_H
@@ -386,6 +389,58 @@ int den_trajectory(int64_t n, int32_t C, const int64_t* cam_ts, const float* cam
 size_t den_image_error_workspace_bytes(int32_t n_img);
 int den_image_error(int32_t n_img, int64_t pixels, const float* pred, const float* target, void* workspace,
                     double* sse_sae, void* stream);
+
+/* ---------------------------------------------------------------- ngp radiance field
+ * The `ngp` arch (external/ngp.py:109-280 NGPradianceField, the default of configs/train/*.yaml):
+ * tiny-cuda-nn multiresolution grid encoding (tcnn.Encoding, otype HashGrid / DenseGrid, Linear
+ * interpolation, 2 features per level, <= 16 levels), mlp_base 32 -> 64 -> 1 + 15, SH degree 4,
+ * mlp_head 31 -> 64 -> 64 -> rd (n_neurons 64, 1 / 2 hidden layers, geo_feat_dim 15: the
+ * shipped configs; others are DEN_EUNSUPPORTED), shifted_trunc_exp density.
+ * Flat parameters (f32): the grid table (den_ngp_table_params floats, tcnn's level-major layout),
+ * then mlp_base.1.hidden_layers.0.{weight,bias}, mlp_base.1.output_layer.{weight,bias},
+ * mlp_head.hidden_layers.{0,1}.{weight,bias}, mlp_head.output_layer.{weight,bias} (torch (out, in)).
+ * Replaces: tcnn.Encoding forward / backward (CUDA) and the torch nn.Linear / SHEncoder /
+ * activation kernels of NGPradianceField.forward and its autograd backward. */
+typedef struct den_ngp_desc {
+  int32_t radiance_dim;          /* 1 or 3 */
+  int32_t n_levels;              /* 1..16 */
+  int32_t n_features_per_level;  /* 2 */
+  int32_t log2_hashmap_size;
+  int32_t base_resolution;
+  float per_level_scale;
+  int32_t grid_type;             /* 0 HashGrid, 1 DenseGrid */
+  int32_t hidden_activation;     /* 0 softplus(beta=100), 1 relu (models/nerf.py:17-20) */
+  int32_t radiance_activation;   /* 0 softplus(beta=1), 1 sigmoid (models/nerf.py:26-29) */
+  int32_t contraction;           /* 0 AABB, 1 UN_BOUNDED_TANH, 2 UN_BOUNDED_SPHERE */
+  float aabb[6];
+} den_ngp_desc;
+
+/* Grid-table floats (tcnn sizing: per level min(next_multiple(res^3, 8), 2^log2_hashmap_size)
+ * entries x 2) and all flat parameters; -1 for an unsupported descriptor. */
+int64_t den_ngp_table_params(const den_ngp_desc* desc);
+int64_t den_ngp_param_count(const den_ngp_desc* desc);
+/* Workspace of a training forward + backward over n samples (saved activations, per-layer
+ * gradients, weight-gradient partials); 0 for inference. */
+size_t den_ngp_workspace_bytes(const den_ngp_desc* desc, int64_t n, int32_t train);
+/* Field at n samples.  points = 1: x (n,3) positions and d (n,3) directions; points = 2: packed
+ * ray-marching samples, x / d = ray origins / unit directions (R,3), ray_idx (n) i32, t0 / t1 (n)
+ * (position o + d (t0 + t1) / 2, external/utils.py:83-96).  density_only skips the head (the
+ * marching pre-pass sigma_fn; out_rgb may be null).  train = 1 keeps what den_ngp_bwd needs in
+ * the workspace.  Outputs: rgb (n, rd), sigma (n). */
+int den_ngp_fwd(const den_ngp_desc* desc, int64_t n, int32_t points, const float* x, const float* d,
+                const int32_t* ray_idx, const float* t0, const float* t1, const float* params, int32_t density_only,
+                int32_t train, void* workspace, float* out_rgb, float* out_sigma, void* stream);
+/* Gradient of sum(d_rgb * rgb) + sum(d_sigma * sigma) w.r.t. the flat parameters of the last
+ * training forward over the same workspace.  grad_params is overwritten (the table part is
+ * cleared on the stream, then scattered with f32 atomics as tcnn does). */
+int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* workspace, const float* d_rgb,
+                const float* d_sigma, float* grad_params, void* stream);
+/* tcnn.Encoding alone: x (n,3) in [0,1] -> out (n, 2 n_levels); backward accumulates
+ * (atomic adds, caller zeroes) d_table += dL/dtable. */
+int den_hashgrid_fwd(const den_ngp_desc* desc, int64_t n, const float* x, const float* table, float* out,
+                     void* stream);
+int den_hashgrid_bwd(const den_ngp_desc* desc, int64_t n, const float* x, const float* d_out, float* d_table,
+                     void* stream);
 
 /* ---------------------------------------------------------------- reductions / optimizer */
 /* out[j] = sum_b partial[j*n_blocks + b] for j < n (deterministic order). */

@@ -778,11 +778,78 @@ def gen_ngp(rd=1, seed=21, cfg="small", contraction="aabb", hidden="softplus", r
          **out, **extra, **mlp_w)
 
 
+def gen_render_ngp(rd=1, seed=25, R=64, sigma_bias_shift=2.0):
+    """render_ngp_rd{rd}.npz -- the reference's NeRF.forward with arch "ngp" (models/nerf.py:105-142,
+    230-286 -> render_image -> rendering) in the chair configuration: the occupancy-grid update at
+    step 0, a training-mode render with its backward, and an eval render -- the flow of gen_render,
+    with oracle/tcnn.py as tcnn.Encoding (8 levels of 2^12 entries: the table is stored) and
+    oracle/nerfacc.py as nerfacc."""
+    from oracle import ngp as ongp
+    from oracle import nerfacc as onerfacc
+    from oracle import tcnn as otcnn
+    nerfm = _refload.load("models.nerf")
+    sys.modules["tinycudann"].Encoding = otcnn.Encoding
+    ED = sys.modules["easydict"].EasyDict
+    CT = sys.modules["nerfacc"].ContractionType
+    c = RENDER_CFG
+    arch = ED(pos_encoding=dict(NGP_SMALL), dir_encoding=dict(degree=4),
+              mlp_base=dict(hidden_activation="softplus", density_activation="shifted_trunc_exp", n_neurons=64,
+                            n_hidden_layers=1, geo_feat_dim=15, weight_norm=False),
+              mlp_head=dict(hidden_activation="softplus", radiance_activation="softplus", n_neurons=64,
+                            n_hidden_layers=2, weight_norm=False))
+    occ = ED(resolution=c["res"], occ_thre=0.01, ema_decay=0.95, warmup_steps=256, n=16)
+    nerf = nerfm.NeRF(c["aabb"], CT.AABB, occ, c["near"], c["far"], c["step"], "parameter", 0.0, 1e-4, 0.0, 16384,
+                      "ngp", arch, 3, rd)
+    p = ongp.build_params(rd, seed, dict(NGP_SMALL))
+    p["mlp_base.0.params"] = p["mlp_base.0.params"] * 1e3
+    rf = nerf.radiance_field
+    rf.load_state_dict(dict(p, aabb=rf.aabb), strict=True)
+    out = dict(seed=seed, rd=rd, res=c["res"], step=c["step"], aabb=np.array(c["aabb"]), near=c["near"], far=c["far"],
+               sigma_bias_shift=sigma_bias_shift, pos_encoding=np.array(json.dumps(NGP_SMALL)),
+               table=p["mlp_base.0.params"].numpy(), **{f"param:{k}": v.numpy() for k, v in p.items()
+                                                       if k != "mlp_base.0.params"})
+    o, d = _chair_rays(R, 33)
+    out.update(rays_o=o.numpy(), rays_d=d.numpy())
+    nerf.train()
+    torch.manual_seed(100)
+    nerf.update_occ_grid(step=0, T_wc_position=o)
+    grid = nerf.occupancy_grid
+    out.update(occ_u=grid.last_u.numpy(), occs=grid.occs.numpy(), binary=grid.binary.numpy())
+    with torch.no_grad():
+        rf.mlp_base[1].output_layer.bias[0] += sigma_bias_shift
+    r = c["res"]
+    cc = (torch.stack(torch.meshgrid(*[torch.arange(r)] * 3, indexing="ij"), -1).float() + 0.5) / r - 0.5
+    ball = (cc.norm(dim=-1) < 0.4) & ~((cc[..., 0] > 0.1) & (cc[..., 1].abs() < 0.1))
+    grid._binary = ball
+    out["binary_render"] = ball.numpy()
+    g = torch.Generator().manual_seed(43)
+    g_rad = torch.randn(R, rd, generator=g) if rd > 1 else torch.randn(R, generator=g)
+    g_op, g_dp = torch.randn(R, generator=g), torch.randn(R, generator=g)
+    torch.manual_seed(101)
+    rad, op, dp, mspr = nerf(o, d)
+    LAST = onerfacc.LAST
+    out.update(train_jitter=LAST["jitter"].numpy(), train_kept_ri=LAST["kept"][0].numpy(),
+               train_radiance=rad.detach().numpy(), train_opacity=op.detach().numpy(),
+               train_depth=dp.detach().numpy(), train_mspr=np.array(mspr), g_rad=g_rad.numpy(), g_op=g_op.numpy(),
+               g_dp=g_dp.numpy())
+    ((rad * g_rad).sum() + (op * g_op).sum() + (dp * g_dp).sum()).backward()
+    for k, prm in rf.named_parameters():
+        out[f"grad:{k}"] = prm.grad.detach().numpy()
+    out["grad_bkgd_orig"] = nerf.parametrizations.render_bkgd.original.grad.numpy()
+    nerf.eval()
+    with torch.no_grad():
+        rad, op, dp, mspr = nerf(o, d)
+    out.update(eval_radiance=rad.numpy(), eval_opacity=op.numpy(), eval_depth=dp.numpy(), eval_mspr=np.array(mspr))
+    save(f"render_ngp_rd{rd}.npz", **out)
+
+
 def gen_ngp_all():
     gen_ngp(1, 21, "small")
     gen_ngp(3, 22, "small", "sphere", "relu", "sigmoid")
     gen_ngp(3, 23, "small", "tanh")
     gen_ngp(3, 24, "default", n=256)
+    gen_render_ngp(1, 25)
+    gen_render_ngp(3, 26)
 
 
 if __name__ == "__main__" and len(sys.argv) > 1:

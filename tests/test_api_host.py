@@ -115,3 +115,31 @@ def test_oracle_roma_rotations_are_proper(golden_dir):
     q = torch.nn.functional.normalize(torch.randn(8, 4, dtype=torch.float64), dim=-1)
     m = oroma.unitquat_to_rotmat(oroma.quat_product(q, oroma.quat_conjugation(q)))
     assert torch.allclose(m, torch.eye(3, dtype=torch.float64).expand(8, 3, 3), atol=1e-12)
+
+
+def test_ngp_field_mirrors_reference_names(golden_dir):
+    """NGPradianceField (external/ngp.py mirror) has the reference's parameter names, shapes and
+    order (the golden's param_names come from the reference module), one flat buffer, and the
+    table size of tcnn's sizing."""
+    import numpy as np
+    from deblur_e_nerf.external import marching, ngp
+    from oracle import ngp as ongp
+    from oracle import tcnn as otcnn
+    z = np.load(os.path.join(golden_dir, "ngp_rd3_default.npz"))
+    f = ngp.NGPradianceField(aabb=[-1.5, -1.5, -1.5, 1.5, 1.5, 1.5], contraction_type=marching.ContractionType.AABB,
+                             pos_encoding_config=dict(ongp.POS_ENCODING),
+                             mlp_base_config=dict(ongp.MLP_BASE, hidden_activation=torch.nn.Softplus(beta=100),
+                                                  density_activation=ngp.shifted_trunc_exp),
+                             mlp_head_config=dict(ongp.MLP_HEAD, hidden_activation=torch.nn.Softplus(beta=100),
+                                                  radiance_activation=torch.nn.Softplus(beta=1), output_dim=3))
+    names = [k for k, _ in f.named_parameters()]
+    assert names == [str(k) for k in z["param_names"]]
+    assert f.mlp_base[0].params.numel() == otcnn.n_params(ongp.POS_ENCODING)
+    for k, v in f.named_parameters():
+        if k != "mlp_base.0.params":
+            assert tuple(v.shape) == z[f"param:{k}"].shape, k
+    flat = f.flat_params
+    assert all(p.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr() for p in f.parameters())
+    with pytest.raises(NotImplementedError):
+        ngp.NGPradianceField(aabb=[-1, -1, -1, 1, 1, 1], mlp_base_config=dict(ongp.MLP_BASE, n_neurons=32,
+                             hidden_activation=torch.nn.ReLU(), density_activation=ngp.shifted_trunc_exp))
