@@ -591,7 +591,7 @@ def synthetic_event_batch(N, S, seed, img=800, ts_lo=1.5e8, ts_hi=9.5e8):
     return dict(event=ev, normalized=nz)
 
 
-def ref_deblur_step_module(d, rd, seed, pixbw, S, ct_free, refr_free, res=24):
+def ref_deblur_step_module(d, rd, seed, pixbw, S, ct_free, refr_free, res=24, arch="mlp"):
     """The reference DeblurENeRF's training-path methods bound to a module assembled from the
     reference's own components (the constructor needs eval images and Lightning)."""
     dm = _refload.load("models.deblur_e_nerf")
@@ -628,7 +628,7 @@ def ref_deblur_step_module(d, rd, seed, pixbw, S, ct_free, refr_free, res=24):
         m.MULTI_PARAM_MODEL_COMPONENTS.append("pixel_bandwidth")
         for p in m.pixel_bandwidth.parameters():
             p.requires_grad_(False)
-    m.nerf = _ref_nerf(rd, seed, res)
+    m.nerf = _ref_nerf(rd, seed, res) if arch == "mlp" else _ref_nerf_ngp(rd, seed, res)[0]
     m.trajectory = trm.LinearTrajectory(cp)
     for c, free in (("contrast_threshold", ct_free), ("refractory_period", refr_free)):
         for p in getattr(m, c).parameters():
@@ -644,7 +644,7 @@ def ref_deblur_step_module(d, rd, seed, pixbw, S, ct_free, refr_free, res=24):
     return m
 
 
-def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None):
+def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp"):
     """step_*.npz -- the reference DeblurENeRF.training_step (deblur_e_nerf.py:396-586) run on a
     reference-shaped batch: event correction, supervision timestamps, the occupancy-grid update,
     render_log_intensity x 4 (trajectory, rays, NeRF.forward through render_image with the nerfacc
@@ -657,14 +657,17 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None):
     d = tempfile.mkdtemp(prefix="den_step_")
     write_dataset(d, cal, poses)
     batch = synthetic_event_batch(N, S if pixbw else 0, seed + 100)
-    out = dict(rd=rd, seed=seed, N=N, S=S, pixbw=pixbw, res=24, sigma_bias_shift=2.0,
+    out = dict(rd=rd, seed=seed, N=N, S=S, pixbw=pixbw, res=24, sigma_bias_shift=2.0, arch=np.array(arch),
                **{f"cal:{k}": v for k, v in cal.items()}, **{f"pose:{k}": v for k, v in poses.items()},
                **{f"event:{k}": v.numpy() for k, v in batch["event"].items()},
                **{f"normalized:{k}": v.numpy() for k, v in batch["normalized"].items()})
     for variant in ("full", "nopose"):
-        m = ref_deblur_step_module(d, rd, seed, pixbw, S, True, True)
+        m = ref_deblur_step_module(d, rd, seed, pixbw, S, True, True, arch=arch)
         with torch.no_grad():
-            m.nerf.radiance_field.mlp.sigma_layer.output_layer.bias.add_(2.0)
+            if arch == "mlp":
+                m.nerf.radiance_field.mlp.sigma_layer.output_layer.bias.add_(2.0)
+            else:
+                m.nerf.radiance_field.mlp_base[1].output_layer.bias[0] += 2.0
         m.train()
         if variant == "nopose":
             orig_forward = type(m.trajectory).forward
@@ -689,7 +692,16 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None):
                        loss=loss.detach().numpy(), mspr=np.array(float(m.train_batch_size) if hasattr(
                            m, "train_batch_size") else 0.0),
                        new_batch_size=np.array(m.trainer.datamodule.train_dataset.batch_size),
-                       **{f"jitter_{i}": j.numpy() for i, j in enumerate(jit)}, **_grad_pick(m.nerf))
+                       **{f"jitter_{i}": j.numpy() for i, j in enumerate(jit)})
+            if arch == "mlp":
+                out.update(_grad_pick(m.nerf))
+            else:
+                rf = m.nerf.radiance_field
+                out.update({f"grad:{k}": prm.grad.detach().numpy() for k, prm in rf.named_parameters()})
+                out.update({f"param:{k}": prm.detach().numpy() for k, prm in rf.named_parameters()
+                            if k != "mlp_base.0.params"})
+                out["table"] = rf.mlp_base[0].params.detach().numpy()
+                out["pos_encoding"] = np.array(json.dumps(NGP_SMALL))
             out["grad_bkgd_orig"] = m.nerf.parametrizations.render_bkgd.original.grad.numpy()
             ctp = m.contrast_threshold.parametrizations
             out["d_p2n_orig"] = ctp.p2n_contrast_threshold_ratio.original.grad.numpy()
@@ -713,6 +725,11 @@ def gen_mlp_unbounded():
 # ----------------------------------------------------------------------------
 NGP_SMALL = dict(otype="HashGrid", n_levels=8, n_features_per_level=2, log2_hashmap_size=12, base_resolution=16,
                  per_level_scale=1.4472692012786865, interpolation="Linear")
+NGP_ARCH = dict(pos_encoding=dict(NGP_SMALL), dir_encoding=dict(degree=4),
+                mlp_base=dict(hidden_activation="softplus", density_activation="shifted_trunc_exp", n_neurons=64,
+                              n_hidden_layers=1, geo_feat_dim=15, weight_norm=False),
+                mlp_head=dict(hidden_activation="softplus", radiance_activation="softplus", n_neurons=64,
+                              n_hidden_layers=2, weight_norm=False))
 
 
 def gen_ngp(rd=1, seed=21, cfg="small", contraction="aabb", hidden="softplus", radiance="softplus", n=512):
@@ -778,32 +795,37 @@ def gen_ngp(rd=1, seed=21, cfg="small", contraction="aabb", hidden="softplus", r
          **out, **extra, **mlp_w)
 
 
-def gen_render_ngp(rd=1, seed=25, R=64, sigma_bias_shift=2.0):
-    """render_ngp_rd{rd}.npz -- the reference's NeRF.forward with arch "ngp" (models/nerf.py:105-142,
-    230-286 -> render_image -> rendering) in the chair configuration: the occupancy-grid update at
-    step 0, a training-mode render with its backward, and an eval render -- the flow of gen_render,
-    with oracle/tcnn.py as tcnn.Encoding (8 levels of 2^12 entries: the table is stored) and
-    oracle/nerfacc.py as nerfacc."""
+def _ref_nerf_ngp(rd, seed, res):
+    """The reference NeRF with arch "ngp" (models/nerf.py:105-142) in the chair configuration,
+    oracle/tcnn.py as tcnn.Encoding (NGP_SMALL: 8 levels of 2^12 entries), weights from
+    oracle/ngp.build_params(seed) with the table x 1e3 -> (nerf, params)."""
     from oracle import ngp as ongp
-    from oracle import nerfacc as onerfacc
     from oracle import tcnn as otcnn
     nerfm = _refload.load("models.nerf")
     sys.modules["tinycudann"].Encoding = otcnn.Encoding
     ED = sys.modules["easydict"].EasyDict
     CT = sys.modules["nerfacc"].ContractionType
     c = RENDER_CFG
-    arch = ED(pos_encoding=dict(NGP_SMALL), dir_encoding=dict(degree=4),
-              mlp_base=dict(hidden_activation="softplus", density_activation="shifted_trunc_exp", n_neurons=64,
-                            n_hidden_layers=1, geo_feat_dim=15, weight_norm=False),
-              mlp_head=dict(hidden_activation="softplus", radiance_activation="softplus", n_neurons=64,
-                            n_hidden_layers=2, weight_norm=False))
-    occ = ED(resolution=c["res"], occ_thre=0.01, ema_decay=0.95, warmup_steps=256, n=16)
+    occ = ED(resolution=res, occ_thre=0.01, ema_decay=0.95, warmup_steps=256, n=16)
     nerf = nerfm.NeRF(c["aabb"], CT.AABB, occ, c["near"], c["far"], c["step"], "parameter", 0.0, 1e-4, 0.0, 16384,
-                      "ngp", arch, 3, rd)
+                      "ngp", ED(NGP_ARCH), 3, rd)
     p = ongp.build_params(rd, seed, dict(NGP_SMALL))
     p["mlp_base.0.params"] = p["mlp_base.0.params"] * 1e3
     rf = nerf.radiance_field
     rf.load_state_dict(dict(p, aabb=rf.aabb), strict=True)
+    return nerf, p
+
+
+def gen_render_ngp(rd=1, seed=25, R=64, sigma_bias_shift=2.0):
+    """render_ngp_rd{rd}.npz -- the reference's NeRF.forward with arch "ngp" (models/nerf.py:105-142,
+    230-286 -> render_image -> rendering) in the chair configuration: the occupancy-grid update at
+    step 0, a training-mode render with its backward, and an eval render -- the flow of gen_render,
+    with oracle/tcnn.py as tcnn.Encoding (8 levels of 2^12 entries: the table is stored) and
+    oracle/nerfacc.py as nerfacc."""
+    from oracle import nerfacc as onerfacc
+    c = RENDER_CFG
+    nerf, p = _ref_nerf_ngp(rd, seed, c["res"])
+    rf = nerf.radiance_field
     out = dict(seed=seed, rd=rd, res=c["res"], step=c["step"], aabb=np.array(c["aabb"]), near=c["near"], far=c["far"],
                sigma_bias_shift=sigma_bias_shift, pos_encoding=np.array(json.dumps(NGP_SMALL)),
                table=p["mlp_base.0.params"].numpy(), **{f"param:{k}": v.numpy() for k, v in p.items()
@@ -850,6 +872,7 @@ def gen_ngp_all():
     gen_ngp(3, 24, "default", n=256)
     gen_render_ngp(1, 25)
     gen_render_ngp(3, 26)
+    gen_step(False, 1, seed=7, tag="step_ngp_nopixbw_rd1.npz", arch="ngp")
 
 
 if __name__ == "__main__" and len(sys.argv) > 1:

@@ -26,6 +26,16 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+def _ngp_arch(z):
+    import json
+    from deblur_e_nerf.utils.easydict import EasyDict as ED
+    return ED(pos_encoding=json.loads(str(z["pos_encoding"])), dir_encoding=ED(degree=4),
+              mlp_base=ED(hidden_activation="softplus", density_activation="shifted_trunc_exp", n_neurons=64,
+                          n_hidden_layers=1, geo_feat_dim=15, weight_norm=False),
+              mlp_head=ED(hidden_activation="softplus", radiance_activation="softplus", n_neurons=64,
+                          n_hidden_layers=2, weight_norm=False))
+
+
 def build_model(z, mode="f32", sampler="occupancy"):
     from deblur_e_nerf.models.deblur_e_nerf import DeblurENeRF
     from deblur_e_nerf.utils.easydict import EasyDict as ED
@@ -41,6 +51,9 @@ def build_model(z, mode="f32", sampler="occupancy"):
                   near_plane=1.43, far_plane=6.63, render_step_size="auto", cone_angle=0.0, early_stop_eps=1e-4,
                   alpha_thre=0.0, test_chunk_size=16384, arch="mlp", mlp=ED(ARCH), load_state_dict=False,
                   freeze=False, compute_mode=mode, sampler=sampler)
+    arch = str(z["arch"]) if "arch" in z.files else "mlp"
+    if arch == "ngp":
+        nerf_cfg.arch, nerf_cfg.ngp = "ngp", _ngp_arch(z)
     m = DeblurENeRF(
         "test", ["novel_view"], 1, [0], 0.001, False, None,
         ED(parameterize_mean_ct=True, load_state_dict=False,
@@ -59,6 +72,13 @@ def build_model(z, mode="f32", sampler="occupancy"):
            relative_lr=ED(refractory_period=1e-3)),
         ED(algo="multi_step_lr", multi_step_lr=ED(milestones=[10], gamma=0.3), interval="epoch"),
         d, True, 131072)
+    if arch == "ngp":
+        rf = m.nerf.radiance_field
+        p = {k[len("param:"):]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param:")}
+        p["mlp_base.0.params"] = torch.from_numpy(z["table"])
+        # the fixture holds the field parameters the reference rendered with (density shift included)
+        rf.load_state_dict(dict(p, aabb=rf.aabb), strict=True)
+        return m.to(DEV)
     p = onerf.build_params(rd, int(z["seed"]))
     m.nerf.radiance_field.flat_params.copy_(flat_from_params(p, rd))
     m = m.to(DEV)
@@ -110,6 +130,42 @@ def test_training_step_matches_reference(golden_dir, fixture, monkeypatch):
         z["grad_bkgd_orig"])).abs().max())
     assert bk_abs <= 1e-6 and e_mct <= 5e-3
     assert abs(dtau - float(z["dtau_orig_nopose"])) <= 1e-15
+
+
+def test_training_step_ngp_matches_reference(golden_dir, monkeypatch):
+    """The same with nerf.arch = ngp (the configs' default field): the reference training_step
+    with its NGPradianceField (tcnn.Encoding restated by oracle/tcnn.py), F32 kernels here.
+    Loss and C+/C- gradient 1e-4; every field gradient (table included) 1e-3 tensor-wise."""
+    from deblur_e_nerf.external import marching
+    z = np.load(os.path.join(golden_dir, "step_ngp_nopixbw_rd1.npz"))
+    m = build_model(z)
+    m.train()
+    jit = [z[f"jitter_{i}"] for i in range(4)]
+    monkeypatch.setattr(marching, "_uniform", _Draws([z["occ_u"], np.concatenate(jit)]))
+    loss = m.training_step(_batch(z), 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    e_loss = abs(float(loss) - float(z["loss"])) / abs(float(z["loss"]))
+    print(f"[ngp step] loss {float(loss):.7f} vs {float(z['loss']):.7f}; batch size {m.train_batch_size} vs "
+          f"{int(z['new_batch_size'])}; occs err {float((m.nerf.occupancy_grid.occs.cpu() - torch.from_numpy(z['occs'])).abs().max()):.3e}"
+          f" binary {float(m.nerf.occupancy_grid.binary.float().mean()):.4f} vs {float(z['binary'].mean()):.4f}")
+    assert e_loss <= 1e-4, (float(loss), float(z["loss"]))
+    assert abs(m.train_batch_size - int(z["new_batch_size"])) <= 1
+    gerr = {}
+    for k, p in m.nerf.radiance_field.named_parameters():
+        ref = torch.from_numpy(z[f"grad:{k}"]).double()
+        gerr[k] = float((p.grad.detach().cpu().double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+    e_p2n = norm_rel(m.contrast_threshold.parametrizations.p2n_contrast_threshold_ratio.original.grad, z["d_p2n_orig"])
+    # the radiance output bias gradient is one sum of per-sample terms of both signs (cancellation-
+    # limited, like the background's): bounded against the scale of its layer's weight gradient
+    k = "mlp_head.output_layer"
+    gb = dict(m.nerf.radiance_field.named_parameters())[k + ".bias"].grad.detach().cpu().double()
+    b_abs = float((gb - torch.from_numpy(z[f"grad:{k}.bias"]).double()).abs().max())
+    b_scale = float(np.abs(z[f"grad:{k}.weight"]).max())
+    gerr.pop(k + ".bias")
+    print(f"[ngp step] loss err {e_loss:.2e}, C+/C- {e_p2n:.2e}, field grads {gerr}, output bias abs {b_abs:.2e} "
+          f"(layer scale {b_scale:.2e})")
+    assert max(gerr.values()) <= 1e-3 and e_p2n <= 1e-4 and b_abs <= 1e-3 * b_scale
 
 
 def test_configure_optimizers_and_fit_step(golden_dir, monkeypatch):
