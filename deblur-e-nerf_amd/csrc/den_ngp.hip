@@ -136,8 +136,8 @@ typedef const __attribute__((address_space(4))) float* ngp_cptr;
 __device__ __forceinline__ ngp_cptr ngp_const(const float* p) { return (ngp_cptr)p; }
 
 // y = W x + b, W row-major (OUT, LD), first IN columns (uniform weights: scalar loads)
-template <int OUT, int IN, int LD>
-__device__ __forceinline__ void ngp_linear(ngp_cptr W, ngp_cptr b, const float* x, float* y) {
+template <int OUT, int IN, int LD, typename Ptr>
+__device__ __forceinline__ void ngp_linear(Ptr W, Ptr b, const float* x, float* y) {
 #pragma unroll
   for (int o = 0; o < OUT; ++o) {
     float acc = 0.0f;
@@ -147,35 +147,74 @@ __device__ __forceinline__ void ngp_linear(ngp_cptr W, ngp_cptr b, const float* 
   }
 }
 // layer 0: the encoding width E = 2 n_levels <= NGP_ENC is a runtime (wave-uniform) row length
-__device__ __forceinline__ void ngp_linear_enc(ngp_cptr W, ngp_cptr b, const float* x, float* y, int E) {
+template <typename Ptr>
+__device__ __forceinline__ void ngp_linear_enc(Ptr W, Ptr b, const float* x, float* y, int E, int LD) {
 #pragma unroll
   for (int o = 0; o < NGP_W; ++o) {
     float acc = 0.0f;
 #pragma unroll
     for (int i = 0; i < NGP_ENC; ++i)
-      if (i < E) acc = fmaf(W[o * E + i], x[i], acc);
+      if (i < E) acc = fmaf(W[o * LD + i], x[i], acc);
     y[o] = acc + b[o];
   }
 }
-__device__ __forceinline__ void ngp_linear_enc_t(ngp_cptr W, const float* dy, float* dx, int E) {
+template <typename Ptr>
+__device__ __forceinline__ void ngp_linear_enc_t(Ptr W, const float* dy, float* dx, int E, int LD) {
 #pragma unroll
   for (int i = 0; i < NGP_ENC; ++i) dx[i] = 0.0f;
 #pragma unroll
   for (int o = 0; o < NGP_W; ++o)
 #pragma unroll
     for (int i = 0; i < NGP_ENC; ++i)
-      if (i < E) dx[i] = fmaf(W[o * E + i], dy[o], dx[i]);
+      if (i < E) dx[i] = fmaf(W[o * LD + i], dy[o], dx[i]);
 }
 
 // dx = W^T dy (OUT rows of W, first IN columns), rows streamed in order
-template <int OUT, int IN, int LD>
-__device__ __forceinline__ void ngp_linear_t(ngp_cptr W, const float* dy, float* dx) {
+template <int OUT, int IN, int LD, typename Ptr>
+__device__ __forceinline__ void ngp_linear_t(Ptr W, const float* dy, float* dx) {
 #pragma unroll
   for (int i = 0; i < IN; ++i) dx[i] = 0.0f;
 #pragma unroll
   for (int o = 0; o < OUT; ++o)
 #pragma unroll
     for (int i = 0; i < IN; ++i) dx[i] = fmaf(W[o * LD + i], dy[o], dx[i]);
+}
+
+// Where the MLP weights come from.  Default (DEN_NGP_LDS 0): wave-uniform scalar loads through the
+// constant address space (SGPR operands of v_fmac_f32).  DEN_NGP_LDS 1: an LDS image staged per
+// workgroup, rows padded to multiples of 4 floats (layer 0 to 32 columns, the 31-wide head input to
+// 32) and read as wave-wide broadcasts.  Measured (profiles/ngp_parts.py, 2^19 samples, synthetic.yaml
+// config): field forward 2.91 ms scalar vs 10.6 ms LDS, density-only 1.28 vs 2.60 ms -- the
+// broadcast reads occupy the LDS->VGPR path for every weight of every wave.
+#ifndef DEN_NGP_LDS
+#define DEN_NGP_LDS 0
+#endif
+constexpr int NL_W0 = 0, NL_B0 = NL_W0 + NGP_W * NGP_ENC;
+constexpr int NL_W1 = NL_B0 + NGP_W, NL_B1 = NL_W1 + (1 + NGP_GEO) * NGP_W;
+constexpr int NL_W2 = NL_B1 + 1 + NGP_GEO, NL_B2 = NL_W2 + NGP_W * 32;
+constexpr int NL_W3 = NL_B2 + NGP_W, NL_B3 = NL_W3 + NGP_W * NGP_W;
+constexpr int NL_W4 = NL_B3 + NGP_W, NL_B4 = NL_W4 + 3 * NGP_W;
+constexpr int NL_FLOATS = NL_B4 + 4;
+static_assert(NL_W1 % 4 == 0 && NL_W2 % 4 == 0 && NL_W3 % 4 == 0 && NL_W4 % 4 == 0, "b128-aligned rows");
+
+__device__ __forceinline__ void ngp_stage_layer(const float* __restrict__ g, int out, int in, int ld, float* lds) {
+  for (int q = threadIdx.x; q < out * ld; q += blockDim.x) {
+    const int o = q / ld, i = q - o * ld;
+    lds[q] = i < in ? g[o * in + i] : 0.0f;
+  }
+}
+__device__ __forceinline__ void ngp_stage(const float* __restrict__ mlp, const NgpOff& off, int E, int rd, float* wl) {
+  const int in[5] = {E, NGP_W, NGP_HIN, NGP_W, NGP_W};
+  const int out[5] = {NGP_W, 1 + NGP_GEO, NGP_W, NGP_W, rd};
+  const int ld[5] = {NGP_ENC, NGP_W, 32, NGP_W, NGP_W};
+  const int lw[5] = {NL_W0, NL_W1, NL_W2, NL_W3, NL_W4};
+  const int lb[5] = {NL_B0, NL_B1, NL_B2, NL_B3, NL_B4};
+#pragma unroll
+  for (int l = 0; l < 5; ++l) {
+    ngp_stage_layer(mlp + off.w[l], out[l], in[l], ld[l], wl + lw[l]);
+    for (int q = threadIdx.x; q < out[l]; q += blockDim.x) wl[lb[l] + q] = mlp[off.b[l] + q];
+  }
+  __syncthreads();
 }
 
 // SHEncoder (external/sh_encoder.py:27-80), degree 4, the reference's f32 operation order
@@ -306,10 +345,27 @@ __device__ __forceinline__ void ngp_point(const NgpArgs& A, int64_t i, float* xn
 }
 
 // ------------------------------------------------------------------ forward
+#if DEN_NGP_LDS
+#define NGP_W_(l) (wl + NL_W##l)
+#define NGP_B_(l) (wl + NL_B##l)
+#define NGP_LD0 NGP_ENC
+#define NGP_LD2 32
+#else
+#define NGP_W_(l) (P + A.off.w[l])
+#define NGP_B_(l) (P + A.off.b[l])
+#define NGP_LD0 A.enc
+#define NGP_LD2 NGP_HIN
+#endif
+
 __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= A.n) return;
+#if DEN_NGP_LDS
+  __shared__ __attribute__((aligned(16))) float wl[NL_FLOATS];
+  ngp_stage(A.mlp, A.off, A.enc, A.rd, wl);
+#else
   const ngp_cptr P = ngp_const(A.mlp);
+#endif
+  if (i >= A.n) return;
   float xn[3], sel, dir[3];
   ngp_point(A, i, xn, &sel, dir);
   float feat[NGP_ENC];
@@ -325,7 +381,7 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
   float h0[NGP_W];
   {
     float h0p[NGP_W];
-    ngp_linear_enc(P + A.off.w[0], P + A.off.b[0], feat, h0p, A.enc);
+    ngp_linear_enc(NGP_W_(0), NGP_B_(0), feat, h0p, A.enc, NGP_LD0);
 #pragma unroll
     for (int o = 0; o < NGP_W; ++o) h0[o] = ngp_act(h0p[o], relu);
     if (S) {
@@ -337,7 +393,7 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
     }
   }
   float ob[1 + NGP_GEO];
-  ngp_linear<1 + NGP_GEO, NGP_W, NGP_W>(P + A.off.w[1], P + A.off.b[1], h0, ob);
+  ngp_linear<1 + NGP_GEO, NGP_W, NGP_W>(NGP_W_(1), NGP_B_(1), h0, ob);
   // shifted_trunc_exp(o0) * selector; selected (not multiplied) so an overflow outside the box is 0
   const float sigma = sel != 0.0f ? expf(ob[0] - 1.0f) : 0.0f;
   A.out_sigma[i] = sigma;
@@ -360,7 +416,7 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
   float h1[NGP_W];
   {
     float h1p[NGP_W];
-    ngp_linear<NGP_W, NGP_HIN, NGP_HIN>(P + A.off.w[2], P + A.off.b[2], hin, h1p);
+    ngp_linear<NGP_W, NGP_HIN, NGP_LD2>(NGP_W_(2), NGP_B_(2), hin, h1p);
 #pragma unroll
     for (int o = 0; o < NGP_W; ++o) h1[o] = ngp_act(h1p[o], relu);
     if (S) {
@@ -374,7 +430,7 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
   float h2[NGP_W];
   {
     float h2p[NGP_W];
-    ngp_linear<NGP_W, NGP_W, NGP_W>(P + A.off.w[3], P + A.off.b[3], h1, h2p);
+    ngp_linear<NGP_W, NGP_W, NGP_W>(NGP_W_(3), NGP_B_(3), h1, h2p);
 #pragma unroll
     for (int o = 0; o < NGP_W; ++o) h2[o] = ngp_act(h2p[o], relu);
     if (S) {
@@ -386,8 +442,8 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
     }
   }
   float r[3] = {0.f, 0.f, 0.f};
-  if (A.rd == 3) ngp_linear<3, NGP_W, NGP_W>(P + A.off.w[4], P + A.off.b[4], h2, r);
-  else ngp_linear<1, NGP_W, NGP_W>(P + A.off.w[4], P + A.off.b[4], h2, r);
+  if (A.rd == 3) ngp_linear<3, NGP_W, NGP_W>(NGP_W_(4), NGP_B_(4), h2, r);
+  else ngp_linear<1, NGP_W, NGP_W>(NGP_W_(4), NGP_B_(4), h2, r);
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     if (c < A.rd) {
@@ -403,8 +459,13 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
 // (tcnn kernel_grid_backward: atomicAdd of weight * dy per corner and feature)
 __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpArgs A) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= A.n) return;
+#if DEN_NGP_LDS
+  __shared__ __attribute__((aligned(16))) float wl[NL_FLOATS];
+  ngp_stage(A.mlp, A.off, A.enc, A.rd, wl);
+#else
   const ngp_cptr P = ngp_const(A.mlp);
+#endif
+  if (i >= A.n) return;
   const float* S = A.save;
   const int64_t n = A.n;
   const int relu = A.hidden_relu;
@@ -428,21 +489,21 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpArgs A) {
   for (int c = 0; c < 3; ++c) D[(ND_R + c) * n + i] = dr[c];
   // head output layer -> h2 -> h1 -> head input
   float dh[NGP_W], dz[NGP_W];
-  if (A.rd == 3) ngp_linear_t<3, NGP_W, NGP_W>(P + A.off.w[4], dr, dh);
-  else ngp_linear_t<1, NGP_W, NGP_W>(P + A.off.w[4], dr, dh);
+  if (A.rd == 3) ngp_linear_t<3, NGP_W, NGP_W>(NGP_W_(4), dr, dh);
+  else ngp_linear_t<1, NGP_W, NGP_W>(NGP_W_(4), dr, dh);
 #pragma unroll
   for (int o = 0; o < NGP_W; ++o) {
     dz[o] = dh[o] * ngp_dact(S[(NS_H2P + o) * n + i], S[(NS_H2 + o) * n + i], relu);
     D[(ND_Z3 + o) * n + i] = dz[o];
   }
-  ngp_linear_t<NGP_W, NGP_W, NGP_W>(P + A.off.w[3], dz, dh);
+  ngp_linear_t<NGP_W, NGP_W, NGP_W>(NGP_W_(3), dz, dh);
 #pragma unroll
   for (int o = 0; o < NGP_W; ++o) {
     dz[o] = dh[o] * ngp_dact(S[(NS_H1P + o) * n + i], S[(NS_H1 + o) * n + i], relu);
     D[(ND_Z2 + o) * n + i] = dz[o];
   }
   float dhin[NGP_HIN];
-  ngp_linear_t<NGP_W, NGP_HIN, NGP_HIN>(P + A.off.w[2], dz, dhin);
+  ngp_linear_t<NGP_W, NGP_HIN, NGP_LD2>(NGP_W_(2), dz, dhin);
   // base output: density (trunc_exp backward clamps the exponent at 15) and the geo features
   float dob[1 + NGP_GEO];
   {
@@ -455,14 +516,14 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpArgs A) {
   for (int g = 0; g < NGP_GEO; ++g) dob[1 + g] = dhin[NGP_SH + g];
 #pragma unroll
   for (int o = 0; o < 1 + NGP_GEO; ++o) D[(ND_O + o) * n + i] = dob[o];
-  ngp_linear_t<1 + NGP_GEO, NGP_W, NGP_W>(P + A.off.w[1], dob, dh);
+  ngp_linear_t<1 + NGP_GEO, NGP_W, NGP_W>(NGP_W_(1), dob, dh);
 #pragma unroll
   for (int o = 0; o < NGP_W; ++o) {
     dz[o] = dh[o] * ngp_dact(S[(NS_H0P + o) * n + i], S[(NS_H0 + o) * n + i], relu);
     D[(ND_Z0 + o) * n + i] = dz[o];
   }
   float dfeat[NGP_ENC];
-  ngp_linear_enc_t(P + A.off.w[0], dz, dfeat, A.enc);
+  ngp_linear_enc_t(NGP_W_(0), dz, dfeat, A.enc, NGP_LD0);
   // hash-table scatter
   float xn[3];
 #pragma unroll
