@@ -1,0 +1,16 @@
+# Round 2, call I: the final round-2 kernels (16-wave streamed dW, split-group reduction, deferred layer tails), the PSNR leg,
+# kernel-trace stats, HBM traffic and MFMA-utilisation PMC passes.
+set -e
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 420 python bench.py --steps 20 --warmup 3 > gpurun_out/b1.log 2>&1
+timeout -k 10 60 rocprofv3 -L > gpurun_out/counters.txt 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-gemm-peak > gpurun_out/prof.log 2>&1
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak > gpurun_out/pmc_fetch.log 2>&1
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak > gpurun_out/pmc_write.log 2>&1
+PMC1=$(python profiles/pick_counters.py gpurun_out/counters.txt SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE)
+echo "pass1: $PMC1" > gpurun_out/pmc_sets.txt
+timeout -s KILL 150 rocprofv3 --pmc $PMC1 --output-format csv -d gpurun_out/pmc_mfma -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak > gpurun_out/pmc_mfma.log 2>&1
+PMC2=$(python profiles/pick_counters.py gpurun_out/counters.txt SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE)
+echo "pass2: $PMC2" >> gpurun_out/pmc_sets.txt
+timeout -s KILL 150 rocprofv3 --pmc $PMC2 --output-format csv -d gpurun_out/pmc_mfma2 -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak > gpurun_out/pmc_mfma2.log 2>&1
