@@ -31,6 +31,9 @@ constexpr int HB_GRID_MAX = 256;
 #ifndef DEN_HB_DEPTH
 #define DEN_HB_DEPTH 3
 #endif
+#ifndef DEN_HB_OVL
+#define DEN_HB_OVL 0  // epilogue / dW overlap: 0 phases apart, 1 compiler order, 2 pinned interleave
+#endif
 #ifndef DEN_HB_PF
 #define DEN_HB_PF 4  // dz_l fragments read ahead of the chain MFMAs
 #endif
@@ -181,9 +184,11 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     *(bf16x8*)d = of[0];
     *(bf16x8*)(d + 1024) = of[1];
 #endif
+#if DEN_HB_OVL == 0
     // keep the scheduler from hoisting the next phase's LDS reads here (register pressure: W^T lives
     // in 128 VGPRs and dW in all 256 AGPRs for the whole launch)
     __builtin_amdgcn_sched_barrier(0);
+#endif
   }
   // weight / bias gradients over the block's 32 samples (two k-steps of 16)
 #pragma unroll
@@ -202,6 +207,17 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
       db[1] += (float)a1[j];
     }
   }
+#if DEN_HB_OVL == 2
+  // one wave per SIMD issues in order: the epilogue's VALU (derivative, bf16 packing) only overlaps
+  // the weight-gradient MFMAs if it is interleaved with them in the instruction stream
+  __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);  // DS reads: epilogue operands + first fragments
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // VALU
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+  }
+#endif
 }
 
 __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P) {
