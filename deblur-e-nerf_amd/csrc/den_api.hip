@@ -19,6 +19,7 @@
 #include "den_march.hip"
 #include "den_misc.hip"
 #include "den_ngp.hip"
+#include "den_ngp_mfma.hip"
 #include "den_pixbw.hip"
 #include "den_render.hip"
 
@@ -1140,6 +1141,12 @@ bool ngp_grid(const den_ngp_desc* d, NgpGrid* G, int64_t* table_floats) {
   return true;
 }
 
+// workgroups of the MFMA field kernels: one 32-sample tile per wave, capped (they loop)
+unsigned ngp_mf_grid(int64_t n) {
+  const int64_t wg = ((n + 31) / 32 + NM_WAVES - 1) / NM_WAVES;
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(wg, DEN_NGP_MF_GRID));
+}
+
 struct NgpWs {
   size_t save, dz, partial, total;
   int splits;
@@ -1215,7 +1222,11 @@ int den_ngp_fwd(const den_ngp_desc* desc, int64_t n, int32_t points, const float
   A.out_rgb = out_rgb;
   A.out_sigma = out_sigma;
   A.save = train ? (float*)((char*)workspace + ngp_ws(n).save) : nullptr;
+#if DEN_NGP_MFMA
+  hipLaunchKernelGGL(ngp_fwd_mfma_kernel, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, (hipStream_t)stream, A);
+#else
   hipLaunchKernelGGL(ngp_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
+#endif
   DEN_LAUNCHED();
   return DEN_OK;
 }
@@ -1248,7 +1259,11 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
   A.d_sigma = d_sigma;
   A.d_table = grad_params;
   A.dz = (float*)(ws + W.dz);
+#if DEN_NGP_MFMA
+  hipLaunchKernelGGL(ngp_bwd_mfma_kernel, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, st, A);
+#else
   hipLaunchKernelGGL(ngp_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
+#endif
   DEN_LAUNCHED();
   const int rd = desc->radiance_dim;
   NgpDwArgs P{};

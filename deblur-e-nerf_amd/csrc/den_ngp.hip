@@ -247,9 +247,18 @@ struct NgpCorner {
   float w[8];
 };
 
-__device__ __forceinline__ uint32_t ngp_index(const NgpGrid& G, int l, uint32_t cx, uint32_t cy, uint32_t cz) {
+// the grid constants of one level
+struct NgpLevel {
+  float scale;
+  uint32_t res, entries, offset;
+};
+__device__ __forceinline__ NgpLevel ngp_level(const NgpGrid& G, int l) {
+  return NgpLevel{G.scale[l], G.res[l], G.entries[l], G.offset[l]};
+}
+
+__device__ __forceinline__ uint32_t ngp_index(const NgpLevel& V, int hashed, uint32_t cx, uint32_t cy, uint32_t cz) {
   // grid_index: dense strides while the stride stays <= the level size, else the prime hash
-  const uint32_t size = G.entries[l], res = G.res[l];
+  const uint32_t size = V.entries, res = V.res;
   uint32_t stride = 1, index = 0;
   const uint32_t c[3] = {cx, cy, cz};
 #pragma unroll
@@ -261,17 +270,17 @@ __device__ __forceinline__ uint32_t ngp_index(const NgpGrid& G, int l, uint32_t 
       stride = 0xFFFFFFFFu;  // the loop has ended (stride > size stays true)
     }
   }
-  if (G.hashed && size < stride) index = cx ^ (cy * 2654435761u) ^ (cz * 805459861u);
+  if (hashed && size < stride) index = cx ^ (cy * 2654435761u) ^ (cz * 805459861u);
   return index % size;
 }
 
-__device__ __forceinline__ void ngp_corners(const NgpGrid& G, int l, const float* x, NgpCorner& C,
+__device__ __forceinline__ void ngp_corners(const NgpLevel& V, int hashed, const float* x, NgpCorner& C,
                                             uint32_t* cell_out = nullptr) {
   float frac[3];
   uint32_t cell[3];
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    float pos = fmaf(G.scale[l], x[d], 0.5f);
+    float pos = fmaf(V.scale, x[d], 0.5f);
     const float fl = floorf(pos);
     cell[d] = (uint32_t)(int)fl;
     frac[d] = pos - fl;
@@ -291,12 +300,16 @@ __device__ __forceinline__ void ngp_corners(const NgpGrid& G, int l, const float
       }
     }
     C.w[c] = w;
-    C.idx[c] = G.offset[l] + ngp_index(G, l, p[0], p[1], p[2]);
+    C.idx[c] = V.offset + ngp_index(V, hashed, p[0], p[1], p[2]);
   }
   if (cell_out) {
 #pragma unroll
     for (int d = 0; d < 3; ++d) cell_out[d] = cell[d];
   }
+}
+__device__ __forceinline__ void ngp_corners(const NgpGrid& G, int l, const float* x, NgpCorner& C,
+                                            uint32_t* cell_out = nullptr) {
+  ngp_corners(ngp_level(G, l), G.hashed, x, C, cell_out);
 }
 
 // Pre-aggregation of the table-gradient scatter: the samples of a wave are consecutive samples of
@@ -325,7 +338,7 @@ template <int K>
 __device__ __forceinline__ void ngp_fold_step(const uint32_t* cell, float* v, bool& alive, uint64_t active) {
   const int lane = threadIdx.x & 63;
   constexpr int M = (2 << K) - 1;
-  // a partner past n has returned: its registers are stale, so it never matches
+  // a partner past n (returned, or not `ok`) has stale registers: it never matches
   bool same = (active >> (lane ^ (1 << K))) & 1;
 #pragma unroll
   for (int d = 0; d < 3; ++d) same = same && (uint32_t)ngp_xlane<K>((int)cell[d], 0) == cell[d];
@@ -336,10 +349,11 @@ __device__ __forceinline__ void ngp_fold_step(const uint32_t* cell, float* v, bo
   }
   if ((lane & M) == (1 << K) && same) alive = false;
 }
-// -> whether this lane still issues its (folded) values
-__device__ __forceinline__ bool ngp_fold(const uint32_t* cell, float* v) {
-  bool alive = true;
-  const uint64_t active = __ballot(1);
+// -> whether this lane still issues its (folded) values; `ok` false: a lane past n (it issues nothing
+// and is nobody's partner)
+__device__ __forceinline__ bool ngp_fold(const uint32_t* cell, float* v, bool ok = true) {
+  bool alive = ok;
+  const uint64_t active = __ballot(ok);
   ngp_fold_step<0>(cell, v, alive, active);
   if constexpr (DEN_NGP_AGG_STEPS > 1) ngp_fold_step<1>(cell, v, alive, active);
   if constexpr (DEN_NGP_AGG_STEPS > 2) ngp_fold_step<2>(cell, v, alive, active);

@@ -1,0 +1,518 @@
+// den_ngp_mfma.hip -- the `ngp` field's MLPs on the matrix cores: v_mfma_f32_32x32x2_f32 (f32
+// operands, f32 accumulation, exact f32 products), forward and backward.  Same inputs, saved rows
+// and outputs as ngp_fwd_kernel / ngp_bwd_kernel (den_ngp.hip), which stay as the DEN_NGP_MFMA 0
+// build.
+//
+// Why: the per-lane formulation runs the 9.3 K MACs per sample as v_fmac_f32 with scalar weight
+// operands -- one FMA per lane per instruction behind a stream of scalar loads -- and measured
+// ~4 TF/s on the head MLP.  Here a wave owns 32 samples; features are the M (row) dimension, the 32
+// samples the N (column) dimension, and the weights the A operand:
+//   * lane (h = lane >> 5, j = lane & 31) supplies B[k = h][n = j]: for step s the activation of
+//     input feature col(s, h) of sample j, and A[m = j][k = h] = W[row m][col(s, h)];
+//   * accumulator register r of a 32-row tile t holds row 32 t + ngp_row(r, h) of sample j, so a
+//     layer's output registers ARE the next layer's B operands (step 16 t + r <-> feature
+//     32 t + ngp_row(r, h)): no cross-lane traffic between layers, only a permutation of W's columns;
+//   * the permuted weights ("images", ~50 KB forward / ~39 KB backward) are built once per
+//     workgroup in LDS from the flat parameters and read as one ds_read_b128 per 4 MFMAs;
+//   * each half of the wave runs the grid encoding of half of the levels of its 32 samples (the
+//     layer-0 B operand), and in the backward scatters the table gradient of the levels whose
+//     feature rows its accumulators hold.
+// Per 32 samples: 192 MFMAs forward (layers 64xE, 16x64, 64x31, 64x64, rdx64), 148 backward
+// (W^T products down to the encoding gradient).
+#include "den_device.h"
+
+namespace den {
+
+#ifndef DEN_NGP_MFMA
+#define DEN_NGP_MFMA 1
+#endif
+#ifndef DEN_NGP_MF_WAVES
+#define DEN_NGP_MF_WAVES 8  // waves (32-sample tiles in flight) per workgroup
+#endif
+#ifndef DEN_NGP_MF_GRID
+#define DEN_NGP_MF_GRID 1024  // workgroups at most (each loops over tiles; the image is built once)
+#endif
+constexpr int NM_WAVES = DEN_NGP_MF_WAVES, NM_THREADS = 64 * NM_WAVES;
+
+// accumulator register r of half h holds row ngp_row(r, h) of its 32-row tile
+__device__ __forceinline__ int ngp_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+// input feature of step s, half h, when the input is a 64-wide layer output (two tiles)
+__device__ __forceinline__ int ngp_col64(int s, int h) { return 32 * (s >> 4) + ngp_row(s & 15, h); }
+
+// Image sections: A operands [tile][step / 4][lane][4] (a lane's 4 consecutive steps are one b128),
+// then (forward) the biases in accumulator order [slot][half][16].
+constexpr int FI_A0 = 0, FI_A1 = FI_A0 + 2 * 16 * 64, FI_A2 = FI_A1 + 32 * 64, FI_A3 = FI_A2 + 2 * 16 * 64,
+              FI_A4 = FI_A3 + 2 * 32 * 64, FI_B = FI_A4 + 32 * 64, FI_FLOATS = FI_B + 8 * 32;
+constexpr int BI_A4 = 0, BI_A3 = BI_A4 + 2 * 4 * 64, BI_A2 = BI_A3 + 2 * 32 * 64, BI_A1 = BI_A2 + 32 * 64,
+              BI_A0 = BI_A1 + 2 * 8 * 64, BI_FLOATS = BI_A0 + 32 * 64;
+
+struct NgpSlot {
+  int t, s, j, h;
+};
+// q-th float of a section of S steps per tile
+__device__ __forceinline__ NgpSlot ngp_slot(int q, int S) {
+  const int t = q / (S * 64), rem = q - t * S * 64, w = rem & 255, lane = w >> 2;
+  return NgpSlot{t, (rem >> 8) * 4 + (w & 3), lane & 31, lane >> 5};
+}
+
+// Forward image.  Layer 0 (64 x E): half h holds the encoding of levels [h L0, ..); layer 1 (16 x 64):
+// one tile, rows >= 16 zero; layer 2 (64 x 31): steps 0..7 the SH values 8 h + s, steps 8..15 the base
+// output registers 0..7 (row ngp_row(s - 8, h); row 0, the density, has zero weight, geo row g is
+// head input 15 + g); layer 3 (64 x 64); layer 4 (rd x 64): rows >= rd zero.
+__device__ float ngp_fi(const float* __restrict__ mlp, const NgpOff& o, int E, int L0, int rd, int q) {
+  if (q < FI_A1) {
+    const NgpSlot z = ngp_slot(q - FI_A0, 16);
+    const int c = z.h ? 2 * L0 + z.s : z.s;
+    const bool v = z.h ? c < E : z.s < 2 * L0;
+    return v ? mlp[o.w[0] + (32 * z.t + z.j) * E + c] : 0.0f;
+  }
+  if (q < FI_A2) {
+    const NgpSlot z = ngp_slot(q - FI_A1, 32);
+    return z.j < 1 + NGP_GEO ? mlp[o.w[1] + z.j * NGP_W + ngp_col64(z.s, z.h)] : 0.0f;
+  }
+  if (q < FI_A3) {
+    const NgpSlot z = ngp_slot(q - FI_A2, 16);
+    int c;
+    if (z.s < 8) {
+      c = 8 * z.h + z.s;
+    } else {
+      const int g = ngp_row(z.s - 8, z.h);
+      c = g >= 1 ? NGP_SH - 1 + g : -1;
+    }
+    return c >= 0 ? mlp[o.w[2] + (32 * z.t + z.j) * NGP_HIN + c] : 0.0f;
+  }
+  if (q < FI_A4) {
+    const NgpSlot z = ngp_slot(q - FI_A3, 32);
+    return mlp[o.w[3] + (32 * z.t + z.j) * NGP_W + ngp_col64(z.s, z.h)];
+  }
+  if (q < FI_B) {
+    const NgpSlot z = ngp_slot(q - FI_A4, 32);
+    return z.j < rd ? mlp[o.w[4] + z.j * NGP_W + ngp_col64(z.s, z.h)] : 0.0f;
+  }
+  // bias slots: layer 0 tiles 0, 1 | layer 1 | layer 2 tiles 0, 1 | layer 3 tiles 0, 1 | layer 4
+  const int b = q - FI_B, k = b >> 5, h = (b >> 4) & 1, r = b & 15;
+  const int layer = k == 0 || k == 1 ? 0 : k == 2 ? 1 : k <= 4 ? 2 : k <= 6 ? 3 : 4;
+  const int t = k == 1 || k == 4 || k == 6 ? 1 : 0;
+  const int out = layer == 1 ? 1 + NGP_GEO : layer == 4 ? rd : NGP_W;
+  const int boff = layer == 0 ? o.b[0] : layer == 1 ? o.b[1] : layer == 2 ? o.b[2] : layer == 3 ? o.b[3] : o.b[4];
+  const int row = 32 * t + ngp_row(r, h);
+  return row < out ? mlp[boff + row] : 0.0f;
+}
+
+// Backward image: A[m][k] = W[k][m] (W^T).  W4^T: 2 tiles, steps s < 2 carry output 2 s + h (< rd);
+// W3^T: 2 tiles x 32 steps; W2^T: one tile whose row m in 1..15 is head input 15 + m (the geo
+// gradient lands on base-output row m; row 0 is the density's); W1^T: 2 tiles x 8 steps (the 16
+// base-output rows); W0^T: one tile of E rows.
+__device__ float ngp_bi(const float* __restrict__ mlp, const NgpOff& o, int E, int rd, int q) {
+  if (q < BI_A3) {
+    const NgpSlot z = ngp_slot(q - BI_A4, 4);
+    const int c = 2 * z.s + z.h;
+    return z.s < 2 && c < rd ? mlp[o.w[4] + c * NGP_W + 32 * z.t + z.j] : 0.0f;
+  }
+  if (q < BI_A2) {
+    const NgpSlot z = ngp_slot(q - BI_A3, 32);
+    return mlp[o.w[3] + ngp_col64(z.s, z.h) * NGP_W + 32 * z.t + z.j];
+  }
+  if (q < BI_A1) {
+    const NgpSlot z = ngp_slot(q - BI_A2, 32);
+    return z.j >= 1 && z.j <= NGP_GEO ? mlp[o.w[2] + ngp_col64(z.s, z.h) * NGP_HIN + NGP_SH - 1 + z.j] : 0.0f;
+  }
+  if (q < BI_A0) {
+    const NgpSlot z = ngp_slot(q - BI_A1, 8);
+    return mlp[o.w[1] + ngp_row(z.s, z.h) * NGP_W + 32 * z.t + z.j];
+  }
+  const NgpSlot z = ngp_slot(q - BI_A0, 32);
+  return z.j < E ? mlp[o.w[0] + ngp_col64(z.s, z.h) * E + z.j] : 0.0f;
+}
+
+__device__ __forceinline__ f32x16 ngp_mfma(float a, float b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+// acc[t] += A(section, tile t) B over the first `steps` steps (rounded up to 4; the weights of the
+// padding steps are zero), b[s] = this lane's B operand of step s
+template <int T, int S>
+__device__ __forceinline__ void ngp_mm(const float* sec, const float* b, f32x16* acc, int lane, int steps = S) {
+#pragma unroll
+  for (int g = 0; g < S / 4; ++g) {
+    if (4 * g >= steps) break;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const f32x4 a = *(const f32x4*)(sec + (t * S + 4 * g) * 64 + lane * 4);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[t] = ngp_mfma(a[u], b[4 * g + u], acc[t]);
+    }
+  }
+}
+__device__ __forceinline__ f32x16 ngp_bias(const float* img, int slot, int h) {
+  const float* p = img + FI_B + slot * 32 + h * 16;
+  f32x16 v;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const f32x4 q = *(const f32x4*)(p + 4 * u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[4 * u + e] = q[e];
+  }
+  return v;
+}
+__device__ __forceinline__ f32x16 ngp_zero16() {
+  f32x16 v;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) v[e] = 0.0f;
+  return v;
+}
+// level l0 + q of half 1, q of half 0 (both indices wave-uniform: scalar loads, then a select)
+__device__ __forceinline__ NgpLevel ngp_level_h(const NgpGrid& G, int q, int l1, int h) {
+  const NgpLevel a = ngp_level(G, q);
+  const NgpLevel b = ngp_level(G, l1 < NGP_MAX_LEVELS ? l1 : 0);
+  return h ? b : a;
+}
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(NM_THREADS) void ngp_fwd_mfma_kernel(NgpArgs A) {
+  __shared__ __attribute__((aligned(16))) float img[FI_FLOATS];
+  const int E = A.enc, L = A.grid.n_levels, L0 = (L + 1) / 2;
+  for (int q = threadIdx.x; q < FI_FLOATS; q += NM_THREADS) img[q] = ngp_fi(A.mlp, A.off, E, L0, A.rd, q);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int relu = A.hidden_relu;
+  const int64_t n = A.n;
+  float* S = A.save;
+  const int64_t ntiles = (n + 31) / 32;
+  const int nl = h ? L - L0 : L0;         // levels encoded by this half
+  const int fbase = h ? 2 * L0 : 0;       // their first feature
+  for (int64_t tile = (int64_t)blockIdx.x * NM_WAVES + (threadIdx.x >> 6); tile < ntiles;
+       tile += (int64_t)gridDim.x * NM_WAVES) {
+    const int64_t i = tile * 32 + j;
+    const bool ok = i < n;
+    const int64_t ic = ok ? i : n - 1;
+    // save rows: uniform row offsets (row * nn; nn is opaque per tile so they are not hoisted out of
+    // the loop as per-row registers) from a per-lane base; Sh adds this half's 4-row shift
+    int64_t nn = n;
+    asm volatile("" : "+s"(nn));
+    float* S0 = S ? S + i : nullptr;
+    float* Sh = S ? S + i + 4 * h * nn : nullptr;
+    float xn[3], sel, dir[3];
+    ngp_point(A, ic, xn, &sel, dir);
+    float feat[16];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float f0 = 0.0f, f1 = 0.0f;
+      if (q < nl) {
+        NgpCorner C;
+        ngp_corners(ngp_level_h(A.grid, q, L0 + q, h), A.grid.hashed, xn, C);
+        float2 v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = *(const float2*)(A.table + 2 * (int64_t)C.idx[c]);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          f0 = fmaf(C.w[c], v[c].x, f0);
+          f1 = fmaf(C.w[c], v[c].y, f1);
+        }
+      }
+      feat[2 * q] = f0;
+      feat[2 * q + 1] = f1;
+    }
+    if (S && ok) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+        if (s < 2 * nl) S0[(NS_FEAT + fbase + s) * nn] = feat[s];
+    }
+    // layer 0 (64 x E) + activation
+    float hb[32];
+    {
+      f32x16 acc[2] = {ngp_bias(img, 0, h), ngp_bias(img, 1, h)};
+      ngp_mm<2, 16>(img + FI_A0, feat, acc, lane, 2 * L0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pre = acc[t][r], a = ngp_act(pre, relu);
+          hb[16 * t + r] = a;
+          if (S && ok) {
+            const int row = 32 * t + ngp_row(r, 0);
+            Sh[(NS_H0P + row) * nn] = pre;
+            Sh[(NS_H0 + row) * nn] = a;
+          }
+        }
+    }
+    // layer 1 (16 x 64): density (row 0) and geo features
+    f32x16 ob[1] = {ngp_bias(img, 2, h)};
+    ngp_mm<1, 32>(img + FI_A1, hb, ob, lane);
+    if (h == 0 && ok) {
+      const float o0 = ob[0][0];
+      A.out_sigma[i] = sel != 0.0f ? expf(o0 - 1.0f) : 0.0f;
+      if (S) {
+        S0[NS_O0 * nn] = o0;
+        S0[NS_SEL * nn] = sel;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) S0[(NS_X + a) * nn] = xn[a];
+      }
+    }
+    if (A.density_only) continue;
+    // head input: SH values 8 h .. 8 h + 7, base-output registers 0..7
+    float hin[16];
+    {
+      float sh[NGP_SH];
+      ngp_sh4(dir, sh);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) hin[s] = h ? sh[8 + s] : sh[s];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) hin[8 + q] = ob[0][q];
+      if (S && ok) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) Sh[(NS_HIN + 4 * h + s) * nn] = hin[s];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          if (q > 0 || h > 0) Sh[(NS_HIN + NGP_SH - 1 + ngp_row(q, 0)) * nn] = hin[8 + q];
+        }
+      }
+    }
+    // head layers 2 (64 x 31) and 3 (64 x 64)
+    {
+      f32x16 acc[2] = {ngp_bias(img, 3, h), ngp_bias(img, 4, h)};
+      ngp_mm<2, 16>(img + FI_A2, hin, acc, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pre = acc[t][r], a = ngp_act(pre, relu);
+          hb[16 * t + r] = a;
+          if (S && ok) {
+            const int row = 32 * t + ngp_row(r, 0);
+            Sh[(NS_H1P + row) * nn] = pre;
+            Sh[(NS_H1 + row) * nn] = a;
+          }
+        }
+    }
+    {
+      f32x16 acc[2] = {ngp_bias(img, 5, h), ngp_bias(img, 6, h)};
+      ngp_mm<2, 32>(img + FI_A3, hb, acc, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pre = acc[t][r], a = ngp_act(pre, relu);
+          hb[16 * t + r] = a;
+          if (S && ok) {
+            const int row = 32 * t + ngp_row(r, 0);
+            Sh[(NS_H2P + row) * nn] = pre;
+            Sh[(NS_H2 + row) * nn] = a;
+          }
+        }
+    }
+    // output layer (rd x 64): rows 0..2 are registers 0..2 of half 0
+    f32x16 ro[1] = {ngp_bias(img, 7, h)};
+    ngp_mm<1, 32>(img + FI_A4, hb, ro, lane);
+    if (h == 0 && ok) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float r = ro[0][c];
+        if (c < A.rd)
+          A.out_rgb[i * A.rd + c] = A.rad_sigmoid ? __fdiv_rn(1.0f, 1.0f + expf(-r)) : (r > 20.0f ? r : log1pf(expf(r)));
+        if (S) S0[(NS_R + c) * nn] = r;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward
+// Table-gradient scatter, transposed over quads of lanes.  Float atomics execute at the memory side,
+// one 64-B request per distinct 64-B segment an instruction touches (MI355X_MICROARCH.md 'Global
+// float atomics': ~20 G requests/s chip-wide), so one lane per sample adding to 8 random corners is
+// 16 requests per sample-level.  Here the 4 lanes of a quad issue, per instruction, the 4 dwords of
+// one x-neighbour corner pair (2k, 2k + 1) of ONE sample (lane q: corner 2k + (q >> 1), feature
+// q & 1): the two features of an entry are always one request, and the pair is one 16-B aligned run
+// whenever the two entries are adjacent (dense levels away from the wrap; hashed levels with an even
+// x cell) -- 4..8 requests per sample-level instead of 16.  The values, indices and emit flags are
+// exchanged with quad_perm DPP moves (lane q receives from lane q ^ r).
+#ifndef DEN_NGP_SCATTER_QUAD
+#define DEN_NGP_SCATTER_QUAD 0
+#endif
+template <int R>
+__device__ __forceinline__ int ngp_qxor(int v) {
+  if constexpr (R == 0) return v;
+  else return __builtin_amdgcn_update_dpp(v, v, R == 1 ? 0xB1 : R == 2 ? 0x4E : 0x1B, 0xF, 0xF, false);
+}
+template <typename T>
+__device__ __forceinline__ T ngp_sel4(T x0, T x1, T x2, T x3, int i) {
+  return i == 0 ? x0 : i == 1 ? x1 : i == 2 ? x2 : x3;
+}
+__device__ __forceinline__ void ngp_scatter_quad(float* d_table, const uint32_t* idx, const float* v, bool emit) {
+  const int q = threadIdx.x & 3;
+  // rv[r][k] = v_{q^r}[4k + q]; ri[r][k] = idx_{q^r}[2k + (q >> 1)]; re[r] = emit_{q^r}
+  float rv[4][4];
+  uint32_t ri[4][4];
+  int re[4];
+#define NGP_QX(R)                                                                                         \
+  {                                                                                                       \
+    const int dst = q ^ R;                                                                                \
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                                       \
+      const float sv = ngp_sel4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3], dst);                 \
+      const uint32_t si = (dst >> 1) ? idx[2 * k + 1] : idx[2 * k];                                       \
+      rv[R][k] = __builtin_bit_cast(float, ngp_qxor<R>(__builtin_bit_cast(int, sv)));                     \
+      ri[R][k] = (uint32_t)ngp_qxor<R>((int)si);                                                          \
+    }                                                                                                     \
+    re[R] = ngp_qxor<R>(emit ? 1 : 0);                                                                    \
+  }
+  NGP_QX(0)
+  NGP_QX(1)
+  NGP_QX(2)
+  NGP_QX(3)
+#undef NGP_QX
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int r = q ^ s;  // sample s of the quad arrived through rotation q ^ s
+    if (ngp_sel4(re[0], re[1], re[2], re[3], r)) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t e = ngp_sel4(ri[0][k], ri[1][k], ri[2][k], ri[3][k], r);
+        const float val = ngp_sel4(rv[0][k], rv[1][k], rv[2][k], rv[3][k], r);
+        unsafeAtomicAdd(d_table + 2 * (int64_t)e + (q & 1), val);
+      }
+    }
+  }
+}
+
+// this lane's activation derivative of saved layer rows (pre-activation rows P, outputs Q)
+__device__ __forceinline__ float ngp_dact_row(const float* S, int P, int Q, int row, int64_t n, int relu) {
+  return relu ? (S[(Q + row) * n] > 0.0f ? 1.0f : 0.0f) : ngp_dsp100(S[(P + row) * n]);
+}
+
+__global__ __launch_bounds__(NM_THREADS) void ngp_bwd_mfma_kernel(NgpArgs A) {
+  __shared__ __attribute__((aligned(16))) float img[BI_FLOATS];
+  const int E = A.enc, L = A.grid.n_levels, rd = A.rd;
+  for (int q = threadIdx.x; q < BI_FLOATS; q += NM_THREADS) img[q] = ngp_bi(A.mlp, A.off, E, rd, q);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int relu = A.hidden_relu;
+  const int64_t n = A.n;
+  const float* S = A.save;
+  float* D = A.dz;
+  const int64_t ntiles = (n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * NM_WAVES + (threadIdx.x >> 6); tile < ntiles;
+       tile += (int64_t)gridDim.x * NM_WAVES) {
+    const int64_t i = tile * 32 + j;
+    const bool ok = i < n;
+    const int64_t ic = ok ? i : n - 1;
+    // per-lane bases + uniform row offsets, as in the forward
+    int64_t nn = n;
+    asm volatile("" : "+s"(nn));
+    const float* S0 = S + ic;
+    const float* Sh = S + ic + 4 * h * nn;
+    float* D0 = D + i;
+    float* Dh = D + i + 4 * h * nn;
+    // radiance activation: this lane's K index carries outputs h (step 0) and 2 + h (step 1)
+    float dr[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = 2 * u + h;
+      if (c < rd) {
+        const float g = A.d_rgb && ok ? A.d_rgb[ic * rd + c] : 0.0f;
+        const float rv = S0[(NS_R + c) * nn];
+        if (A.rad_sigmoid) {
+          const float s = __fdiv_rn(1.0f, 1.0f + expf(-rv));
+          dr[u] = g * (s * (1.0f - s));
+        } else {
+          const float z = expf(rv);
+          dr[u] = rv > 20.0f ? g : g * __fdiv_rn(z, z + 1.0f);
+        }
+      }
+      if (ok && c < 3) D0[(ND_R + c) * nn] = dr[u];
+    }
+    float dz[32];
+    {
+      f32x16 acc[2] = {ngp_zero16(), ngp_zero16()};
+      ngp_mm<2, 4>(img + BI_A4, dr, acc, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = 32 * t + ngp_row(r, 0);
+          dz[16 * t + r] = acc[t][r] * ngp_dact_row(Sh, NS_H2P, NS_H2, row, nn, relu);
+          if (ok) Dh[(ND_Z3 + row) * nn] = dz[16 * t + r];
+        }
+    }
+    {
+      f32x16 acc[2] = {ngp_zero16(), ngp_zero16()};
+      ngp_mm<2, 32>(img + BI_A3, dz, acc, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = 32 * t + ngp_row(r, 0);
+          dz[16 * t + r] = acc[t][r] * ngp_dact_row(Sh, NS_H1P, NS_H1, row, nn, relu);
+          if (ok) Dh[(ND_Z2 + row) * nn] = dz[16 * t + r];
+        }
+    }
+    // base output: geo rows 1..15 from the head input gradient, row 0 the density's
+    float dob[8];
+    {
+      f32x16 dg[1] = {ngp_zero16()};
+      ngp_mm<1, 32>(img + BI_A2, dz, dg, lane);
+      const float gs = A.d_sigma && ok ? A.d_sigma[ic] : 0.0f;
+      const float sel = S0[NS_SEL * nn];
+      const float o0 = S0[NS_O0 * nn];
+      const float d0 = sel != 0.0f ? gs * expf(fminf(o0 - 1.0f, 15.0f)) : 0.0f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        dob[q] = q == 0 && h == 0 ? d0 : dg[0][q];
+        if (ok) Dh[(ND_O + ngp_row(q, 0)) * nn] = dob[q];
+      }
+    }
+    {
+      f32x16 acc[2] = {ngp_zero16(), ngp_zero16()};
+      ngp_mm<2, 8>(img + BI_A1, dob, acc, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = 32 * t + ngp_row(r, 0);
+          dz[16 * t + r] = acc[t][r] * ngp_dact_row(Sh, NS_H0P, NS_H0, row, nn, relu);
+          if (ok) Dh[(ND_Z0 + row) * nn] = dz[16 * t + r];
+        }
+    }
+    f32x16 df[1] = {ngp_zero16()};
+    ngp_mm<1, 32>(img + BI_A0, dz, df, lane);
+    // hash-table scatter: half h holds feature rows 2 l, 2 l + 1 of levels l = 4 a + 2 h + b
+    // (registers 4 a + 2 b, + 1)
+    float xn[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) xn[a] = S0[(NS_X + a) * nn];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int l = 4 * a + 2 * h + b;
+        if (l >= L) continue;
+        const NgpLevel V = ngp_level_h(A.grid, 4 * a + b, 4 * a + 2 + b, h);
+        NgpCorner C;
+        uint32_t cell[3];
+        ngp_corners(V, A.grid.hashed, xn, C, cell);
+        const float g0 = df[0][4 * a + 2 * b], g1 = df[0][4 * a + 2 * b + 1];
+        float v[16];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          v[2 * c] = C.w[c] * g0;
+          v[2 * c + 1] = C.w[c] * g1;
+        }
+        bool emit = ok;
+#if DEN_NGP_AGG_RES > 0
+        if (V.res <= (uint32_t)DEN_NGP_AGG_RES) emit = ngp_fold(cell, v, ok);
+#endif
+#if DEN_NGP_SCATTER_QUAD
+        ngp_scatter_quad(A.d_table, C.idx, v, emit);
+#else
+        if (emit) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            float* t = A.d_table + 2 * (int64_t)C.idx[c];
+            unsafeAtomicAdd(t, v[2 * c]);
+            unsafeAtomicAdd(t + 1, v[2 * c + 1]);
+          }
+        }
+#endif
+      }
+  }
+}
+
+}  // namespace den
