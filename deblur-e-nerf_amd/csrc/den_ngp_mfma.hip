@@ -326,7 +326,7 @@ __global__ __launch_bounds__(NM_THREADS) void ngp_fwd_mfma_kernel(NgpArgs A) {
 // x cell) -- 4..8 requests per sample-level instead of 16.  The values, indices and emit flags are
 // exchanged with quad_perm DPP moves (lane q receives from lane q ^ r).
 #ifndef DEN_NGP_SCATTER_QUAD
-#define DEN_NGP_SCATTER_QUAD 0
+#define DEN_NGP_SCATTER_QUAD 1
 #endif
 template <int R>
 __device__ __forceinline__ int ngp_qxor(int v) {
