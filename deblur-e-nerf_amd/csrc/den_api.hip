@@ -1152,20 +1152,21 @@ struct NgpWs {
   int splits;
   int64_t per_split;
 };
+int64_t ngp_ld(int64_t n) { return (n + 63) / 64 * 64; }
 NgpWs ngp_ws(int64_t n) {
   NgpWs w{};
   size_t off = 0;
   w.save = off;
-  off += align256((size_t)NS_ROWS * n * 4);
+  off += align256((size_t)NS_ROWS * ngp_ld(n) * 4);
   w.dz = off;
-  off += align256((size_t)ND_ROWS * n * 4);
+  off += align256((size_t)ND_ROWS * ngp_ld(n) * 4);
   int64_t splits = std::max<int64_t>(1, std::min<int64_t>(256, (n + 4095) / 4096));
   int64_t per = (n + splits - 1) / splits;
   per = (per + NGP_DW_CHUNK - 1) / NGP_DW_CHUNK * NGP_DW_CHUNK;
   w.splits = (int)((n + per - 1) / per);
   w.per_split = per;
   w.partial = off;
-  off += align256((size_t)5 * w.splits * NGP_DW_PM * NGP_DW_PK * 4);
+  off += align256(std::max((size_t)5 * w.splits * NGP_DW_PM * NGP_DW_PK, (size_t)NDW_TASKS * w.splits * NDW_PART) * 4);
   w.total = off;
   return w;
 }
@@ -1221,6 +1222,7 @@ int den_ngp_fwd(const den_ngp_desc* desc, int64_t n, int32_t points, const float
   A.grid = g;
   A.out_rgb = out_rgb;
   A.out_sigma = out_sigma;
+  A.ld = ngp_ld(n);
   A.save = train ? (float*)((char*)workspace + ngp_ws(n).save) : nullptr;
 #if DEN_NGP_MFMA
   hipLaunchKernelGGL(ngp_fwd_mfma_kernel, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, (hipStream_t)stream, A);
@@ -1254,6 +1256,7 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
   A.off = ngp_offsets(2 * g.n_levels, desc->radiance_dim);
   A.enc = 2 * g.n_levels;
   A.grid = g;
+  A.ld = ngp_ld(n);
   A.save = (float*)(ws + W.save);
   A.d_rgb = d_rgb;
   A.d_sigma = d_sigma;
@@ -1266,15 +1269,37 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
 #endif
   DEN_LAUNCHED();
   const int rd = desc->radiance_dim;
+  const NgpOff& O = A.off;
+#if DEN_NGP_DW_MFMA
+  NgpDwMfArgs Q{};
+  Q.dz = A.dz;
+  Q.save = A.save;
+  Q.n = n;
+  Q.ld = A.ld;
+  Q.per_split = W.per_split;
+  Q.splits = W.splits;
+  Q.partial = (float*)(ws + W.partial);
+  Q.grad = grad_params + tfl;
+  Q.T[0] = NgpDwTask{ND_Z0, NGP_W, 2, NS_FEAT, A.enc, A.enc, 0, O.w[0], O.b[0]};
+  Q.T[1] = NgpDwTask{ND_O, 1 + NGP_GEO, 1, NS_H0, NGP_W, NGP_W, 0, O.w[1], O.b[1]};
+  Q.T[2] = NgpDwTask{ND_Z2, NGP_W, 2, NS_HIN, NGP_HIN, NGP_HIN, 0, O.w[2], O.b[2]};
+  Q.T[3] = NgpDwTask{ND_Z3, 32, 1, NS_H1, NGP_W, NGP_W, 0, O.w[3], O.b[3]};
+  Q.T[4] = NgpDwTask{ND_Z3 + 32, 32, 1, NS_H1, NGP_W, NGP_W, 32, O.w[3], O.b[3]};
+  Q.T[5] = NgpDwTask{ND_R, rd, 1, NS_H2, NGP_W, NGP_W, 0, O.w[4], O.b[4]};
+  hipLaunchKernelGGL(ngp_dw_mfma_kernel, dim3((unsigned)W.splits, NDW_TASKS), dim3(256), 0, st, Q);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(ngp_dw_mfma_reduce_kernel, dim3((NDW_PART + 255) / 256, NDW_TASKS), dim3(256), 0, st, Q);
+  DEN_LAUNCHED();
+#else
   NgpDwArgs P{};
   P.dz = A.dz;
   P.save = A.save;
   P.n = n;
+  P.ld = A.ld;
   P.per_split = W.per_split;
   P.splits = W.splits;
   P.partial = (float*)(ws + W.partial);
   P.grad = grad_params + tfl;
-  const NgpOff& O = A.off;
   P.L[0] = NgpDwLayer{ND_Z0, NGP_W, NS_FEAT, A.enc, O.w[0], O.b[0]};
   P.L[1] = NgpDwLayer{ND_O, 1 + NGP_GEO, NS_H0, NGP_W, O.w[1], O.b[1]};
   P.L[2] = NgpDwLayer{ND_Z2, NGP_W, NS_HIN, NGP_HIN, O.w[2], O.b[2]};
@@ -1284,6 +1309,7 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
   DEN_LAUNCHED();
   hipLaunchKernelGGL(ngp_dw_reduce_kernel, dim3((NGP_DW_PM * NGP_DW_PK + 255) / 256, 5), dim3(256), 0, st, P);
   DEN_LAUNCHED();
+#endif
   return DEN_OK;
 }
 

@@ -103,12 +103,13 @@ struct NgpArgs {
   NgpGrid grid;
   float* out_rgb;      // (n, rd)
   float* out_sigma;    // (n)
-  float* save;         // train: [NS_ROWS][n]
+  int64_t ld;          // row stride of save / dz: n rounded up to 64 (16-B aligned sample quads)
+  float* save;         // train: [NS_ROWS][ld]
   // backward
   const float* d_rgb;
   const float* d_sigma;
   float* d_table;
-  float* dz;           // [ND_ROWS][n]
+  float* dz;           // [ND_ROWS][ld]
 };
 
 // ------------------------------------------------------------------ elementwise pieces
@@ -440,11 +441,11 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
   ngp_encode(A.grid, A.table, xn, feat);
   const int relu = A.hidden_relu;
   float* S = A.save;
-  const int64_t n = A.n;
+  const int64_t ld = A.ld;
   if (S) {
 #pragma unroll
     for (int f = 0; f < NGP_ENC; ++f)
-      if (f < A.enc) S[(NS_FEAT + f) * n + i] = feat[f];
+      if (f < A.enc) S[(NS_FEAT + f) * ld + i] = feat[f];
   }
   float h0[NGP_W];
   {
@@ -455,8 +456,8 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
     if (S) {
 #pragma unroll
       for (int o = 0; o < NGP_W; ++o) {
-        S[(NS_H0P + o) * n + i] = h0p[o];
-        S[(NS_H0 + o) * n + i] = h0[o];
+        S[(NS_H0P + o) * ld + i] = h0p[o];
+        S[(NS_H0 + o) * ld + i] = h0[o];
       }
     }
   }
@@ -466,10 +467,10 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
   const float sigma = sel != 0.0f ? expf(ob[0] - 1.0f) : 0.0f;
   A.out_sigma[i] = sigma;
   if (S) {
-    S[NS_O0 * n + i] = ob[0];
-    S[NS_SEL * n + i] = sel;
+    S[NS_O0 * ld + i] = ob[0];
+    S[NS_SEL * ld + i] = sel;
 #pragma unroll
-    for (int a = 0; a < 3; ++a) S[(NS_X + a) * n + i] = xn[a];
+    for (int a = 0; a < 3; ++a) S[(NS_X + a) * ld + i] = xn[a];
   }
   if (A.density_only) return;
   float hin[NGP_HIN];
@@ -478,7 +479,7 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
   for (int g = 0; g < NGP_GEO; ++g) hin[NGP_SH + g] = ob[1 + g];
   if (S) {
 #pragma unroll
-    for (int f = 0; f < NGP_HIN; ++f) S[(NS_HIN + f) * n + i] = hin[f];
+    for (int f = 0; f < NGP_HIN; ++f) S[(NS_HIN + f) * ld + i] = hin[f];
   }
   // each layer's saved rows are stored as soon as it is computed (keeps them out of VGPRs)
   float h1[NGP_W];
@@ -490,8 +491,8 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
     if (S) {
 #pragma unroll
       for (int o = 0; o < NGP_W; ++o) {
-        S[(NS_H1P + o) * n + i] = h1p[o];
-        S[(NS_H1 + o) * n + i] = h1[o];
+        S[(NS_H1P + o) * ld + i] = h1p[o];
+        S[(NS_H1 + o) * ld + i] = h1[o];
       }
     }
   }
@@ -504,8 +505,8 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
     if (S) {
 #pragma unroll
       for (int o = 0; o < NGP_W; ++o) {
-        S[(NS_H2P + o) * n + i] = h2p[o];
-        S[(NS_H2 + o) * n + i] = h2[o];
+        S[(NS_H2P + o) * ld + i] = h2p[o];
+        S[(NS_H2 + o) * ld + i] = h2[o];
       }
     }
   }
@@ -518,7 +519,7 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
       const float v = A.rad_sigmoid ? __fdiv_rn(1.0f, 1.0f + expf(-r[c])) : (r[c] > 20.0f ? r[c] : log1pf(expf(r[c])));
       A.out_rgb[i * A.rd + c] = v;
     }
-    if (S) S[(NS_R + c) * n + i] = r[c];
+    if (S) S[(NS_R + c) * ld + i] = r[c];
   }
 }
 
@@ -535,7 +536,7 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpArgs A) {
 #endif
   if (i >= A.n) return;
   const float* S = A.save;
-  const int64_t n = A.n;
+  const int64_t ld = A.ld;
   const int relu = A.hidden_relu;
   float* D = A.dz;
   // radiance activation
@@ -544,7 +545,7 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpArgs A) {
   for (int c = 0; c < 3; ++c) {
     if (c >= A.rd) break;
     const float g = A.d_rgb ? A.d_rgb[i * A.rd + c] : 0.0f;
-    const float rv = S[(NS_R + c) * n + i];
+    const float rv = S[(NS_R + c) * ld + i];
     if (A.rad_sigmoid) {
       const float s = __fdiv_rn(1.0f, 1.0f + expf(-rv));
       dr[c] = g * (s * (1.0f - s));
@@ -554,21 +555,21 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpArgs A) {
     }
   }
 #pragma unroll
-  for (int c = 0; c < 3; ++c) D[(ND_R + c) * n + i] = dr[c];
+  for (int c = 0; c < 3; ++c) D[(ND_R + c) * ld + i] = dr[c];
   // head output layer -> h2 -> h1 -> head input
   float dh[NGP_W], dz[NGP_W];
   if (A.rd == 3) ngp_linear_t<3, NGP_W, NGP_W>(NGP_W_(4), dr, dh);
   else ngp_linear_t<1, NGP_W, NGP_W>(NGP_W_(4), dr, dh);
 #pragma unroll
   for (int o = 0; o < NGP_W; ++o) {
-    dz[o] = dh[o] * ngp_dact(S[(NS_H2P + o) * n + i], S[(NS_H2 + o) * n + i], relu);
-    D[(ND_Z3 + o) * n + i] = dz[o];
+    dz[o] = dh[o] * ngp_dact(S[(NS_H2P + o) * ld + i], S[(NS_H2 + o) * ld + i], relu);
+    D[(ND_Z3 + o) * ld + i] = dz[o];
   }
   ngp_linear_t<NGP_W, NGP_W, NGP_W>(NGP_W_(3), dz, dh);
 #pragma unroll
   for (int o = 0; o < NGP_W; ++o) {
-    dz[o] = dh[o] * ngp_dact(S[(NS_H1P + o) * n + i], S[(NS_H1 + o) * n + i], relu);
-    D[(ND_Z2 + o) * n + i] = dz[o];
+    dz[o] = dh[o] * ngp_dact(S[(NS_H1P + o) * ld + i], S[(NS_H1 + o) * ld + i], relu);
+    D[(ND_Z2 + o) * ld + i] = dz[o];
   }
   float dhin[NGP_HIN];
   ngp_linear_t<NGP_W, NGP_HIN, NGP_LD2>(NGP_W_(2), dz, dhin);
@@ -576,26 +577,26 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpArgs A) {
   float dob[1 + NGP_GEO];
   {
     const float gs = A.d_sigma ? A.d_sigma[i] : 0.0f;
-    const float sel = S[NS_SEL * n + i];
-    const float o0 = S[NS_O0 * n + i];
+    const float sel = S[NS_SEL * ld + i];
+    const float o0 = S[NS_O0 * ld + i];
     dob[0] = sel != 0.0f ? gs * expf(fminf(o0 - 1.0f, 15.0f)) : 0.0f;
   }
 #pragma unroll
   for (int g = 0; g < NGP_GEO; ++g) dob[1 + g] = dhin[NGP_SH + g];
 #pragma unroll
-  for (int o = 0; o < 1 + NGP_GEO; ++o) D[(ND_O + o) * n + i] = dob[o];
+  for (int o = 0; o < 1 + NGP_GEO; ++o) D[(ND_O + o) * ld + i] = dob[o];
   ngp_linear_t<1 + NGP_GEO, NGP_W, NGP_W>(NGP_W_(1), dob, dh);
 #pragma unroll
   for (int o = 0; o < NGP_W; ++o) {
-    dz[o] = dh[o] * ngp_dact(S[(NS_H0P + o) * n + i], S[(NS_H0 + o) * n + i], relu);
-    D[(ND_Z0 + o) * n + i] = dz[o];
+    dz[o] = dh[o] * ngp_dact(S[(NS_H0P + o) * ld + i], S[(NS_H0 + o) * ld + i], relu);
+    D[(ND_Z0 + o) * ld + i] = dz[o];
   }
   float dfeat[NGP_ENC];
   ngp_linear_enc_t(NGP_W_(0), dz, dfeat, A.enc, NGP_LD0);
   // hash-table scatter
   float xn[3];
 #pragma unroll
-  for (int a = 0; a < 3; ++a) xn[a] = S[(NS_X + a) * n + i];
+  for (int a = 0; a < 3; ++a) xn[a] = S[(NS_X + a) * ld + i];
   for (int l = 0; l < A.grid.n_levels; ++l) {
     NgpCorner C;
     uint32_t cell[3];
@@ -679,6 +680,7 @@ struct NgpDwArgs {
   const float* dz;
   const float* save;
   int64_t n;
+  int64_t ld;  // row stride
   int64_t per_split;
   int splits;
   NgpDwLayer L[5];
@@ -708,8 +710,8 @@ __global__ __launch_bounds__(256) void ngp_dw_kernel(NgpDwArgs P) {
       const int64_t si = c0 + s;
       const bool ok = si < s1;
       float va = 0.0f, vb = 0.0f;
-      if (r < L.m && ok) va = P.dz[(int64_t)(L.a_row + r) * P.n + si];
-      if (r < L.k && ok) vb = P.save[(int64_t)(L.b_row + r) * P.n + si];
+      if (r < L.m && ok) va = P.dz[(int64_t)(L.a_row + r) * P.ld + si];
+      if (r < L.k && ok) vb = P.save[(int64_t)(L.b_row + r) * P.ld + si];
       else if (r == L.k && ok) vb = 1.0f;
       sa[s * NGP_DW_LD + r] = va;
       sb[s * NGP_DW_LD + r] = vb;

@@ -26,6 +26,9 @@ namespace den {
 #ifndef DEN_NGP_MFMA
 #define DEN_NGP_MFMA 1
 #endif
+#ifndef DEN_NGP_SAVE_PRE
+#define DEN_NGP_SAVE_PRE 0  // 1: store the hidden pre-activations too (the VALU kernels' derivative)
+#endif
 #ifndef DEN_NGP_MF_WAVES
 #define DEN_NGP_MF_WAVES 8  // waves (32-sample tiles in flight) per workgroup
 #endif
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(NM_THREADS) void ngp_fwd_mfma_kernel(NgpArgs A) {
     const int64_t ic = ok ? i : n - 1;
     // save rows: uniform row offsets (row * nn; nn is opaque per tile so they are not hoisted out of
     // the loop as per-row registers) from a per-lane base; Sh adds this half's 4-row shift
-    int64_t nn = n;
+    int64_t nn = A.ld;
     asm volatile("" : "+s"(nn));
     float* S0 = S ? S + i : nullptr;
     float* Sh = S ? S + i + 4 * h * nn : nullptr;
@@ -230,7 +233,7 @@ __global__ __launch_bounds__(NM_THREADS) void ngp_fwd_mfma_kernel(NgpArgs A) {
           hb[16 * t + r] = a;
           if (S && ok) {
             const int row = 32 * t + ngp_row(r, 0);
-            Sh[(NS_H0P + row) * nn] = pre;
+            if (DEN_NGP_SAVE_PRE) Sh[(NS_H0P + row) * nn] = pre;
             Sh[(NS_H0 + row) * nn] = a;
           }
         }
@@ -279,7 +282,7 @@ __global__ __launch_bounds__(NM_THREADS) void ngp_fwd_mfma_kernel(NgpArgs A) {
           hb[16 * t + r] = a;
           if (S && ok) {
             const int row = 32 * t + ngp_row(r, 0);
-            Sh[(NS_H1P + row) * nn] = pre;
+            if (DEN_NGP_SAVE_PRE) Sh[(NS_H1P + row) * nn] = pre;
             Sh[(NS_H1 + row) * nn] = a;
           }
         }
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(NM_THREADS) void ngp_fwd_mfma_kernel(NgpArgs A) {
           hb[16 * t + r] = a;
           if (S && ok) {
             const int row = 32 * t + ngp_row(r, 0);
-            Sh[(NS_H2P + row) * nn] = pre;
+            if (DEN_NGP_SAVE_PRE) Sh[(NS_H2P + row) * nn] = pre;
             Sh[(NS_H2 + row) * nn] = a;
           }
         }
@@ -374,8 +377,17 @@ __device__ __forceinline__ void ngp_scatter_quad(float* d_table, const uint32_t*
 }
 
 // this lane's activation derivative of saved layer rows (pre-activation rows P, outputs Q)
+// DEN_NGP_SAVE_PRE 0: the softplus derivative from the saved OUTPUT y alone: exp(100 x) / (exp(100 x)
+// + 1) = 1 - exp(-100 y) = -expm1(-100 y), and 100 y > 20 exactly where 100 x > 20 (torch's
+// threshold; at the boundary both round to 1).  Saves and re-reads 192 rows (768 B) per sample less.
+__device__ __forceinline__ float ngp_dsp100_out(float y) {
+  const float by = y * 100.0f;
+  return by > 20.0f ? 1.0f : -expm1f(-by);
+}
 __device__ __forceinline__ float ngp_dact_row(const float* S, int P, int Q, int row, int64_t n, int relu) {
-  return relu ? (S[(Q + row) * n] > 0.0f ? 1.0f : 0.0f) : ngp_dsp100(S[(P + row) * n]);
+  if (relu) return S[(Q + row) * n] > 0.0f ? 1.0f : 0.0f;
+  if (DEN_NGP_SAVE_PRE) return ngp_dsp100(S[(P + row) * n]);
+  return ngp_dsp100_out(S[(Q + row) * n]);
 }
 
 __global__ __launch_bounds__(NM_THREADS) void ngp_bwd_mfma_kernel(NgpArgs A) {
@@ -395,7 +407,7 @@ __global__ __launch_bounds__(NM_THREADS) void ngp_bwd_mfma_kernel(NgpArgs A) {
     const bool ok = i < n;
     const int64_t ic = ok ? i : n - 1;
     // per-lane bases + uniform row offsets, as in the forward
-    int64_t nn = n;
+    int64_t nn = A.ld;
     asm volatile("" : "+s"(nn));
     const float* S0 = S + ic;
     const float* Sh = S + ic + 4 * h * nn;
@@ -512,6 +524,144 @@ __global__ __launch_bounds__(NM_THREADS) void ngp_bwd_mfma_kernel(NgpArgs A) {
         }
 #endif
       }
+  }
+}
+
+}  // namespace den
+
+namespace den {
+
+// ------------------------------------------------------------------ weight gradients on MFMA
+// dW[o][k] = sum_s dZ[o][s] X[k][s], db[o] = sum_s dZ[o][s] with the samples as the K dimension of
+// v_mfma_f32_32x32x2_f32: A[m][k] = dZ row m, B[k][n] = X row n.  Six tasks of two 32 x 32 tiles
+// each: layer 0 (2 row tiles x E columns), layer 1 (16 rows x 2 column tiles), layer 2 (2 x 31),
+// layer 3 rows 0..31 and 32..63 (x 2 column tiles each), layer 4 (rd x 2).  Lane (j, h) loads row j
+// of a 32-row block at samples 8 u + 4 h .. + 3 (one 16-B load per operand row block and 4 steps;
+// any sample-to-k assignment works as long as A and B agree), so the feature-major rows stream in
+// without LDS.  The bias is the row sum of the A operand, accumulated from the same registers.
+// Workgroup = (split, task), 4 waves over interleaved 32-sample chunks, reduced through LDS into
+// partials [task][split][2][32][32] + [64]; a second kernel sums the splits in a fixed order.
+#ifndef DEN_NGP_DW_MFMA
+#define DEN_NGP_DW_MFMA 1
+#endif
+constexpr int NDW_TASKS = 6, NDW_PART = 2 * 32 * 32 + 64;
+
+struct NgpDwTask {
+  int a_row, a_rows, mt;  // dZ rows (first, valid count), row tiles (1 or 2; column tiles = 3 - mt)
+  int b_row, b_rows;      // X rows
+  int k_in, m_off;        // weight row length, first weight row of the task
+  int64_t w_off, b_off;
+};
+struct NgpDwMfArgs {
+  const float* dz;
+  const float* save;
+  int64_t n, ld, per_split;
+  int splits;
+  NgpDwTask T[NDW_TASKS];
+  float* partial;  // [task][split][NDW_PART]
+  float* grad;
+};
+
+// 4 samples of row `row` (valid if row < rows) starting at q (zero past s1)
+__device__ __forceinline__ f32x4 ngp_dw_load(const float* base, int row, int rows, int64_t ld, int64_t q, int64_t s1) {
+  f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (row < rows && q < s1) {
+    v = *(const f32x4*)(base + (int64_t)row * ld + q);
+    if (q + 4 > s1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (q + e >= s1) v[e] = 0.0f;
+    }
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P) {
+  __shared__ __attribute__((aligned(16))) float red[2][NDW_PART];
+  const NgpDwTask T = P.T[blockIdx.y];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int mt = T.mt, nt = 3 - T.mt;
+  const float* Ab = P.dz + (int64_t)T.a_row * P.ld;
+  const float* Bb = P.save + (int64_t)T.b_row * P.ld;
+  const int64_t s0 = (int64_t)blockIdx.x * P.per_split;
+  const int64_t s1 = s0 + P.per_split < P.n ? s0 + P.per_split : P.n;
+  f32x16 acc[2] = {ngp_zero16(), ngp_zero16()};
+  float bsum[2] = {0.0f, 0.0f};
+  for (int64_t c = s0 + 32 * wave; c < s1; c += 128) {
+    f32x4 a[2][4], b[2][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t q = c + 8 * u + 4 * h;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        a[t][u] = t < mt ? ngp_dw_load(Ab, 32 * t + j, T.a_rows, P.ld, q, s1) : f32x4{0.f, 0.f, 0.f, 0.f};
+        b[t][u] = t < nt ? ngp_dw_load(Bb, 32 * t + j, T.b_rows, P.ld, q, s1) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (mt == 2) {
+          acc[0] = ngp_mfma(a[0][u][e], b[0][u][e], acc[0]);
+          acc[1] = ngp_mfma(a[1][u][e], b[0][u][e], acc[1]);
+        } else {
+          acc[0] = ngp_mfma(a[0][u][e], b[0][u][e], acc[0]);
+          acc[1] = ngp_mfma(a[0][u][e], b[1][u][e], acc[1]);
+        }
+        bsum[0] += a[0][u][e];
+        bsum[1] += a[1][u][e];
+      }
+  }
+  // tile tt: rows ngp_row(r, h), column j; bias of rows 32 t + j from both halves.  Waves 2, 3 store,
+  // waves 0, 1 add theirs: the split's partial is (w0 + w2) + (w1 + w3), a fixed order.
+  float bias[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) bias[t] = bsum[t] + __shfl_xor(bsum[t], 32);
+  float* R = red[wave & 1];
+  if (wave >= 2) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) R[tt * 1024 + ngp_row(r, h) * 32 + j] = acc[tt][r];
+    if (h == 0) {
+      R[2048 + j] = bias[0];
+      R[2048 + 32 + j] = bias[1];
+    }
+  }
+  __syncthreads();
+  if (wave < 2) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float& d = R[tt * 1024 + ngp_row(r, h) * 32 + j];
+        d = acc[tt][r] + d;
+      }
+    if (h == 0) {
+      R[2048 + j] = bias[0] + R[2048 + j];
+      R[2048 + 32 + j] = bias[1] + R[2048 + 32 + j];
+    }
+  }
+  __syncthreads();
+  float* out = P.partial + ((int64_t)blockIdx.y * P.splits + blockIdx.x) * NDW_PART;
+  for (int e = threadIdx.x; e < NDW_PART; e += 256) out[e] = red[0][e] + red[1][e];
+}
+
+__global__ __launch_bounds__(256) void ngp_dw_mfma_reduce_kernel(NgpDwMfArgs P) {
+  const NgpDwTask T = P.T[blockIdx.y];
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= NDW_PART) return;
+  const float* src = P.partial + (int64_t)blockIdx.y * P.splits * NDW_PART + e;
+  float s = 0.0f;
+  for (int sp = 0; sp < P.splits; ++sp) s += src[(int64_t)sp * NDW_PART];
+  if (e < 2048) {
+    const int tt = e >> 10, row = (e >> 5) & 31, col = e & 31;
+    const int mrow = (T.mt == 2 ? 32 * tt : 0) + row, ncol = (T.mt == 2 ? 0 : 32 * tt) + col;
+    if (mrow < T.a_rows && ncol < T.b_rows) P.grad[T.w_off + (int64_t)(T.m_off + mrow) * T.k_in + ncol] = s;
+  } else {
+    const int m = e - 2048;
+    if (m < T.a_rows) P.grad[T.b_off + T.m_off + m] = s;
   }
 }
 
