@@ -32,8 +32,11 @@ namespace den {
 #ifndef DEN_NGP_MF_WAVES
 #define DEN_NGP_MF_WAVES 8  // waves (32-sample tiles in flight) per workgroup
 #endif
+#ifndef DEN_NGP_MF_OCC
+#define DEN_NGP_MF_OCC 4  // waves per SIMD the field kernels are compiled for (128 VGPRs; 2 / 3 measured slower)
+#endif
 #ifndef DEN_NGP_MF_GRID
-#define DEN_NGP_MF_GRID 1024  // workgroups at most (each loops over tiles; the image is built once)
+#define DEN_NGP_MF_GRID 4096  // workgroups at most (each loops over tiles; the image is built once per workgroup)
 #endif
 constexpr int NM_WAVES = DEN_NGP_MF_WAVES, NM_THREADS = 64 * NM_WAVES;
 
@@ -171,7 +174,7 @@ __device__ __forceinline__ NgpLevel ngp_level_h(const NgpGrid& G, int q, int l1,
 }
 
 // ------------------------------------------------------------------ forward
-__global__ __launch_bounds__(NM_THREADS) void ngp_fwd_mfma_kernel(NgpArgs A) {
+__global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kernel(NgpArgs A) {
   __shared__ __attribute__((aligned(16))) float img[FI_FLOATS];
   const int E = A.enc, L = A.grid.n_levels, L0 = (L + 1) / 2;
   for (int q = threadIdx.x; q < FI_FLOATS; q += NM_THREADS) img[q] = ngp_fi(A.mlp, A.off, E, L0, A.rd, q);
@@ -390,7 +393,7 @@ __device__ __forceinline__ float ngp_dact_row(const float* S, int P, int Q, int 
   return ngp_dsp100_out(S[(Q + row) * n]);
 }
 
-__global__ __launch_bounds__(NM_THREADS) void ngp_bwd_mfma_kernel(NgpArgs A) {
+__global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_bwd_mfma_kernel(NgpArgs A) {
   __shared__ __attribute__((aligned(16))) float img[BI_FLOATS];
   const int E = A.enc, L = A.grid.n_levels, rd = A.rd;
   for (int q = threadIdx.x; q < BI_FLOATS; q += NM_THREADS) img[q] = ngp_bi(A.mlp, A.off, E, rd, q);
