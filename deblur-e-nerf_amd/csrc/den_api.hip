@@ -812,7 +812,10 @@ int den_march_count(int32_t n_rays, const float* rays_o, const float* rays_d, co
   if (rc) return rc;
   if (!counts) return fail(DEN_EINVAL, "counts is required");
   M.counts = counts;
-  hipLaunchKernelGGL(march_kernel<false>, dim3((n_rays + 127) / 128), dim3(128), 0, (hipStream_t)stream, M);
+  if (DEN_MARCH_WAVE && M.contraction != CONTRACT_AABB)
+    hipLaunchKernelGGL(march_wave_kernel<false>, dim3((n_rays + 3) / 4), dim3(256), 0, (hipStream_t)stream, M);
+  else
+    hipLaunchKernelGGL(march_kernel<false>, dim3((n_rays + 127) / 128), dim3(128), 0, (hipStream_t)stream, M);
   DEN_LAUNCHED();
   return DEN_OK;
 }
@@ -829,7 +832,10 @@ int den_march_fill(int32_t n_rays, const float* rays_o, const float* rays_d, con
   M.ray_idx = ray_indices;
   M.t0 = t_starts;
   M.t1 = t_ends;
-  hipLaunchKernelGGL(march_kernel<true>, dim3((n_rays + 127) / 128), dim3(128), 0, (hipStream_t)stream, M);
+  if (DEN_MARCH_WAVE && M.contraction != CONTRACT_AABB)
+    hipLaunchKernelGGL(march_wave_kernel<true>, dim3((n_rays + 3) / 4), dim3(256), 0, (hipStream_t)stream, M);
+  else
+    hipLaunchKernelGGL(march_kernel<true>, dim3((n_rays + 127) / 128), dim3(128), 0, (hipStream_t)stream, M);
   DEN_LAUNCHED();
   return DEN_OK;
 }

@@ -127,6 +127,46 @@ def test_marching_matches_reference_samples(golden_dir, rd):
     assert np.array_equal(t1.cpu().numpy(), z["train_marched_t1"])
 
 
+@pytest.mark.parametrize("ctype,cone", [(2, 0.004), (1, 0.004), (2, 0.0)])
+def test_marching_unbounded_matches_oracle(ctype, cone):
+    """The wave-parallel march (den_march_count / fill for the sphere and tanh contractions: every
+    lane runs the step chain, lanes test 64 steps at once) against oracle/nerfacc.march's sequential
+    loop: bit-exact samples, including a ray that misses (near > far) and configs[3]'s near 0.01,
+    far 13, cone angle 0.004 on a random 32^3 grid."""
+    import ctypes
+    from oracle import nerfacc as onacc
+    nat, marching, _, _ = _mods()
+    g = torch.Generator().manual_seed(5 + ctype)
+    R = 24
+    aabb = [0.2, -0.4, 0.0, 3.7, 3.7, 1.8]
+    lo, hi = torch.tensor(aabb[:3]), torch.tensor(aabb[3:])
+    o = lo + torch.rand(R, 3, generator=g) * (hi - lo)
+    d = torch.nn.functional.normalize(torch.randn(R, 3, generator=g), dim=-1)
+    tmin = torch.full((R,), 0.01) + torch.rand(R, generator=g) * 0.005
+    tmax = torch.full((R,), 13.0)
+    tmin[3], tmax[3] = 1e10, 1e10  # a miss
+    res = [32, 32, 32]
+    binary = (torch.rand(*res, generator=g) < 0.3).to(torch.uint8)
+    step = 0.005
+    ri_r, t0_r, t1_r, cnt_r = onacc.march(o.numpy(), d.numpy(), tmin.numpy(), tmax.numpy(), binary.numpy(),
+                                          np.asarray(aabb, np.float32), res, ctype, step, cone)
+    L = nat.lib()
+    od, dd, tmin_d, tmax_d, bin_d = (t.to(DEV) for t in (o, d, tmin, tmax, binary))
+    args = (R, nat._ptr(od), nat._ptr(dd), nat._ptr(tmin_d), nat._ptr(tmax_d), marching._carr(ctypes.c_float, aabb),
+            marching._carr(ctypes.c_int32, res), nat._ptr(bin_d), ctype, step, cone)
+    counts = torch.empty(R, dtype=torch.int32, device=DEV)
+    nat._check(L.den_march_count(*args, nat._ptr(counts), nat._stream()))
+    off, n = marching._scan(counts)
+    ri = torch.empty(n, dtype=torch.int32, device=DEV)
+    t0 = torch.empty(n, device=DEV)
+    t1 = torch.empty(n, device=DEV)
+    nat._check(L.den_march_fill(*args, nat._ptr(off), nat._ptr(ri), nat._ptr(t0), nat._ptr(t1), nat._stream()))
+    print(f"[ctype={ctype} cone={cone}] {n} samples (oracle {len(ri_r)}), max per ray {int(cnt_r.max())}")
+    assert np.array_equal(counts.cpu().numpy(), cnt_r) and cnt_r[3] == 0 and n > 0
+    assert np.array_equal(ri.cpu().numpy(), ri_r)
+    assert np.array_equal(t0.cpu().numpy(), t0_r) and np.array_equal(t1.cpu().numpy(), t1_r)
+
+
 @pytest.mark.parametrize("rd", [1, 3])
 def test_vol_rendering_matches_reference(golden_dir, rd):
     """external/vol_rendering.rendering on explicit packed samples: colours / opacities / depths
