@@ -636,6 +636,11 @@ int den_pixbw_bwd(int32_t S, int32_t N, int32_t reset, const float* it, const do
   A.d_it = d_it;
   A.d_delta_in = d_delta_in;
   A.d_prm = d_prm;
+#if DEN_PIXBW_SEGPAR
+  const int64_t seg_threads = 4 * (int64_t)(S - 1) * N;
+  hipLaunchKernelGGL(pixbw_seg_kernel, dim3((unsigned)((seg_threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
+  DEN_LAUNCHED();
+#endif
   hipLaunchKernelGGL(pixbw_bwd_kernel, dim3((unsigned)den_pixbw_blocks(N)), dim3(PIXBW_BLOCK), 0, (hipStream_t)stream, A);
   DEN_LAUNCHED();
   return DEN_OK;

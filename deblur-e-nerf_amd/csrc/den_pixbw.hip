@@ -25,7 +25,12 @@ namespace den {
 
 constexpr int PIXBW_BLOCK = 64;    // one wave per block
 constexpr int PIXBW_NPARAM = 7;
-constexpr int PIXBW_SEG_F = 24;    // workspace doubles per segment: Phi (16), Bd (4), Btd (4)
+#ifndef DEN_PIXBW_SEGPAR
+#define DEN_PIXBW_SEGPAR 1  // 0: the per-event serial backward (matrix exponentials inside the sweeps)
+#endif
+// workspace doubles per segment: Phi (16), Bd (4), Btd (4), then (segment-parallel backward) the four
+// Frechet derivatives L(X, E_m) (4 x 16)
+constexpr int PIXBW_SEG_F = DEN_PIXBW_SEGPAR ? 24 + 64 : 24;
 constexpr double PIXBW_NS = 1e-9;  // PixelBandwidth.NS_TO_S
 
 // ------------------------------------------------------------------ dual numbers
@@ -234,10 +239,30 @@ __device__ __forceinline__ double* pb_row(const PixArgs& A, int n, int i, int f)
   return A.ws + ((int64_t)(A.S - 1) * PIXBW_SEG_F + (int64_t)i * 8 + f) * A.N + n;
 }
 
+// Phi = e^{A dt}, Bd, Btd of segment k of event n (linearisation at I[k+1], FOH discretisation)
+__device__ __forceinline__ void pb_seg_sys(const PixArgs& A, int n, const PixPrm& P, int k, Mat4<double>& phi,
+                                           double* bd, double* btd) {
+  const double I1 = (double)A.it[(int64_t)(k + 1) * A.N + n];
+  const double dt = pb_dt(A, n, k);
+  const double ws = 1.0 / P.tsf, wd = 1.0 / P.tdf;
+  double a, b;
+  pb_lin(P, I1, &a, &b);
+  Mat4<double> X;
+  pb_X(a, b, ws, wd, dt, X);
+  mat_exp(X, phi);
+  double g1[4], yv[4];
+  pb_foh(phi, a, b, ws, wd, dt, g1, yv);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    btd[q] = yv[q] + (q ? 1.0 : 0.0);
+    bd[q] = g1[q] - btd[q];
+  }
+}
+
 // Forward sweep of event n (discretized_sys_to_weight, :283-294, fused with the weighted log-sum of
 // :406-415): segments k = S-2 .. 0 with c = c_{k+1} = C Phi[S-2] ... Phi[k+1]:
 //   w[k+1] += c Btd_k,   w[k] = c Bd_k (completed by the next step),   c <- c Phi_k.
-template <bool KEEP>
+template <bool KEEP, bool PRE = false>
 __device__ void pb_sweep(const PixArgs& A, int n, const PixPrm& P, double* y, double* den) {
   const int S = A.S, N = A.N, no = A.reset ? 2 : 1;
   const double ws = 1.0 / P.tsf, wd = 1.0 / P.tdf;
@@ -251,20 +276,20 @@ __device__ void pb_sweep(const PixArgs& A, int n, const PixPrm& P, double* y, do
   double num[2] = {0.0, 0.0}, dsum[2] = {0.0, 0.0}, wpend[2] = {0.0, 0.0};
   for (int k = S - 2; k >= 0; --k) {
     const double I1 = (double)A.it[(int64_t)(k + 1) * N + n];
-    const double dt = pb_dt(A, n, k);
-    double a, b;
-    pb_lin(P, I1, &a, &b);
-    Mat4<double> X, phi;
-    pb_X(a, b, ws, wd, dt, X);
-    mat_exp(X, phi);
-    double g1[4], yv[4], bd[4], btd[4];
-    pb_foh(phi, a, b, ws, wd, dt, g1, yv);
+    Mat4<double> phi;
+    double bd[4], btd[4];
+    if constexpr (PRE) {  // from pixbw_seg_kernel
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      btd[q] = yv[q] + (q ? 1.0 : 0.0);
-      bd[q] = g1[q] - btd[q];
+      for (int e = 0; e < 16; ++e) phi.e[e] = *pb_seg(A, n, k, e);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bd[q] = *pb_seg(A, n, k, 16 + q);
+        btd[q] = *pb_seg(A, n, k, 20 + q);
+      }
+    } else {
+      pb_seg_sys(A, n, P, k, phi, bd, btd);
     }
-    if constexpr (KEEP) {
+    if constexpr (KEEP && !PRE) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) *pb_seg(A, n, k, e) = phi.e[e];
 #pragma unroll
@@ -272,6 +297,8 @@ __device__ void pb_sweep(const PixArgs& A, int n, const PixPrm& P, double* y, do
         *pb_seg(A, n, k, 16 + q) = bd[q];
         *pb_seg(A, n, k, 20 + q) = btd[q];
       }
+    }
+    if constexpr (KEEP) {
 #pragma unroll
       for (int o = 0; o < 2; ++o)
 #pragma unroll
@@ -378,6 +405,22 @@ __device__ double pb_seg_bwd(const PixArgs& A, int n, const PixPrm& P, int k, co
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 1; j < 4; ++j) phib[4 * i + j] -= g1b[i];
+#if DEN_PIXBW_SEGPAR
+  // Phi = e^X: the four entries of dL/dX = L(X^T, dL/dPhi) the parameters reach, as
+  // <E_m, L(X^T, G)> = <L(X, E_m), G> with the L(X, E_m) of pixbw_seg_kernel
+  double fr[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s += *pb_seg(A, n, k, 24 + 16 * m + e) * phib[e];
+    fr[m] = s;
+  }
+  ab -= dt * fr[0];
+  bb -= dt * fr[1];
+  wsb += dt * fr[2];
+  wdb += dt * fr[3];
+#else
   // Phi = e^X:  dL/dX = L(X^T, dL/dPhi) = tangent of e^(X^T + eps dL/dPhi)
   Mat4<Dual> XT, R;
 #pragma unroll
@@ -389,6 +432,7 @@ __device__ double pb_seg_bwd(const PixArgs& A, int n, const PixPrm& P, int k, co
   bb -= dt * R.e[1].d;
   wsb += dt * (R.e[9].d - R.e[10].d);
   wdb += dt * (R.e[14].d - R.e[15].d);
+#endif
   // linearized_sys_params (:183-191) chain rule
   const double tin = P.kin / I1, tmil = P.kmil / I1, pp = (tin + tmil) * P.tout;
   const double aamp = 1.0 / P.ainv, aloop = 1.0 / P.linv;
@@ -406,6 +450,51 @@ __device__ double pb_seg_bwd(const PixArgs& A, int n, const PixPrm& P, int k, co
   return -(tinb * tin + tmilb * tmil) / I1;
 }
 
+// Segment-parallel part of the backward: one thread per (event, segment, m).  The per-segment work
+// -- Phi = e^X and the Frechet derivatives the adjoint needs -- does not depend on the recurrences,
+// so it leaves the per-event serial loop (a 68-event micro-batch was 68 threads running 29 segments
+// x 2 matrix exponentials each).  Thread m computes e^(X + eps E_m) in dual arithmetic, E_m the
+// directions whose entries of dL/dX the parameters reach: E_0 = e_00 (a), E_1 = e_01 (b),
+// E_2 = e_21 - e_22 (w_sf), E_3 = e_32 - e_33 (w_diff); m = 0 also stores Phi, Bd, Btd.
+__global__ __launch_bounds__(256) void pixbw_seg_kernel(PixArgs A) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t per = (int64_t)(A.S - 1) * A.N;
+  if (t >= 4 * per) return;
+  const int m = (int)(t / per);
+  const int64_t r = t - m * per;
+  const int k = (int)(r / A.N), n = (int)(r - (int64_t)k * A.N);
+  const PixPrm P = pb_params(A.prm);
+  const double I1 = (double)A.it[(int64_t)(k + 1) * A.N + n];
+  const double dt = pb_dt(A, n, k);
+  const double ws = 1.0 / P.tsf, wd = 1.0 / P.tdf;
+  double a, b;
+  pb_lin(P, I1, &a, &b);
+  Mat4<double> X;
+  pb_X(a, b, ws, wd, dt, X);
+  Mat4<Dual> XE, R;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) XE.e[e] = Dual{X.e[e], 0.0};
+  if (m == 0) XE.e[0].d = 1.0;
+  else if (m == 1) XE.e[1].d = 1.0;
+  else if (m == 2) { XE.e[9].d = 1.0; XE.e[10].d = -1.0; }
+  else { XE.e[14].d = 1.0; XE.e[15].d = -1.0; }
+  mat_exp(XE, R);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) *pb_seg(A, n, k, 24 + 16 * m + e) = R.e[e].d;
+  if (m == 0) {
+    Mat4<double> phi;
+    double bd[4], btd[4];
+    pb_seg_sys(A, n, P, k, phi, bd, btd);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) *pb_seg(A, n, k, e) = phi.e[e];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      *pb_seg(A, n, k, 16 + q) = bd[q];
+      *pb_seg(A, n, k, 20 + q) = btd[q];
+    }
+  }
+}
+
 __global__ __launch_bounds__(PIXBW_BLOCK) void pixbw_bwd_kernel(PixArgs A) {
   const int n = blockIdx.x * PIXBW_BLOCK + threadIdx.x;
   double gp[PIXBW_NPARAM] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -413,7 +502,7 @@ __global__ __launch_bounds__(PIXBW_BLOCK) void pixbw_bwd_kernel(PixArgs A) {
     const int S = A.S, N = A.N, no = A.reset ? 2 : 1;
     const PixPrm P = pb_params(A.prm);
     double y[2] = {0.0, 0.0}, den[2] = {1.0, 1.0};
-    pb_sweep<true>(A, n, P, y, den);
+    pb_sweep<true, DEN_PIXBW_SEGPAR != 0>(A, n, P, y, den);
     // adjoints of the weighted outputs
     double yb[2] = {0.0, 0.0};
     const double g = (double)A.d_out[n];
