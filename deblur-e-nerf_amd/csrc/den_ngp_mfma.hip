@@ -590,8 +590,8 @@ __global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P) {
   const int64_t s1 = s0 + P.per_split < P.n ? s0 + P.per_split : P.n;
   f32x16 acc[2] = {ngp_zero16(), ngp_zero16()};
   float bsum[2] = {0.0f, 0.0f};
-  for (int64_t c = s0 + 32 * wave; c < s1; c += 128) {
-    f32x4 a[2][4], b[2][4];
+  // the operands of chunk c + 128 load while chunk c's MFMAs run (two register sets, unrolled by 2)
+  auto load = [&](int64_t c, f32x4 (&a)[2][4], f32x4 (&b)[2][4]) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t q = c + 8 * u + 4 * h;
@@ -601,6 +601,8 @@ __global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P) {
         b[t][u] = t < nt ? ngp_dw_load(Bb, 32 * t + j, T.b_rows, P.ld, q, s1) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
+  };
+  auto compute = [&](const f32x4 (&a)[2][4], const f32x4 (&b)[2][4]) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -615,6 +617,15 @@ __global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P) {
         bsum[0] += a[0][u][e];
         bsum[1] += a[1][u][e];
       }
+  };
+  f32x4 a0[2][4], b0[2][4], a1[2][4], b1[2][4];
+  const int64_t c0 = s0 + 32 * wave;
+  if (c0 < s1) load(c0, a0, b0);
+  for (int64_t c = c0; c < s1; c += 256) {
+    if (c + 128 < s1) load(c + 128, a1, b1);
+    compute(a0, b0);
+    if (c + 256 < s1) load(c + 256, a0, b0);
+    if (c + 128 < s1) compute(a1, b1);
   }
   // tile tt: rows ngp_row(r, h), column j; bias of rows 32 t + j from both halves.  Waves 2, 3 store,
   // waves 0, 1 add theirs: the split's partial is (w0 + w2) + (w1 + w3), a fixed order.
