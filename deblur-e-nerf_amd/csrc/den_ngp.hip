@@ -271,8 +271,12 @@ __device__ __forceinline__ uint32_t ngp_index(const NgpLevel& V, int hashed, uin
       stride = 0xFFFFFFFFu;  // the loop has ended (stride > size stays true)
     }
   }
-  if (hashed && size < stride) index = cx ^ (cy * 2654435761u) ^ (cz * 805459861u);
-  return index % size;
+  // index % size without the ~40-instruction runtime division where it is not needed: a hashed
+  // level has size = 2^log2_hashmap_size (entries were capped there); a dense index of in-range cells
+  // is below 2 size (cell <= res - 1, +1 for the upper corner: < res^3 + res^2 + res < 2 size)
+  if (hashed && size < stride) return (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (size - 1);
+  if (index < size) return index;
+  return index - size < size ? index - size : index % size;
 }
 
 __device__ __forceinline__ void ngp_corners(const NgpLevel& V, int hashed, const float* x, NgpCorner& C,

@@ -29,6 +29,12 @@ namespace den {
 #ifndef DEN_NGP_SAVE_PRE
 #define DEN_NGP_SAVE_PRE 0  // 1: store the hidden pre-activations too (the VALU kernels' derivative)
 #endif
+#ifndef DEN_NGP_EXP_NO_ATOMIC
+#define DEN_NGP_EXP_NO_ATOMIC 0  // experiment builds (wrong results): cost of the scatter / the gathers
+#endif
+#ifndef DEN_NGP_EXP_LOCAL_GATHER
+#define DEN_NGP_EXP_LOCAL_GATHER 0
+#endif
 #ifndef DEN_NGP_MF_WAVES
 #define DEN_NGP_MF_WAVES 8  // waves (32-sample tiles in flight) per workgroup
 #endif
@@ -208,7 +214,8 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kerne
         ngp_corners(ngp_level_h(A.grid, q, L0 + q, h), A.grid.hashed, xn, C);
         float2 v[8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = *(const float2*)(A.table + 2 * (int64_t)C.idx[c]);
+        for (int c = 0; c < 8; ++c)
+          v[c] = *(const float2*)(A.table + 2 * (int64_t)(DEN_NGP_EXP_LOCAL_GATHER ? (C.idx[c] & 4095) : C.idx[c]));
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
           f0 = fmaf(C.w[c], v[c].x, f0);
@@ -514,7 +521,9 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_bwd_mfma_kerne
 #if DEN_NGP_AGG_RES > 0
         if (V.res <= (uint32_t)DEN_NGP_AGG_RES) emit = ngp_fold(cell, v, ok);
 #endif
-#if DEN_NGP_SCATTER_QUAD
+#if DEN_NGP_EXP_NO_ATOMIC  // experiment build only: the backward without its table scatter
+        (void)emit;
+#elif DEN_NGP_SCATTER_QUAD
         ngp_scatter_quad(A.d_table, C.idx, v, emit);
 #else
         if (emit) {
