@@ -1236,7 +1236,10 @@ int den_ngp_fwd(const den_ngp_desc* desc, int64_t n, int32_t points, const float
   A.ld = ngp_ld(n);
   A.save = train ? (float*)((char*)workspace + ngp_ws(n).save) : nullptr;
 #if DEN_NGP_MFMA
-  hipLaunchKernelGGL(ngp_fwd_mfma_kernel, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, (hipStream_t)stream, A);
+  if (A.hidden_relu)
+    hipLaunchKernelGGL(ngp_fwd_mfma_kernel<true>, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, (hipStream_t)stream, A);
+  else
+    hipLaunchKernelGGL(ngp_fwd_mfma_kernel<false>, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, (hipStream_t)stream, A);
 #else
   hipLaunchKernelGGL(ngp_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
 #endif
@@ -1274,7 +1277,10 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
   A.d_table = grad_params;
   A.dz = (float*)(ws + W.dz);
 #if DEN_NGP_MFMA
-  hipLaunchKernelGGL(ngp_bwd_mfma_kernel, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, st, A);
+  if (A.hidden_relu)
+    hipLaunchKernelGGL(ngp_bwd_mfma_kernel<true>, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, st, A);
+  else
+    hipLaunchKernelGGL(ngp_bwd_mfma_kernel<false>, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, st, A);
 #else
   hipLaunchKernelGGL(ngp_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
 #endif

@@ -46,6 +46,35 @@ namespace den {
 #endif
 constexpr int NM_WAVES = DEN_NGP_MF_WAVES, NM_THREADS = 64 * NM_WAVES;
 
+// Activations of the MFMA kernels.  DEN_NGP_FAST_ACT 1: softplus(beta = 100) with torch's threshold as
+// max(bx, 0) + log1p(exp(-|bx|)) from the hardware exp2 / log2 with log1p(t) = log(1 + t) t / ((1 + t) - 1)
+// (Goldberg) and a multiply by 0.01; its derivative from the output y as -expm1(-100 y) with
+// expm1(z) = (e^z - 1) z / log(e^z) (Kahan).  A few ulps from the libm forms (which cost ~50 VALU
+// instructions per element with the IEEE division); 0: torch's operation order (ngp_sp100 /
+// ngp_dsp100_out).
+#ifndef DEN_NGP_FAST_ACT
+#define DEN_NGP_FAST_ACT 1
+#endif
+__device__ __forceinline__ float ngp_sp100_fast(float x) {
+  const float bx = x * 100.0f;
+  const float t = __expf(-fabsf(bx));
+  const float u = 1.0f + t;
+  const float l1p = u == 1.0f ? t : __logf(u) * (t * __builtin_amdgcn_rcpf(u - 1.0f));
+  const float v = (fmaxf(bx, 0.0f) + l1p) * 0.01f;
+  return bx > 20.0f ? x : v;
+}
+__device__ __forceinline__ float ngp_dsp100_out_fast(float y) {
+  const float by = y * 100.0f;
+  const float z = -by, u = __expf(z);
+  const float em1 = u == 1.0f ? z : (u - 1.0f) * (z * __builtin_amdgcn_rcpf(__logf(u)));
+  return by > 20.0f ? 1.0f : -em1;
+}
+template <bool RELU>
+__device__ __forceinline__ float ngp_act_t(float x) {
+  if constexpr (RELU) return fmaxf(x, 0.0f);
+  else return DEN_NGP_FAST_ACT ? ngp_sp100_fast(x) : ngp_sp100(x);
+}
+
 // accumulator register r of half h holds row ngp_row(r, h) of its 32-row tile
 __device__ __forceinline__ int ngp_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 // input feature of step s, half h, when the input is a 64-wide layer output (two tiles)
@@ -180,13 +209,13 @@ __device__ __forceinline__ NgpLevel ngp_level_h(const NgpGrid& G, int q, int l1,
 }
 
 // ------------------------------------------------------------------ forward
+template <bool RELU>
 __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kernel(NgpArgs A) {
   __shared__ __attribute__((aligned(16))) float img[FI_FLOATS];
   const int E = A.enc, L = A.grid.n_levels, L0 = (L + 1) / 2;
   for (int q = threadIdx.x; q < FI_FLOATS; q += NM_THREADS) img[q] = ngp_fi(A.mlp, A.off, E, L0, A.rd, q);
   __syncthreads();
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
-  const int relu = A.hidden_relu;
   const int64_t n = A.n;
   float* S = A.save;
   const int64_t ntiles = (n + 31) / 32;
@@ -239,7 +268,7 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kerne
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pre = acc[t][r], a = ngp_act(pre, relu);
+          const float pre = acc[t][r], a = ngp_act_t<RELU>(pre);
           hb[16 * t + r] = a;
           if (S && ok) {
             const int row = 32 * t + ngp_row(r, 0);
@@ -288,7 +317,7 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kerne
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pre = acc[t][r], a = ngp_act(pre, relu);
+          const float pre = acc[t][r], a = ngp_act_t<RELU>(pre);
           hb[16 * t + r] = a;
           if (S && ok) {
             const int row = 32 * t + ngp_row(r, 0);
@@ -304,7 +333,7 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kerne
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pre = acc[t][r], a = ngp_act(pre, relu);
+          const float pre = acc[t][r], a = ngp_act_t<RELU>(pre);
           hb[16 * t + r] = a;
           if (S && ok) {
             const int row = 32 * t + ngp_row(r, 0);
@@ -394,19 +423,20 @@ __device__ __forceinline__ float ngp_dsp100_out(float y) {
   const float by = y * 100.0f;
   return by > 20.0f ? 1.0f : -expm1f(-by);
 }
-__device__ __forceinline__ float ngp_dact_row(const float* S, int P, int Q, int row, int64_t n, int relu) {
-  if (relu) return S[(Q + row) * n] > 0.0f ? 1.0f : 0.0f;
+template <bool RELU>
+__device__ __forceinline__ float ngp_dact_row(const float* S, int P, int Q, int row, int64_t n) {
+  if constexpr (RELU) return S[(Q + row) * n] > 0.0f ? 1.0f : 0.0f;
   if (DEN_NGP_SAVE_PRE) return ngp_dsp100(S[(P + row) * n]);
-  return ngp_dsp100_out(S[(Q + row) * n]);
+  return DEN_NGP_FAST_ACT ? ngp_dsp100_out_fast(S[(Q + row) * n]) : ngp_dsp100_out(S[(Q + row) * n]);
 }
 
+template <bool RELU>
 __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_bwd_mfma_kernel(NgpArgs A) {
   __shared__ __attribute__((aligned(16))) float img[BI_FLOATS];
   const int E = A.enc, L = A.grid.n_levels, rd = A.rd;
   for (int q = threadIdx.x; q < BI_FLOATS; q += NM_THREADS) img[q] = ngp_bi(A.mlp, A.off, E, rd, q);
   __syncthreads();
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
-  const int relu = A.hidden_relu;
   const int64_t n = A.n;
   const float* S = A.save;
   float* D = A.dz;
@@ -450,7 +480,7 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_bwd_mfma_kerne
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = 32 * t + ngp_row(r, 0);
-          dz[16 * t + r] = acc[t][r] * ngp_dact_row(Sh, NS_H2P, NS_H2, row, nn, relu);
+          dz[16 * t + r] = acc[t][r] * ngp_dact_row<RELU>(Sh, NS_H2P, NS_H2, row, nn);
           if (ok) Dh[(ND_Z3 + row) * nn] = dz[16 * t + r];
         }
     }
@@ -462,7 +492,7 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_bwd_mfma_kerne
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = 32 * t + ngp_row(r, 0);
-          dz[16 * t + r] = acc[t][r] * ngp_dact_row(Sh, NS_H1P, NS_H1, row, nn, relu);
+          dz[16 * t + r] = acc[t][r] * ngp_dact_row<RELU>(Sh, NS_H1P, NS_H1, row, nn);
           if (ok) Dh[(ND_Z2 + row) * nn] = dz[16 * t + r];
         }
     }
@@ -489,7 +519,7 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_bwd_mfma_kerne
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = 32 * t + ngp_row(r, 0);
-          dz[16 * t + r] = acc[t][r] * ngp_dact_row(Sh, NS_H0P, NS_H0, row, nn, relu);
+          dz[16 * t + r] = acc[t][r] * ngp_dact_row<RELU>(Sh, NS_H0P, NS_H0, row, nn);
           if (ok) Dh[(ND_Z0 + row) * nn] = dz[16 * t + r];
         }
     }
