@@ -1305,7 +1305,7 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
   Q.T[5] = NgpDwTask{ND_R, rd, 1, NS_H2, NGP_W, NGP_W, 0, O.w[4], O.b[4]};
   hipLaunchKernelGGL(ngp_dw_mfma_kernel, dim3((unsigned)W.splits, NDW_TASKS), dim3(256), 0, st, Q);
   DEN_LAUNCHED();
-  hipLaunchKernelGGL(ngp_dw_mfma_reduce_kernel, dim3((NDW_PART + 255) / 256, NDW_TASKS), dim3(256), 0, st, Q);
+  hipLaunchKernelGGL(ngp_dw_mfma_reduce_kernel, dim3((NDW_PART + 63) / 64, NDW_TASKS), dim3(256), 0, st, Q);
   DEN_LAUNCHED();
 #else
   NgpDwArgs P{};

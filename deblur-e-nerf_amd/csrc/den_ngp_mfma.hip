@@ -701,13 +701,30 @@ __global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P) {
   for (int e = threadIdx.x; e < NDW_PART; e += 256) out[e] = red[0][e] + red[1][e];
 }
 
+// 64 partial elements per workgroup, the splits in 4 interleaved groups (8 loads in flight per
+// lane), the groups combined in a fixed order
 __global__ __launch_bounds__(256) void ngp_dw_mfma_reduce_kernel(NgpDwMfArgs P) {
+  __shared__ float part[4][64];
   const NgpDwTask T = P.T[blockIdx.y];
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= NDW_PART) return;
-  const float* src = P.partial + (int64_t)blockIdx.y * P.splits * NDW_PART + e;
+  const int el = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + el;
   float s = 0.0f;
-  for (int sp = 0; sp < P.splits; ++sp) s += src[(int64_t)sp * NDW_PART];
+  if (e < NDW_PART) {
+    const float* src = P.partial + (int64_t)blockIdx.y * P.splits * NDW_PART + e;
+    int sp = g;
+    for (; sp + 28 < P.splits; sp += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(sp + 4 * u) * NDW_PART];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; sp < P.splits; sp += 4) s += src[(int64_t)sp * NDW_PART];
+  }
+  part[g][el] = s;
+  __syncthreads();
+  if (g != 0 || e >= NDW_PART) return;
+  s = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
   if (e < 2048) {
     const int tt = e >> 10, row = (e >> 5) & 31, col = e & 31;
     const int mrow = (T.mt == 2 ? 32 * tt : 0) + row, ncol = (T.mt == 2 ? 0 : 32 * tt) + col;
