@@ -1281,6 +1281,11 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
     hipLaunchKernelGGL(ngp_bwd_mfma_kernel<true>, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, st, A);
   else
     hipLaunchKernelGGL(ngp_bwd_mfma_kernel<false>, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, st, A);
+#if DEN_NGP_SCATTER_LDS
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(ngp_scatter_kernel, dim3((unsigned)((n + NSC_THREADS - 1) / NSC_THREADS)), dim3(NSC_THREADS), 0, st,
+                     A);
+#endif
 #else
   hipLaunchKernelGGL(ngp_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
 #endif

@@ -70,8 +70,9 @@ enum {
   NS_ROWS = NS_X + 3
 };
 // per-layer pre-activation gradients (rows): layer 0 (64), base output (16), head 0 (64), head 1 (64), rgb (rd)
+// and (MFMA backward with the workgroup-aggregated scatter) the encoding gradient (E rows)
 enum { ND_Z0 = 0, ND_O = ND_Z0 + NGP_W, ND_Z2 = ND_O + 1 + NGP_GEO, ND_Z3 = ND_Z2 + NGP_W, ND_R = ND_Z3 + NGP_W,
-       ND_ROWS = ND_R + 4 };
+       ND_F = ND_R + 4, ND_ROWS = ND_F + NGP_ENC };
 
 struct NgpGrid {
   int n_levels;

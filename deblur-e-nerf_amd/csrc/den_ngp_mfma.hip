@@ -35,6 +35,9 @@ namespace den {
 #ifndef DEN_NGP_EXP_LOCAL_GATHER
 #define DEN_NGP_EXP_LOCAL_GATHER 0
 #endif
+#ifndef DEN_NGP_SCATTER_LDS
+#define DEN_NGP_SCATTER_LDS 1  // table gradient through ngp_scatter_kernel (0: in the backward kernel)
+#endif
 #ifndef DEN_NGP_MF_WAVES
 #define DEN_NGP_MF_WAVES 8  // waves (32-sample tiles in flight) per workgroup
 #endif
@@ -525,6 +528,15 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_bwd_mfma_kerne
     }
     f32x16 df[1] = {ngp_zero16()};
     ngp_mm<1, 32>(img + BI_A0, dz, df, lane);
+#if DEN_NGP_SCATTER_LDS
+    // the encoding gradient goes to ND_F rows; ngp_scatter_kernel aggregates and adds it
+    if (ok) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (ngp_row(r, h) < E) Dh[(ND_F + ngp_row(r, 0)) * nn] = df[0][r];
+    }
+    continue;
+#endif
     // hash-table scatter: half h holds feature rows 2 l, 2 l + 1 of levels l = 4 a + 2 h + b
     // (registers 4 a + 2 b, + 1)
     float xn[3];
@@ -572,6 +584,68 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_bwd_mfma_kerne
 }  // namespace den
 
 namespace den {
+
+// ------------------------------------------------------------------ workgroup-aggregated table scatter
+// The memory-side atomic requests (one per distinct 64-B segment per instruction) bound the table
+// gradient: 32 per sample in the configs[3] emulation with the in-kernel fold + quad scatter.  Here a
+// workgroup takes 256 consecutive samples (ray-ordered: one or two rays) and, level by level, inserts
+// their 8 corner contributions into an LDS hash table keyed by the entry index (open addressing, slot
+// = index mod 4096, at most 2,048 records so never full; LDS float atomics merge equal entries), then
+// walks the table in slot order with lane pairs on the two features of one entry: entries that are
+// neighbours in memory (x-neighbour cells: dense rows, or the aligned 8-entry groups of a hashed level)
+// sit in neighbouring slots, so one 64-B request carries up to 8 entries' adds.
+constexpr int NSC_SLOTS = 4096, NSC_THREADS = 256;
+constexpr uint32_t NSC_EMPTY = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(NSC_THREADS) void ngp_scatter_kernel(NgpArgs A) {
+  __shared__ uint32_t key[NSC_SLOTS];
+  __shared__ float val[2][NSC_SLOTS];
+  const int tid = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * NSC_THREADS + tid;
+  const bool ok = i < A.n;
+  const int64_t ic = ok ? i : A.n - 1;
+  float xn[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) xn[a] = A.save[(int64_t)(NS_X + a) * A.ld + ic];
+  for (int l = 0; l < A.grid.n_levels; ++l) {
+    for (int q = tid; q < NSC_SLOTS; q += NSC_THREADS) {
+      key[q] = NSC_EMPTY;
+      val[0][q] = 0.0f;
+      val[1][q] = 0.0f;
+    }
+    __syncthreads();
+    if (ok) {
+      const float g0 = A.dz[(int64_t)(ND_F + 2 * l) * A.ld + i], g1 = A.dz[(int64_t)(ND_F + 2 * l + 1) * A.ld + i];
+      if (g0 != 0.0f || g1 != 0.0f) {
+        NgpCorner C;
+        ngp_corners(A.grid, l, xn, C);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const uint32_t e = C.idx[c];
+          uint32_t s = e & (NSC_SLOTS - 1);
+          while (true) {
+            const uint32_t k = key[s];
+            if (k == e) break;
+            if (k == NSC_EMPTY) {
+              const uint32_t old = atomicCAS(&key[s], NSC_EMPTY, e);
+              if (old == NSC_EMPTY || old == e) break;
+            }
+            s = (s + 1) & (NSC_SLOTS - 1);
+          }
+          atomicAdd(&val[0][s], C.w[c] * g0);
+          atomicAdd(&val[1][s], C.w[c] * g1);
+        }
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < 2 * NSC_SLOTS; q += NSC_THREADS) {
+      const int s = q >> 1, f = q & 1;
+      const uint32_t k = key[s];
+      if (k != NSC_EMPTY) unsafeAtomicAdd(A.d_table + 2 * (int64_t)k + f, val[f][s]);
+    }
+    __syncthreads();
+  }
+}
 
 // ------------------------------------------------------------------ weight gradients on MFMA
 // dW[o][k] = sum_s dZ[o][s] X[k][s], db[o] = sum_s dZ[o][s] with the samples as the K dimension of
