@@ -597,6 +597,8 @@ namespace den {
 constexpr int NSC_SLOTS = 4096, NSC_THREADS = 256;
 constexpr uint32_t NSC_EMPTY = 0xFFFFFFFFu;
 
+// Same-cell lanes fold first (ngp_fold: coarse levels put whole runs of a ray in one cell, which would
+// serialise on the LDS atomics); the emission pass leaves the table empty for the next level.
 __global__ __launch_bounds__(NSC_THREADS) void ngp_scatter_kernel(NgpArgs A) {
   __shared__ uint32_t key[NSC_SLOTS];
   __shared__ float val[2][NSC_SLOTS];
@@ -607,41 +609,52 @@ __global__ __launch_bounds__(NSC_THREADS) void ngp_scatter_kernel(NgpArgs A) {
   float xn[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) xn[a] = A.save[(int64_t)(NS_X + a) * A.ld + ic];
+  for (int q = tid; q < NSC_SLOTS; q += NSC_THREADS) {
+    key[q] = NSC_EMPTY;
+    val[0][q] = 0.0f;
+    val[1][q] = 0.0f;
+  }
+  __syncthreads();
   for (int l = 0; l < A.grid.n_levels; ++l) {
-    for (int q = tid; q < NSC_SLOTS; q += NSC_THREADS) {
-      key[q] = NSC_EMPTY;
-      val[0][q] = 0.0f;
-      val[1][q] = 0.0f;
-    }
-    __syncthreads();
-    if (ok) {
-      const float g0 = A.dz[(int64_t)(ND_F + 2 * l) * A.ld + i], g1 = A.dz[(int64_t)(ND_F + 2 * l + 1) * A.ld + i];
-      if (g0 != 0.0f || g1 != 0.0f) {
-        NgpCorner C;
-        ngp_corners(A.grid, l, xn, C);
+    const float g0 = ok ? A.dz[(int64_t)(ND_F + 2 * l) * A.ld + ic] : 0.0f;
+    const float g1 = ok ? A.dz[(int64_t)(ND_F + 2 * l + 1) * A.ld + ic] : 0.0f;
+    NgpCorner C;
+    uint32_t cell[3];
+    ngp_corners(A.grid, l, xn, C, cell);
+    float v[16];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const uint32_t e = C.idx[c];
-          uint32_t s = e & (NSC_SLOTS - 1);
-          while (true) {
-            const uint32_t k = key[s];
-            if (k == e) break;
-            if (k == NSC_EMPTY) {
-              const uint32_t old = atomicCAS(&key[s], NSC_EMPTY, e);
-              if (old == NSC_EMPTY || old == e) break;
-            }
-            s = (s + 1) & (NSC_SLOTS - 1);
+    for (int c = 0; c < 8; ++c) {
+      v[2 * c] = C.w[c] * g0;
+      v[2 * c + 1] = C.w[c] * g1;
+    }
+    const bool emit = ngp_fold(cell, v, ok) && (g0 != 0.0f || g1 != 0.0f);
+    if (emit) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint32_t e = C.idx[c];
+        uint32_t s = e & (NSC_SLOTS - 1);
+        while (true) {
+          const uint32_t k = key[s];
+          if (k == e) break;
+          if (k == NSC_EMPTY) {
+            const uint32_t old = atomicCAS(&key[s], NSC_EMPTY, e);
+            if (old == NSC_EMPTY || old == e) break;
           }
-          atomicAdd(&val[0][s], C.w[c] * g0);
-          atomicAdd(&val[1][s], C.w[c] * g1);
+          s = (s + 1) & (NSC_SLOTS - 1);
         }
+        atomicAdd(&val[0][s], v[2 * c]);
+        atomicAdd(&val[1][s], v[2 * c + 1]);
       }
     }
     __syncthreads();
     for (int q = tid; q < 2 * NSC_SLOTS; q += NSC_THREADS) {
       const int s = q >> 1, f = q & 1;
       const uint32_t k = key[s];
-      if (k != NSC_EMPTY) unsafeAtomicAdd(A.d_table + 2 * (int64_t)k + f, val[f][s]);
+      if (k != NSC_EMPTY) {
+        unsafeAtomicAdd(A.d_table + 2 * (int64_t)k + f, val[f][s]);
+        val[f][s] = 0.0f;
+        if (f == 0) key[s] = NSC_EMPTY;  // the f = 1 lane of the pair read it in the same instruction
+      }
     }
     __syncthreads();
   }
