@@ -1308,7 +1308,12 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
   Q.T[3] = NgpDwTask{ND_Z3, 32, 1, NS_H1, NGP_W, NGP_W, 0, O.w[3], O.b[3]};
   Q.T[4] = NgpDwTask{ND_Z3 + 32, 32, 1, NS_H1, NGP_W, NGP_W, 32, O.w[3], O.b[3]};
   Q.T[5] = NgpDwTask{ND_R, rd, 1, NS_H2, NGP_W, NGP_W, 0, O.w[4], O.b[4]};
-  hipLaunchKernelGGL(ngp_dw_mfma_kernel, dim3((unsigned)W.splits, NDW_TASKS), dim3(256), 0, st, Q);
+  // tasks 0, 2: two row tiles; 1, 3, 4, 5: one
+  hipLaunchKernelGGL(ngp_dw_mfma_kernel<2>, dim3((unsigned)W.splits, 2), dim3(256), 0, st, Q, 0, 2);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(ngp_dw_mfma_kernel<1>, dim3((unsigned)W.splits, 1), dim3(256), 0, st, Q, 1, 0);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(ngp_dw_mfma_kernel<1>, dim3((unsigned)W.splits, 3), dim3(256), 0, st, Q, 3, 1);
   DEN_LAUNCHED();
   hipLaunchKernelGGL(ngp_dw_mfma_reduce_kernel, dim3((NDW_PART + 63) / 64, NDW_TASKS), dim3(256), 0, st, Q);
   DEN_LAUNCHED();

@@ -705,11 +705,15 @@ __device__ __forceinline__ f32x4 ngp_dw_load(const float* base, int row, int row
   return v;
 }
 
-__global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P) {
+// MT: row tiles of the launch's tasks (2: layers 0 and 2; 1: the others) -- a compile-time operand
+// shape keeps the double-buffered operands at 3 x 4 x 4 registers per buffer
+template <int MT>
+__global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P, int task0, int task_stride) {
   __shared__ __attribute__((aligned(16))) float red[2][NDW_PART];
-  const NgpDwTask T = P.T[blockIdx.y];
+  const int task = task0 + (int)blockIdx.y * task_stride;
+  const NgpDwTask T = P.T[task];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-  const int mt = T.mt, nt = 3 - T.mt;
+  constexpr int mt = MT, nt = 3 - MT;
   const float* Ab = P.dz + (int64_t)T.a_row * P.ld;
   const float* Bb = P.save + (int64_t)T.b_row * P.ld;
   const int64_t s0 = (int64_t)blockIdx.x * P.per_split;
@@ -717,34 +721,33 @@ __global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P) {
   f32x16 acc[2] = {ngp_zero16(), ngp_zero16()};
   float bsum[2] = {0.0f, 0.0f};
   // the operands of chunk c + 128 load while chunk c's MFMAs run (two register sets, unrolled by 2)
-  auto load = [&](int64_t c, f32x4 (&a)[2][4], f32x4 (&b)[2][4]) {
+  auto load = [&](int64_t c, f32x4 (&a)[mt][4], f32x4 (&b)[nt][4]) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t q = c + 8 * u + 4 * h;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        a[t][u] = t < mt ? ngp_dw_load(Ab, 32 * t + j, T.a_rows, P.ld, q, s1) : f32x4{0.f, 0.f, 0.f, 0.f};
-        b[t][u] = t < nt ? ngp_dw_load(Bb, 32 * t + j, T.b_rows, P.ld, q, s1) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      for (int t = 0; t < mt; ++t) a[t][u] = ngp_dw_load(Ab, 32 * t + j, T.a_rows, P.ld, q, s1);
+#pragma unroll
+      for (int t = 0; t < nt; ++t) b[t][u] = ngp_dw_load(Bb, 32 * t + j, T.b_rows, P.ld, q, s1);
     }
   };
-  auto compute = [&](const f32x4 (&a)[2][4], const f32x4 (&b)[2][4]) {
+  auto compute = [&](const f32x4 (&a)[mt][4], const f32x4 (&b)[nt][4]) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        if (mt == 2) {
+        if constexpr (mt == 2) {
           acc[0] = ngp_mfma(a[0][u][e], b[0][u][e], acc[0]);
           acc[1] = ngp_mfma(a[1][u][e], b[0][u][e], acc[1]);
+          bsum[1] += a[1][u][e];
         } else {
           acc[0] = ngp_mfma(a[0][u][e], b[0][u][e], acc[0]);
           acc[1] = ngp_mfma(a[0][u][e], b[1][u][e], acc[1]);
         }
         bsum[0] += a[0][u][e];
-        bsum[1] += a[1][u][e];
       }
   };
-  f32x4 a0[2][4], b0[2][4], a1[2][4], b1[2][4];
+  f32x4 a0[mt][4], b0[nt][4], a1[mt][4], b1[nt][4];
   const int64_t c0 = s0 + 32 * wave;
   if (c0 < s1) load(c0, a0, b0);
   for (int64_t c = c0; c < s1; c += 256) {
@@ -784,7 +787,7 @@ __global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P) {
     }
   }
   __syncthreads();
-  float* out = P.partial + ((int64_t)blockIdx.y * P.splits + blockIdx.x) * NDW_PART;
+  float* out = P.partial + ((int64_t)task * P.splits + blockIdx.x) * NDW_PART;
   for (int e = threadIdx.x; e < NDW_PART; e += 256) out[e] = red[0][e] + red[1][e];
 }
 
