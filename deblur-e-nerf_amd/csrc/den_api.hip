@@ -616,7 +616,10 @@ int den_pixbw_fwd(int32_t S, int32_t N, int32_t reset, const float* it, const do
   if (!out || (reset && !delta_out)) return fail(DEN_EINVAL, "out (and delta_out for a reset call) are required");
   A.out = out;
   A.delta_out = delta_out;
-  hipLaunchKernelGGL(pixbw_fwd_kernel, dim3((unsigned)den_pixbw_blocks(N)), dim3(PIXBW_BLOCK), 0, (hipStream_t)stream, A);
+  if (DEN_PIXBW_SEGPAR && S - 1 <= PIXBW_WAVE_SEGS)
+    hipLaunchKernelGGL(pixbw_fwd_wave_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, (hipStream_t)stream, A);
+  else
+    hipLaunchKernelGGL(pixbw_fwd_kernel, dim3((unsigned)den_pixbw_blocks(N)), dim3(PIXBW_BLOCK), 0, (hipStream_t)stream, A);
   DEN_LAUNCHED();
   return DEN_OK;
 }

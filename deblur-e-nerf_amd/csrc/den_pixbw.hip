@@ -262,8 +262,10 @@ __device__ __forceinline__ void pb_seg_sys(const PixArgs& A, int n, const PixPrm
 // Forward sweep of event n (discretized_sys_to_weight, :283-294, fused with the weighted log-sum of
 // :406-415): segments k = S-2 .. 0 with c = c_{k+1} = C Phi[S-2] ... Phi[k+1]:
 //   w[k+1] += c Btd_k,   w[k] = c Bd_k (completed by the next step),   c <- c Phi_k.
+// PRE: Phi / Bd / Btd from the workspace (pixbw_seg_kernel); lds != null: from an LDS image [k][24]
 template <bool KEEP, bool PRE = false>
-__device__ void pb_sweep(const PixArgs& A, int n, const PixPrm& P, double* y, double* den) {
+__device__ void pb_sweep(const PixArgs& A, int n, const PixPrm& P, double* y, double* den,
+                         const double* lds = nullptr) {
   const int S = A.S, N = A.N, no = A.reset ? 2 : 1;
   const double ws = 1.0 / P.tsf, wd = 1.0 / P.tdf;
   double c[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
@@ -285,6 +287,14 @@ __device__ void pb_sweep(const PixArgs& A, int n, const PixPrm& P, double* y, do
       for (int q = 0; q < 4; ++q) {
         bd[q] = *pb_seg(A, n, k, 16 + q);
         btd[q] = *pb_seg(A, n, k, 20 + q);
+      }
+    } else if (lds) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) phi.e[e] = lds[k * 24 + e];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bd[q] = lds[k * 24 + 16 + q];
+        btd[q] = lds[k * 24 + 20 + q];
       }
     } else {
       pb_seg_sys(A, n, P, k, phi, bd, btd);
@@ -354,6 +364,41 @@ __global__ __launch_bounds__(PIXBW_BLOCK) void pixbw_fwd_kernel(PixArgs A) {
     A.delta_out[n] = (float)(y[1] - y[0]);
   } else {
     // decay of the reset offset (:435-446); reset_dt is cast to f32 as the reference does
+    const double rdt = (double)(float)(A.out_ts[n] - A.reset_ts[n]) * PIXBW_NS;
+    A.out[n] = (float)(y[0] - (double)A.delta_in[n] * exp(-rdt / P.tdf));
+  }
+}
+
+// Forward with one wave per event: lane k computes segment k's Phi / Bd / Btd (the matrix
+// exponentials run in parallel) into LDS, lane 0 runs the weight recurrence over them.  A 68-event
+// micro-batch was 68 threads each running S - 1 exponentials in sequence.  S - 1 <= PIXBW_WAVE_SEGS.
+constexpr int PIXBW_WAVE_SEGS = 63;
+__global__ __launch_bounds__(256) void pixbw_fwd_wave_kernel(PixArgs A) {
+  __shared__ double seg[4][PIXBW_WAVE_SEGS * 24];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + w;
+  const PixPrm P = pb_params(A.prm);
+  if (n < A.N && lane < A.S - 1) {
+    Mat4<double> phi;
+    double bd[4], btd[4];
+    pb_seg_sys(A, n, P, lane, phi, bd, btd);
+    double* d = seg[w] + lane * 24;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) d[e] = phi.e[e];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      d[16 + q] = bd[q];
+      d[20 + q] = btd[q];
+    }
+  }
+  __syncthreads();
+  if (n >= A.N || lane != 0) return;
+  double y[2] = {0.0, 0.0}, den[2] = {1.0, 1.0};
+  pb_sweep<false>(A, n, P, y, den, seg[w]);
+  if (A.reset) {
+    A.out[n] = (float)y[0];
+    A.delta_out[n] = (float)(y[1] - y[0]);
+  } else {
     const double rdt = (double)(float)(A.out_ts[n] - A.reset_ts[n]) * PIXBW_NS;
     A.out[n] = (float)(y[0] - (double)A.delta_in[n] * exp(-rdt / P.tdf));
   }
