@@ -45,7 +45,7 @@ namespace den {
 #define DEN_NGP_MF_OCC 4  // waves per SIMD the field kernels are compiled for (128 VGPRs; 2 / 3 measured slower)
 #endif
 #ifndef DEN_NGP_MF_GRID
-#define DEN_NGP_MF_GRID 4096  // workgroups at most (each loops over tiles; the image is built once per workgroup)
+#define DEN_NGP_MF_GRID 512  // workgroups at most: 2 resident per CU, each loops over tiles (1024 / 2048 / 4096 measured slower)
 #endif
 constexpr int NM_WAVES = DEN_NGP_MF_WAVES, NM_THREADS = 64 * NM_WAVES;
 

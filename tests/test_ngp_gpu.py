@@ -97,6 +97,37 @@ def test_ngp_field_ragged_matches_oracle(n_levels, n, rd, hidden, radiance):
         assert torch.equal(f.query_density(x.to(DEV)).reshape(-1), sig.detach().reshape(-1))
 
 
+def test_ngp_field_large_batch_equals_chunks():
+    """Past DEN_NGP_MF_GRID workgroups x 8 waves x 32 samples the field kernels loop over tiles: a
+    140,000-sample call equals 4,096-sample chunks bit for bit in the forward (per-sample
+    arithmetic does not depend on the grid) and to 1e-4 in the gradients (atomic and split order)."""
+    from deblur_e_nerf.external import ngp
+    torch.manual_seed(4)
+    f = ngp.NGPradianceField(aabb=[-1.5, -1.5, -1.5, 1.5, 1.5, 1.5], pos_encoding_config=dict(ongp.POS_ENCODING),
+                             mlp_base_config=dict(ongp.MLP_BASE, hidden_activation=torch.nn.Softplus(beta=100),
+                                                  density_activation=ngp.shifted_trunc_exp),
+                             mlp_head_config=dict(ongp.MLP_HEAD, hidden_activation=torch.nn.Softplus(beta=100),
+                                                  radiance_activation=torch.nn.Softplus(beta=1), output_dim=3)).to(DEV)
+    with torch.no_grad():
+        f.mlp_base[0].params.mul_(1e3)
+    n = 140_000
+    x = torch.rand(n, 3, device=DEV) * 3 - 1.5
+    d = torch.nn.functional.normalize(torch.randn(n, 3, device=DEV), dim=-1)
+    g_rgb, g_sig = torch.randn(n, 3, device=DEV), torch.randn(n, 1, device=DEV)
+    rgb, sig = f(x, d)
+    ((rgb * g_rgb).sum() + (sig * g_sig).sum()).backward()
+    full = {k: p.grad.clone() for k, p in f.named_parameters()}
+    f.zero_grad()
+    outs = []
+    for s in range(0, n, 4096):
+        r, q = f(x[s:s + 4096], d[s:s + 4096])
+        ((r * g_rgb[s:s + 4096]).sum() + (q * g_sig[s:s + 4096]).sum()).backward()
+        outs.append((r.detach(), q.detach()))
+    assert torch.equal(rgb.detach(), torch.cat([o[0] for o in outs])) and torch.equal(sig.detach(), torch.cat([o[1] for o in outs]))
+    errs = {k: _tensor_rel(full[k], p.grad) for k, p in f.named_parameters()}
+    assert max(errs.values()) < 1e-4, errs
+
+
 @pytest.mark.parametrize("otype,log2", [("HashGrid", 19), ("HashGrid", 12), ("DenseGrid", 19)])
 def test_hashgrid_matches_oracle(otype, log2):
     """den_hashgrid_fwd / bwd (tcnn.Encoding) vs oracle/tcnn.py on random points, including
