@@ -22,6 +22,7 @@
 #include "den_ngp_mfma.hip"
 #include "den_pixbw.hip"
 #include "den_render.hip"
+#include "den_raygrad.hip"
 
 using namespace den;
 
@@ -533,6 +534,59 @@ int den_render_bwd_part(const den_render_desc* d, const den_render_io* io, const
                       : render_bwd_impl<1>(d, io, g, (hipStream_t)stream, part);
 }
 
+size_t den_render_ray_grad_workspace_bytes(const den_render_desc* d) {
+  if (check_desc(d) != DEN_OK) return 0;
+  return (size_t)d->n_rays * d->n_samples * 6 * sizeof(float);
+}
+
+int den_render_ray_grad(const den_render_desc* d, const den_render_io* io, const float* params, int32_t n_rays_out,
+                        int64_t n_valid, void* rg_workspace, float* d_rays_o, float* d_rays_d, void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (!d->train) return fail(DEN_EINVAL, "den_render_ray_grad needs a train=1 forward and its den_render_bwd");
+  if (!io || !io->workspace || !io->rays_o || !io->rays_d || !params || !rg_workspace || !d_rays_o || !d_rays_d ||
+      (d->points == 0 && !io->jitter) || (d->points == 2 && (!io->ray_indices || !io->t_starts || !io->t_ends)))
+    return fail(DEN_EINVAL, "null pointer");
+  const int64_t n = (int64_t)d->n_rays * d->n_samples;
+  if (d->points == 2 && (n_rays_out <= 0 || n_valid < 0 || n_valid > n))
+    return fail(DEN_EINVAL, "points = 2 needs n_rays_out > 0 and 0 <= n_valid <= samples");
+  const WsLayout L = ws_layout(d);
+  const char* ws = (const char*)io->workspace;
+  RayGradArgs G{};
+  G.points = d->points;
+  G.contraction = d->contraction;
+  G.rd = d->radiance_dim;
+  G.n_samples = d->n_samples;
+  G.n = n;
+  for (int i = 0; i < 6; ++i) G.aabb[i] = d->aabb[i];
+  G.near_p = d->near_plane;
+  G.far_p = d->far_plane;
+  G.rays_o = io->rays_o;
+  G.rays_d = io->rays_d;
+  G.jitter = io->jitter;
+  G.ray_idx = io->ray_indices;
+  G.t0 = io->t_starts;
+  G.t1 = io->t_ends;
+  G.per_sample = (float*)rg_workspace;
+  RayGradMlp M{params, ws + L.act[D_Z0 + 0], ws + L.act[D_Z0 + 5], ws + L.act[D_ZG],
+               d->mode == DEN_MODE_F32 ? 1.0f : (float)KAPPA};
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned grid = (unsigned)((n + RG_THREADS - 1) / RG_THREADS);
+  if (d->mode == DEN_MODE_F32) hipLaunchKernelGGL(raygrad_mlp_kernel<0>, dim3(grid), dim3(RG_THREADS), 0, st, G, M);
+  else hipLaunchKernelGGL(raygrad_mlp_kernel<1>, dim3(grid), dim3(RG_THREADS), 0, st, G, M);
+  DEN_LAUNCHED();
+  if (d->points == 1) {
+    hipLaunchKernelGGL(raygrad_split_kernel, dim3(grid), dim3(RG_THREADS), 0, st, n, G.per_sample, d_rays_o,
+                       d_rays_d);
+  } else {
+    const int R = d->points == 0 ? d->n_rays : n_rays_out;
+    hipLaunchKernelGGL(raygrad_reduce_kernel, dim3((R + 3) / 4), dim3(256), 0, st, R, d->points, d->n_samples,
+                       io->ray_indices, n_valid, G.per_sample, d_rays_o, d_rays_d);
+  }
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
 int den_sum_partials(int32_t n, int32_t nb, const float* part, float* out, void* stream) {
   if (n <= 0 || nb <= 0 || !part || !out) return fail(DEN_EINVAL, "bad arguments");
   hipLaunchKernelGGL(sum_partials_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, n, nb, part, out);
@@ -585,6 +639,25 @@ int den_pixbw_sample_ts(int32_t S, int32_t N, const double* gen, const double* o
   const int64_t tot = (int64_t)S * N;
   hipLaunchKernelGGL(pixbw_sample_ts_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      S, N, gen, out_ts, rate, cum, ts);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_pixbw_sample_ts_bwd(int32_t S, int32_t N, const double* g_sample_ts, double* d_output_ts, void* stream) {
+  if (S < 2 || N <= 0 || !g_sample_ts || !d_output_ts) return fail(DEN_EINVAL, "bad arguments");
+  hipLaunchKernelGGL(pixbw_sample_ts_bwd_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     S, N, g_sample_ts, d_output_ts);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_pixbw_decay_ts_bwd(int32_t N, const double* output_ts, const double* reset_ts, const float* params,
+                           const float* delta_in, const float* d_out, double* d_output_ts, double* d_reset_ts,
+                           void* stream) {
+  if (N <= 0 || !output_ts || !reset_ts || !params || !delta_in || !d_out) return fail(DEN_EINVAL, "bad arguments");
+  if (!d_output_ts && !d_reset_ts) return DEN_OK;
+  hipLaunchKernelGGL(pixbw_decay_ts_bwd_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     N, output_ts, reset_ts, params, delta_in, d_out, d_output_ts, d_reset_ts);
   DEN_LAUNCHED();
   return DEN_OK;
 }
@@ -764,6 +837,18 @@ int den_pixel_rays(int32_t M, int32_t N, const float* k_inv, const float* pixel,
   return DEN_OK;
 }
 
+int den_pixel_rays_bwd(int32_t M, int32_t N, const float* k_inv, const float* pixel, const float* t_rot,
+                       const float* g_ray_o, const float* g_ray_d, float* d_t_pos, float* d_t_rot, void* stream) {
+  if (M <= 0 || N <= 0 || (int64_t)M * N > (int64_t)INT32_MAX * 64 || !k_inv || !pixel || !t_rot ||
+      (!d_t_pos && !d_t_rot))
+    return fail(DEN_EINVAL, "bad arguments");
+  const int64_t n = (int64_t)M * N;
+  hipLaunchKernelGGL(pixel_rays_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, M,
+                     N, k_inv, pixel, t_rot, g_ray_o, g_ray_d, d_t_pos, d_t_rot);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
 // ------------------------------------------------------------------ packed rendering (den_march.hip)
 static int march_args(int32_t n_rays, const float* o, const float* d, const float* t_min, const float* t_max,
                       const float* roi, const int32_t* res, const uint8_t* grid, int32_t contraction, float step,
@@ -926,9 +1011,9 @@ int den_compact(int32_t n_rays, const int64_t* offsets, const uint8_t* keep, con
   return DEN_OK;
 }
 
-int den_composite_fwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts, const float* t_ends,
-                      const float* sigmas, const float* rgbs, const float* bkgd, float* colors, float* opacities,
-                      float* depths, void* stream) {
+static int composite_fwd_impl(int alpha, int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts,
+                              const float* t_ends, const float* sigmas, const float* rgbs, const float* bkgd,
+                              float* colors, float* opacities, float* depths, void* stream) {
   if (n_rays <= 0 || rd < 1 || rd > 3 || !offsets || !t_starts || !t_ends || !sigmas || !rgbs || !colors ||
       !opacities || !depths)
     return fail(DEN_EINVAL, "bad arguments");
@@ -944,6 +1029,7 @@ int den_composite_fwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const 
   C.color = colors;
   C.opacity = opacities;
   C.depth = depths;
+  C.alpha = alpha;
   hipLaunchKernelGGL(composite_fwd_kernel, dim3((n_rays + RAYS_PER_WG - 1) / RAYS_PER_WG), dim3(64 * RAYS_PER_WG), 0,
                      (hipStream_t)stream, C);
   DEN_LAUNCHED();
@@ -954,10 +1040,11 @@ size_t den_composite_workspace_bytes(int32_t n_rays, int32_t rd) {
   return n_rays > 0 && rd > 0 ? (size_t)n_rays * rd * sizeof(float) : 0;
 }
 
-int den_composite_bwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts, const float* t_ends,
-                      const float* sigmas, const float* rgbs, const float* bkgd, const float* d_colors,
-                      const float* d_opacities, const float* d_depths, float* d_sigmas, float* d_rgbs, float* d_bkgd,
-                      void* workspace, void* stream) {
+static int composite_bwd_impl(int alpha, int32_t n_rays, int32_t rd, const int64_t* offsets,
+                              const float* t_starts, const float* t_ends, const float* sigmas, const float* rgbs,
+                              const float* bkgd, const float* d_colors, const float* d_opacities,
+                              const float* d_depths, float* d_sigmas, float* d_rgbs, float* d_bkgd, void* workspace,
+                              void* stream) {
   if (n_rays <= 0 || rd < 1 || rd > 3 || !offsets || !t_starts || !t_ends || !sigmas || !rgbs || !d_colors ||
       !d_sigmas || !d_rgbs || (d_bkgd && (!bkgd || !workspace)))
     return fail(DEN_EINVAL, "bad arguments");
@@ -976,6 +1063,7 @@ int den_composite_bwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const 
   C.d_sigma = d_sigmas;
   C.d_rgb = d_rgbs;
   C.bkgd_partial = d_bkgd ? (float*)workspace : nullptr;
+  C.alpha = alpha;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(composite_bwd_kernel, dim3((n_rays + RAYS_PER_WG - 1) / RAYS_PER_WG), dim3(64 * RAYS_PER_WG), 0,
                      st, C);
@@ -985,6 +1073,33 @@ int den_composite_bwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const 
     DEN_LAUNCHED();
   }
   return DEN_OK;
+}
+
+int den_composite_fwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts, const float* t_ends,
+                      const float* sigmas, const float* rgbs, const float* bkgd, float* colors, float* opacities,
+                      float* depths, void* stream) {
+  return composite_fwd_impl(0, n_rays, rd, offsets, t_starts, t_ends, sigmas, rgbs, bkgd, colors, opacities, depths,
+                            stream);
+}
+int den_composite_alpha_fwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts,
+                            const float* t_ends, const float* alphas, const float* rgbs, const float* bkgd,
+                            float* colors, float* opacities, float* depths, void* stream) {
+  return composite_fwd_impl(1, n_rays, rd, offsets, t_starts, t_ends, alphas, rgbs, bkgd, colors, opacities, depths,
+                            stream);
+}
+int den_composite_bwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts, const float* t_ends,
+                      const float* sigmas, const float* rgbs, const float* bkgd, const float* d_colors,
+                      const float* d_opacities, const float* d_depths, float* d_sigmas, float* d_rgbs, float* d_bkgd,
+                      void* workspace, void* stream) {
+  return composite_bwd_impl(0, n_rays, rd, offsets, t_starts, t_ends, sigmas, rgbs, bkgd, d_colors, d_opacities,
+                            d_depths, d_sigmas, d_rgbs, d_bkgd, workspace, stream);
+}
+int den_composite_alpha_bwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts,
+                            const float* t_ends, const float* alphas, const float* rgbs, const float* bkgd,
+                            const float* d_colors, const float* d_opacities, const float* d_depths, float* d_alphas,
+                            float* d_rgbs, float* d_bkgd, void* workspace, void* stream) {
+  return composite_bwd_impl(1, n_rays, rd, offsets, t_starts, t_ends, alphas, rgbs, bkgd, d_colors, d_opacities,
+                            d_depths, d_alphas, d_rgbs, d_bkgd, workspace, stream);
 }
 
 constexpr int OCC_NB = 1024;  // fixed reduction width (deterministic mean)
@@ -1049,6 +1164,19 @@ int den_trajectory(int64_t n, int32_t C, const int64_t* cam_ts, const float* cam
   if (n == 0) return DEN_OK;
   TrajArgs T{n, C, cam_ts, cam_pos, cam_quat, query_ts, position, rotation, status};
   hipLaunchKernelGGL(trajectory_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, T);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_trajectory_bwd(int64_t n, int32_t C, const int64_t* cam_ts, const float* cam_pos, const float* cam_quat,
+                       const double* query_ts, const float* g_position, const float* g_rotation, double* d_query_ts,
+                       void* stream) {
+  if (n < 0 || C < 2 || !cam_ts || !cam_pos || !cam_quat || (n > 0 && (!query_ts || !d_query_ts)))
+    return fail(DEN_EINVAL, "bad arguments (a trajectory needs >= 2 poses)");
+  if (n == 0) return DEN_OK;
+  TrajArgs T{n, C, cam_ts, cam_pos, cam_quat, query_ts, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL(trajectory_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, T,
+                     g_position, g_rotation, d_query_ts);
   DEN_LAUNCHED();
   return DEN_OK;
 }
@@ -1340,6 +1468,62 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
   hipLaunchKernelGGL(ngp_dw_reduce_kernel, dim3((NGP_DW_PM * NGP_DW_PK + 255) / 256, 5), dim3(256), 0, st, P);
   DEN_LAUNCHED();
 #endif
+  return DEN_OK;
+}
+
+size_t den_ngp_ray_grad_workspace_bytes(int64_t n) { return n > 0 ? (size_t)n * 6 * sizeof(float) : 0; }
+
+int den_ngp_ray_grad(const den_ngp_desc* desc, int64_t n, int32_t points, int32_t n_rays, const float* x,
+                     const float* d, const int32_t* ray_idx, const float* t0, const float* t1, const float* params,
+                     void* workspace, void* rg_workspace, float* d_x, float* d_d, void* stream) {
+  NgpGrid g;
+  int64_t tfl;
+  if (!ngp_grid(desc, &g, &tfl)) return fail(DEN_EUNSUPPORTED, "unsupported ngp descriptor");
+#if !(DEN_NGP_MFMA && DEN_NGP_SCATTER_LDS)
+  return fail(DEN_EUNSUPPORTED, "the ngp ray gradient reads the encoding-gradient rows of the MFMA backward");
+#endif
+  if (n < 0 || (points != 1 && points != 2) || !params || !workspace || !d_x || !d_d || (n > 0 && !rg_workspace) ||
+      (n > 0 && (!x || !d)) || (points == 2 && (n_rays <= 0 || (n > 0 && (!ray_idx || !t0 || !t1)))))
+    return fail(DEN_EINVAL, "bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    if (points == 2) {
+      DEN_HIP(hipMemsetAsync(d_x, 0, (size_t)n_rays * 3 * 4, st));
+      DEN_HIP(hipMemsetAsync(d_d, 0, (size_t)n_rays * 3 * 4, st));
+    }
+    return DEN_OK;
+  }
+  const NgpWs W = ngp_ws(n);
+  char* ws = (char*)workspace;
+  RayGradArgs G{};
+  G.points = points;
+  G.contraction = desc->contraction;
+  G.rd = desc->radiance_dim;
+  G.n = n;
+  for (int i = 0; i < 6; ++i) G.aabb[i] = desc->aabb[i];
+  G.rays_o = x;
+  G.rays_d = d;
+  G.ray_idx = ray_idx;
+  G.t0 = t0;
+  G.t1 = t1;
+  G.per_sample = (float*)rg_workspace;
+  RayGradNgp Q{};
+  Q.table = params;
+  Q.mlp = params + tfl;
+  Q.off = ngp_offsets(2 * g.n_levels, desc->radiance_dim);
+  Q.grid = g;
+  Q.ld = ngp_ld(n);
+  Q.save = (const float*)(ws + W.save);
+  Q.dz = (const float*)(ws + W.dz);
+  const unsigned grid = (unsigned)((n + RG_THREADS - 1) / RG_THREADS);
+  hipLaunchKernelGGL(raygrad_ngp_kernel, dim3(grid), dim3(RG_THREADS), 0, st, G, Q);
+  DEN_LAUNCHED();
+  if (points == 1)
+    hipLaunchKernelGGL(raygrad_split_kernel, dim3(grid), dim3(RG_THREADS), 0, st, n, G.per_sample, d_x, d_d);
+  else
+    hipLaunchKernelGGL(raygrad_reduce_kernel, dim3((n_rays + 3) / 4), dim3(256), 0, st, n_rays, 2, 0, ray_idx, n,
+                       G.per_sample, d_x, d_d);
+  DEN_LAUNCHED();
   return DEN_OK;
 }
 

@@ -101,6 +101,44 @@ __global__ void pixel_rays_kernel(int M, int N, const float* __restrict__ k_inv,
     ray_o[3 * r + a] = t_pos[3 * r + a];
   }
 }
+// Reverse mode of pixel_rays_kernel (NeRF.pixel_params_to_ray autograd): with y = R (K^-1 [u v 1]),
+// d = y / |y|:  dL/dy = (g_d - d (d . g_d)) / |y|,  dL/dR = dL/dy (K^-1 [u v 1])^T,  dL/dp = g_o.
+// Overwrites d_t_pos (M,N,3) / d_t_rot (M,N,3,3); either may be null.
+__global__ void pixel_rays_bwd_kernel(int M, int N, const float* __restrict__ k_inv, const float* __restrict__ pixel,
+                                      const float* __restrict__ t_rot, const float* __restrict__ g_o,
+                                      const float* __restrict__ g_d, float* __restrict__ d_t_pos,
+                                      float* __restrict__ d_t_rot) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= (int64_t)M * N) return;
+  const int n = (int)(r % N);
+  const float u = pixel[2 * n], v = pixel[2 * n + 1];
+  float kp[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) kp[a] = (k_inv[3 * a] * u + k_inv[3 * a + 1] * v) + k_inv[3 * a + 2];
+  const float* R = t_rot + 9 * r;
+  float y[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) y[a] = (R[3 * a] * kp[0] + R[3 * a + 1] * kp[1]) + R[3 * a + 2] * kp[2];
+  const float nrm = sqrtf((y[0] * y[0] + y[1] * y[1]) + y[2] * y[2]);
+  float gd[3], dd[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    gd[a] = g_d ? g_d[3 * r + a] : 0.0f;
+    dd[a] = y[a] / nrm;
+  }
+  const float dot = (dd[0] * gd[0] + dd[1] * gd[1]) + dd[2] * gd[2];
+  if (d_t_rot)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float gy = (gd[a] - dd[a] * dot) / nrm;
+#pragma unroll
+      for (int b = 0; b < 3; ++b) d_t_rot[9 * r + 3 * a + b] = gy * kp[b];
+    }
+  if (d_t_pos)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) d_t_pos[3 * r + a] = g_o ? g_o[3 * r + a] : 0.0f;
+}
+
 // ------------------------------------------------------------------ event preparation: backward
 // Reverse mode of event_prep_kernel (and of the loss target), per event in f64, with torch's
 // derivative conventions: lerp(a, b, w) -> (1 - w, w); maximum / minimum -> the larger / smaller
@@ -377,6 +415,90 @@ __global__ void trajectory_kernel(TrajArgs T) {
   m[2] = 2.0f * (xz + yw);
   m[5] = 2.0f * (yz - xw);
   m[8] = ((-x2 - y2) + z2) + w2;
+}
+
+// Reverse mode of trajectory_kernel with respect to the query timestamp (the camera samples are
+// buffers): w = (t - ts[l]) / bw, so dL/dt = dL/dw / bw with
+//   dL/dw = g_pos . (p[r] - p[l])                                  (torch.lerp: d/dweight = end - start)
+//         + g_R : dR/dq . (q0 (x) dr/dw)                           (q = q0 (x) r(w), r = rotvec_to_unitquat(w v0))
+// r(w) = [sin(w |v0| / 2) v0 / |v0|, cos(w |v0| / 2)] so dr/dw = [cos(h) v0 / 2, -|v0| sin(h) / 2],
+// h = w |v0| / 2 (the limit of RoMa's small-angle series as well).  dq/dw is tangent to the unit
+// sphere, so any quaternion -> matrix form with the right values on it gives the same dR/dw.
+// Out-of-span queries (clamped to the end bins by the forward) get the clamped bin's derivative.
+__global__ void trajectory_bwd_kernel(TrajArgs T, const float* g_pos, const float* g_rot, double* d_query) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T.n) return;
+  const double t = T.query[i];
+  int lo = 0, hi = T.C;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((double)T.cam_ts[mid] < t) lo = mid + 1;
+    else hi = mid;
+  }
+  int right = lo;
+  int left = (t == (double)T.cam_ts[0]) ? right : right - 1;
+  if (left < 0 || right >= T.C || left > T.C - 2) {
+    left = left < 0 ? 0 : (left > T.C - 2 ? T.C - 2 : left);
+    right = right >= T.C ? T.C - 1 : (right < left ? left : right);
+  }
+  const double bw = (double)(T.cam_ts[left + 1] - T.cam_ts[left]);
+  const float w = (float)((t - (double)T.cam_ts[left]) / bw);
+  float gw = 0.0f;
+  if (g_pos)
+    for (int a = 0; a < 3; ++a) gw += g_pos[i * 3 + a] * (T.cam_pos[right * 3 + a] - T.cam_pos[left * 3 + a]);
+  if (g_rot) {
+    float q0[4], q1[4];
+    for (int a = 0; a < 4; ++a) {
+      q0[a] = T.cam_q[left * 4 + a];
+      q1[a] = T.cam_q[right * 4 + a];
+    }
+    if (((q0[0] * q1[0] + q0[1] * q1[1]) + q0[2] * q1[2]) + q0[3] * q1[3] < 0.0f)
+      for (int a = 0; a < 4; ++a) q1[a] = -q1[a];
+    const float q0c[4] = {-q0[0], -q0[1], -q0[2], q0[3]};
+    float rel[4];
+    quat_mul(q0c, q1, rel);
+    const float vn = sqrtf((rel[0] * rel[0] + rel[1] * rel[1]) + rel[2] * rel[2]);
+    const float ang = 2.0f * atan2f(vn, rel[3]);
+    float sc;
+    if (fabsf(ang) <= 1e-3f) {
+      const float a2 = ang * ang;
+      sc = (2.0f + a2 / 12.0f) + 7.0f * (a2 * a2) / 2880.0f;
+    } else {
+      sc = ang / sinf(ang / 2.0f);
+    }
+    float v0[3];
+    for (int a = 0; a < 3; ++a) v0[a] = sc * rel[a];
+    const float th = sqrtf((v0[0] * v0[0] + v0[1] * v0[1]) + v0[2] * v0[2]);
+    // the forward rotation r(w) and dr/dw
+    const float n = fabsf(w) * th;
+    float s2;
+    if (n <= 1e-3f) {
+      const float n2 = n * n;
+      s2 = (0.5f - n2 / 48.0f) + (n2 * n2) / 3840.0f;
+    } else {
+      s2 = sinf(n / 2.0f) / n;
+    }
+    const float r[4] = {s2 * w * v0[0], s2 * w * v0[1], s2 * w * v0[2], cosf(n / 2.0f)};
+    const float h = 0.5f * w * th;
+    const float dr[4] = {0.5f * cosf(h) * v0[0], 0.5f * cosf(h) * v0[1], 0.5f * cosf(h) * v0[2],
+                         -0.5f * th * sinf(h)};
+    float q[4], dq[4];
+    quat_mul(q0, r, q);
+    quat_mul(q0, dr, dq);
+    const float x = q[0], y = q[1], z = q[2], ww = q[3];
+    const float* G = g_rot + i * 9;
+    // dR/dq of the forward's matrix (rows of 4: d/dx, d/dy, d/dz, d/dw), contracted with g_R
+    const float gq0 = 2.0f * (G[0] * x + G[3] * y + G[6] * z + G[1] * y - G[4] * x + G[7] * ww + G[2] * z -
+                              G[5] * ww - G[8] * x);
+    const float gq1 = 2.0f * (-G[0] * y + G[3] * x - G[6] * ww + G[1] * x + G[4] * y + G[7] * z + G[2] * ww +
+                              G[5] * z - G[8] * y);
+    const float gq2 = 2.0f * (-G[0] * z + G[3] * ww + G[6] * x - G[1] * ww - G[4] * z + G[7] * y + G[2] * x +
+                              G[5] * y + G[8] * z);
+    const float gq3 = 2.0f * (G[0] * ww + G[3] * z - G[6] * y - G[1] * z + G[4] * ww + G[7] * x + G[2] * y -
+                              G[5] * x + G[8] * ww);
+    gw += ((gq0 * dq[0] + gq1 * dq[1]) + gq2 * dq[2]) + gq3 * dq[3];
+  }
+  d_query[i] = (double)gw / bw;
 }
 #pragma clang fp contract(on)
 

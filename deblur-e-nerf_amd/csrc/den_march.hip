@@ -431,17 +431,29 @@ struct CompArgs {
   float* d_sigma;         // (n)
   float* d_rgb;           // (n, rd)
   float* bkgd_partial;    // (rd, R)
+  int alpha;              // 1: `sigma` holds alphas (render_weight_from_alpha)
 };
 
-// per sample: tau (0 for zero-length samples), t_mid
+// per sample: tau (0 for zero-length samples), t_mid.  Alpha mode (render_weight_from_alpha,
+// vol_rendering.py:96-106's rgb_alpha_fn branch): the input is alpha, tau = -log(1 - alpha), and dlt
+// = 1 so that d/d(input) below is d/dtau * dtau/dalpha with the 1 / (1 - alpha) applied separately.
 __device__ __forceinline__ void comp_sample(const CompArgs& C, int64_t s, bool in, float* tau, float* dlt,
                                             float* tmid) {
 #pragma clang fp contract(off)
   if (!in) { *tau = 0.0f; *dlt = 0.0f; *tmid = 0.0f; return; }
   const float a0 = C.t0[s], a1 = C.t1[s];
+  *tmid = (a0 + a1) / 2.0f;
+  if (C.alpha) {
+    *dlt = 1.0f;
+    *tau = -log1pf(-fminf(C.sigma[s], 1.0f));
+    return;
+  }
   *dlt = a1 - a0;
   *tau = (a1 > a0) ? C.sigma[s] * *dlt : 0.0f;
-  *tmid = (a0 + a1) / 2.0f;
+}
+// 1 - exp(-tau): alpha itself in alpha mode (exact, also at alpha = 1)
+__device__ __forceinline__ float comp_alpha(const CompArgs& C, int64_t s, float tau) {
+  return C.alpha ? fminf(C.sigma[s], 1.0f) : 1.0f - expf(-tau);
 }
 
 // nerfacc render_weight_from_density (w_i = exp(-sum_{j<i} tau_j)(1 - exp(-tau_i))) +
@@ -459,7 +471,7 @@ __global__ void composite_fwd_kernel(CompArgs C) {
     float tau, dlt, tmid;
     comp_sample(C, s, in, &tau, &dlt, &tmid);
     const float excl = carry + wave_excl_scan(tau);
-    const float w = in ? expf(-excl) * (1.0f - expf(-tau)) : 0.0f;
+    const float w = in ? expf(-excl) * comp_alpha(C, s, tau) : 0.0f;
     if (in)
       for (int ch = 0; ch < C.rd; ++ch) cs[ch] += w * C.rgb[s * C.rd + ch];
     op += w;
@@ -505,7 +517,7 @@ __global__ void composite_bwd_kernel(CompArgs C) {
     comp_sample(C, s, in, &tau, &dlt, &tmid);
     const float excl = carry + wave_excl_scan(tau);
     if (in) {
-      const float w = expf(-excl) * (1.0f - expf(-tau));
+      const float w = expf(-excl) * comp_alpha(C, s, tau);
       float g = dO_eff + dD * tmid;
       for (int ch = 0; ch < C.rd; ++ch) g += dC[ch] * C.rgb[s * C.rd + ch];
       op += w;
@@ -527,7 +539,7 @@ __global__ void composite_bwd_kernel(CompArgs C) {
     const float excl = carry + ex;
     float w = 0.0f, g = 0.0f;
     if (in) {
-      w = expf(-excl) * (1.0f - expf(-tau));
+      w = expf(-excl) * comp_alpha(C, s, tau);
       g = dO_eff + dD * tmid;
       for (int ch = 0; ch < C.rd; ++ch) g += dC[ch] * C.rgb[s * C.rd + ch];
     }
@@ -535,8 +547,14 @@ __global__ void composite_bwd_kernel(CompArgs C) {
     if (in) {
       const float suffix = total - (prefix + wgi);
       const float Tnext = expf(-(excl + tau));
-      const float dtau = Tnext * g - suffix;
-      C.d_sigma[s] = (dlt > 0.0f) ? dtau * dlt : 0.0f;
+      if (C.alpha) {
+        // dL/dalpha_i = T_i g_i - suffix_i / (1 - alpha_i); at alpha = 1 every later weight is 0
+        const float a = fminf(C.sigma[s], 1.0f);
+        C.d_sigma[s] = expf(-excl) * g - (a < 1.0f ? __fdiv_rn(suffix, 1.0f - a) : 0.0f);
+      } else {
+        const float dtau = Tnext * g - suffix;
+        C.d_sigma[s] = (dlt > 0.0f) ? dtau * dlt : 0.0f;
+      }
       for (int ch = 0; ch < C.rd; ++ch) C.d_rgb[s * C.rd + ch] = w * dC[ch];
     }
     prefix += __shfl(wgi, 63, 64);

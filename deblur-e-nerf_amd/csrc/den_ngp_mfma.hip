@@ -627,7 +627,9 @@ __global__ __launch_bounds__(NSC_THREADS) void ngp_scatter_kernel(NgpArgs A) {
       v[2 * c] = C.w[c] * g0;
       v[2 * c + 1] = C.w[c] * g1;
     }
-    const bool emit = ngp_fold(cell, v, ok) && (g0 != 0.0f || g1 != 0.0f);
+    // the zero test goes into the fold: a lane with nothing to add neither absorbs its same-cell
+    // partners (which would drop their values) nor is absorbed
+    const bool emit = ngp_fold(cell, v, ok && (g0 != 0.0f || g1 != 0.0f));
     if (emit) {
 #pragma unroll
       for (int c = 0; c < 8; ++c) {

@@ -709,4 +709,31 @@ __global__ void pixbw_sample_ts_kernel(int S, int N, const double* gen, const do
   ts[e] = out_ts[n] - (-log1p(-p) / (double)rate);
 }
 
+// Reverse mode of the sample timestamps with respect to output_ts: ts_k = out_ts - lifetime_k with the
+// lifetimes out of autograd (sample_intensity runs under no_grad; only output_ts - lifetime is
+// recorded, pixel_bandwidth.py:359-363), so d out_ts = sum_k d ts_k.  Overwrites d_out_ts (N).
+__global__ void pixbw_sample_ts_bwd_kernel(int S, int N, const double* g_ts, double* d_out_ts) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double acc = 0.0;
+  for (int k = 0; k < S; ++k) acc += g_ts[(int64_t)k * N + n];
+  d_out_ts[n] = acc;
+}
+
+// Reverse mode of the offset decay of a non-reset call (:435-446) with respect to its timestamps:
+// out = y - delta exp(-w_diff 1e-9 f32(out_ts - reset_ts)), so d out / d out_ts = delta e w_diff 1e-9 =
+// -d out / d reset_ts.  d_out_ts / d_reset_ts (N) overwritten; either may be null.
+__global__ void pixbw_decay_ts_bwd_kernel(int N, const double* out_ts, const double* reset_ts, const float* prm,
+                                          const float* delta_in, const float* d_out, double* d_out_ts,
+                                          double* d_reset_ts) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const double tdf = (double)prm[6];
+  const double rdt = (double)(float)(out_ts[n] - reset_ts[n]) * PIXBW_NS;
+  const double e = exp(-rdt / tdf);
+  const double g = (double)d_out[n] * (double)delta_in[n] * e * PIXBW_NS / tdf;
+  if (d_out_ts) d_out_ts[n] = g;
+  if (d_reset_ts) d_reset_ts[n] = -g;
+}
+
 }  // namespace den

@@ -7,5 +7,6 @@ render / event-measurement path runs in libden.so (HIP kernels for gfx950);
 see DESIGN.md.
 """
 from . import _native  # noqa: F401
+from . import data, loss_metric, models, utils  # noqa: F401  (deblur_e_nerf/__init__.py:1)
 
 __version__ = "0.1.0"

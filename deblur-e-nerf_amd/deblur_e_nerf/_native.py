@@ -106,6 +106,8 @@ _SIGS = {
     "den_composite_fwd": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 10),
     "den_composite_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32] * 2),
     "den_composite_bwd": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 14),
+    "den_composite_alpha_fwd": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 10),
+    "den_composite_alpha_bwd": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 14),
     "den_event_prep_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
     "den_event_prep_bwd": (ctypes.c_int, [ctypes.c_int32] * 3 + [ctypes.c_void_p] * 17),
     "den_event_target_bwd": (ctypes.c_int, [ctypes.c_int32] + [ctypes.c_void_p] * 12),
@@ -122,6 +124,16 @@ _SIGS = {
     "den_ngp_bwd": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64] + [ctypes.c_void_p] * 6),
     "den_hashgrid_fwd": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64] + [ctypes.c_void_p] * 4),
     "den_hashgrid_bwd": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64] + [ctypes.c_void_p] * 4),
+    "den_render_ray_grad_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(RenderDesc)]),
+    "den_render_ray_grad": (ctypes.c_int, [ctypes.POINTER(RenderDesc), ctypes.POINTER(RenderIO), ctypes.c_void_p,
+                                           ctypes.c_int32, ctypes.c_int64] + [ctypes.c_void_p] * 4),
+    "den_ngp_ray_grad_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "den_ngp_ray_grad": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
+                         + [ctypes.c_void_p] * 11),
+    "den_pixel_rays_bwd": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 8),
+    "den_trajectory_bwd": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 8),
+    "den_pixbw_sample_ts_bwd": (ctypes.c_int, [ctypes.c_int32] * 2 + [ctypes.c_void_p] * 3),
+    "den_pixbw_decay_ts_bwd": (ctypes.c_int, [ctypes.c_int32] + [ctypes.c_void_p] * 8),
     "den_occ_workspace_bytes": (ctypes.c_size_t, []),
     "den_occ_points": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int32]
                        + [ctypes.c_void_p] * 4),
@@ -259,14 +271,18 @@ class RenderFunction(torch.autograd.Function):
     given points instead: rays_o = positions (n,3), rays_d = directions (n,3),
     outputs rgb (n,rd), sigma (n), unused (n).  ``points=2`` evaluates it at the
     packed samples ``samples = (ray_indices (n) i32, t_starts (n), t_ends (n))`` of
-    the rays rays_o / rays_d (n a multiple of the tile): outputs rgb (n,rd), sigma (n)."""
+    the rays rays_o / rays_d (n a multiple of the tile; the first ``n_valid`` are the
+    real, ray-sorted samples): outputs rgb (n,rd), sigma (n).  When rays_o / rays_d
+    require grad the backward also returns their gradients (den_render_ray_grad: the
+    positions o + d t and view directions d of the samples, t detached as nerfacc's)."""
 
     @staticmethod
-    def forward(ctx, rays_o, rays_d, jitter, bkgd, flat, cfg, packed, n_samples, points, samples=None):
+    def forward(ctx, rays_o, rays_d, jitter, bkgd, flat, cfg, packed, n_samples, points, samples=None, n_valid=None):
         _require_device(rays_o, rays_d, jitter, bkgd, flat)
         rd = cfg["rd"]
         train = torch.is_grad_enabled() and (flat.requires_grad or (bkgd is not None and bkgd.requires_grad))
-        train = train or ctx.needs_input_grad[4] or (bkgd is not None and ctx.needs_input_grad[3])
+        train = (train or ctx.needs_input_grad[4] or (bkgd is not None and ctx.needs_input_grad[3])
+                 or ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
         R = samples[0].numel() if points == 2 else rays_o.shape[0]
         desc = _desc(cfg, R if not points else R // n_samples, n_samples, train, bkgd is not None, points)
         ws = torch.empty(render_workspace_bytes(desc), dtype=torch.uint8, device=rays_o.device)
@@ -278,14 +294,15 @@ class RenderFunction(torch.autograd.Function):
                       _ptr(packed.bias), _ptr(bkgd), _ptr(ws), _ptr(out_rgb), _ptr(out_op), _ptr(out_dp),
                       _ptr(ri), _ptr(t0), _ptr(t1))
         _check(lib().den_render_fwd(ctypes.byref(desc), ctypes.byref(io), _stream(rays_o.device)))
-        ctx.desc, ctx.io_keep = desc, (rays_o, rays_d, jitter, bkgd, ws, packed, ri, t0, t1)
+        ctx.desc, ctx.io_keep = desc, (rays_o, rays_d, jitter, bkgd, ws, packed, ri, t0, t1, flat)
         ctx.flat_shape = flat.shape
         ctx.has_bkgd = bkgd is not None
+        ctx.n_valid = R if n_valid is None else int(n_valid)
         return out_rgb, out_op, out_dp
 
     @staticmethod
     def backward(ctx, g_rgb, g_op, g_dp):
-        rays_o, rays_d, jitter, bkgd, ws, packed, ri, t0, t1 = ctx.io_keep
+        rays_o, rays_d, jitter, bkgd, ws, packed, ri, t0, t1, flat = ctx.io_keep
         dev = rays_o.device
         g_rgb = torch.zeros_like(g_rgb) if g_rgb is None else g_rgb.contiguous()
         g_op = None if g_op is None else g_op.contiguous()
@@ -296,10 +313,18 @@ class RenderFunction(torch.autograd.Function):
                       _ptr(packed.bias), _ptr(bkgd), _ptr(ws), None, None, None, _ptr(ri), _ptr(t0), _ptr(t1))
         gr = RenderGrad(_ptr(g_rgb), _ptr(g_op), _ptr(g_dp), _ptr(grad_flat), _ptr(grad_bkgd))
         _check(lib().den_render_bwd(ctypes.byref(ctx.desc), ctypes.byref(io), ctypes.byref(gr), _stream(dev)))
+        d_o = d_d = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            L = lib()
+            d_o, d_d = torch.empty_like(rays_o), torch.empty_like(rays_d)
+            rg = torch.empty(L.den_render_ray_grad_workspace_bytes(ctypes.byref(ctx.desc)), dtype=torch.uint8,
+                             device=dev)
+            _check(L.den_render_ray_grad(ctypes.byref(ctx.desc), ctypes.byref(io), _ptr(flat.detach()),
+                                         rays_o.shape[0], ctx.n_valid, _ptr(rg), _ptr(d_o), _ptr(d_d), _stream(dev)))
         # release the workspace (the activations kept for this backward) as soon as the
         # stream is done with it: the caching allocator orders the reuse on the same stream
         ctx.io_keep = None
-        return None, None, None, grad_bkgd, grad_flat, None, None, None, None, None
+        return d_o, d_d, None, grad_bkgd, grad_flat, None, None, None, None, None, None
 
 
 def render(rays_o, rays_d, jitter, bkgd, flat, cfg, packed, n_samples):
@@ -343,7 +368,7 @@ def field_packed(rays_o, rays_d, ray_indices, t_starts, t_ends, flat, cfg, packe
         t0 = torch.cat([t0, t0.new_zeros(pad)])
         t1 = torch.cat([t1, t1.new_zeros(pad)])
     rgb, sig, _ = RenderFunction.apply(rays_o.float().contiguous(), rays_d.float().contiguous(), None, None, flat,
-                                       cfg, packed, group, 2, (ri.contiguous(), t0.contiguous(), t1.contiguous()))
+                                       cfg, packed, group, 2, (ri.contiguous(), t0.contiguous(), t1.contiguous()), n)
     return rgb[:n], sig[:n]
 
 
@@ -391,7 +416,12 @@ class NgpFieldFunction(torch.autograd.Function):
         n = (ri.numel() if points == 2 else x.shape[0])
         dev = flat.device
         # (grad mode is off inside Function.forward: needs_input_grad says whether a backward follows)
-        train = bool(ctx.needs_input_grad[0]) and not density_only
+        if density_only and (ctx.needs_input_grad[0] or ctx.needs_input_grad[3] or ctx.needs_input_grad[4]):
+            # the density-only pass keeps no state for a backward (the reference's query_density
+            # call sites are all no-grad: nerf.py:170-204, external/utils.py:68-81)
+            raise NotImplementedError("ngp density-only query is not differentiable here: call it under "
+                                      "torch.no_grad() or use the full field")
+        train = bool(ctx.needs_input_grad[0] or ctx.needs_input_grad[3] or ctx.needs_input_grad[4])
         ws = (torch.empty(lib().den_ngp_workspace_bytes(ctypes.byref(desc), n, 1), dtype=torch.uint8, device=dev)
               if train and n > 0 else None)
         rgb = torch.empty(n, desc.radiance_dim, dtype=torch.float32, device=dev)
@@ -399,32 +429,48 @@ class NgpFieldFunction(torch.autograd.Function):
         _check(lib().den_ngp_fwd(ctypes.byref(desc), n, points, _ptr(x), _ptr(d), _ptr(ri), _ptr(t0), _ptr(t1),
                                  _ptr(flat), int(bool(density_only)), int(train), _ptr(ws), _ptr(rgb), _ptr(sig),
                                  _stream(dev)))
-        ctx.keep = (desc, n, flat, ws)
+        ctx.keep = (desc, n, flat, ws, points, x, d, ri, t0, t1)
         return rgb, sig
 
     @staticmethod
     def backward(ctx, g_rgb, g_sig):
-        desc, n, flat, ws = ctx.keep
+        desc, n, flat, ws, points, x, d, ri, t0, t1 = ctx.keep
         grad = torch.empty_like(flat)
         g_rgb = None if g_rgb is None else g_rgb.contiguous()
         g_sig = None if g_sig is None else g_sig.contiguous()
+        d_x = d_d = None
         if ws is None:
             grad.zero_()
         else:
+            st = _stream(flat.device)
             _check(lib().den_ngp_bwd(ctypes.byref(desc), n, _ptr(flat), _ptr(ws), _ptr(g_rgb), _ptr(g_sig),
-                                     _ptr(grad), _stream(flat.device)))
+                                     _ptr(grad), st))
+            if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
+                L = lib()
+                d_x, d_d = torch.empty_like(x), torch.empty_like(d)
+                rg = torch.empty(max(1, L.den_ngp_ray_grad_workspace_bytes(n)), dtype=torch.uint8, device=x.device)
+                _check(L.den_ngp_ray_grad(ctypes.byref(desc), n, points, x.shape[0] if points == 2 else 0, _ptr(x),
+                                          _ptr(d), _ptr(ri), _ptr(t0), _ptr(t1), _ptr(flat), _ptr(ws), _ptr(rg),
+                                          _ptr(d_x), _ptr(d_d), st))
         ctx.keep = None
-        return grad, None, None, None, None, None, None, None, None
+        return grad, None, None, d_x, d_d, None, None, None, None
+
+
+def _no_grad_if(density_only, t):
+    # the density-only pass (the marching pre-pass / occupancy update) is never differentiated
+    return t.detach() if density_only else t
 
 
 def ngp_field(flat, desc, x, d, density_only=False):
     """-> rgb (n, rd), sigma (n) at positions x (n,3) viewed along d (n,3)."""
+    x, d = _no_grad_if(density_only, x), _no_grad_if(density_only, d)
     return NgpFieldFunction.apply(flat, desc, 1, x.float().contiguous(), d.float().contiguous(), None, None, None,
                                   density_only)
 
 
 def ngp_field_packed(flat, desc, rays_o, rays_d, ray_indices, t_starts, t_ends, density_only=False):
     """-> rgb (n, rd), sigma (n) at packed ray-marching samples (external/utils.py:83-96)."""
+    rays_o, rays_d = _no_grad_if(density_only, rays_o), _no_grad_if(density_only, rays_d)
     return NgpFieldFunction.apply(flat, desc, 2, rays_o.float().contiguous(), rays_d.float().contiguous(),
                                   ray_indices.reshape(-1).to(torch.int32).contiguous(),
                                   t_starts.reshape(-1).float().contiguous(), t_ends.reshape(-1).float().contiguous(),
@@ -512,20 +558,39 @@ def event_target(ts_diff, lid, end_ts, start_ts, c):
 PIXBW_NPARAM = 7
 
 
+class SampleTsFunction(torch.autograd.Function):
+    """den_pixbw_sample_ts, differentiable in output_ts (the lifetimes are drawn under no_grad in
+    the reference, pixel_bandwidth.py:298-367: d output_ts = sum over the S samples,
+    den_pixbw_sample_ts_bwd)."""
+
+    @staticmethod
+    def forward(ctx, gen, output_ts, omega_c_min, max_cumprob):
+        _require_device(gen, output_ts)
+        S = gen.shape[0] + 1
+        batch = output_ts.shape
+        N = output_ts.numel()
+        g = gen.reshape(S - 1, N).to(torch.float64).contiguous()
+        o = output_ts.reshape(N).to(torch.float64).contiguous()
+        ts = torch.empty(S, N, dtype=torch.float64, device=gen.device)
+        _check(lib().den_pixbw_sample_ts(S, N, _ptr(g), _ptr(o), float(omega_c_min), float(max_cumprob), _ptr(ts),
+                                         _stream(gen.device)))
+        ctx.meta = (S, N, batch, output_ts.dtype)
+        return ts.reshape(S, *batch)
+
+    @staticmethod
+    def backward(ctx, g_ts):
+        S, N, batch, dt = ctx.meta
+        d = torch.empty(N, dtype=torch.float64, device=g_ts.device)
+        _check(lib().den_pixbw_sample_ts_bwd(S, N, _ptr(g_ts.to(torch.float64).reshape(S, N).contiguous()), _ptr(d),
+                                             _stream(g_ts.device)))
+        return None, d.reshape(batch).to(dt), None, None
+
+
 def pixbw_sample_ts(gen, output_ts, omega_c_min, max_cumprob):
     """den_pixbw_sample_ts: (S-1, ...) f64 interval generators and (...) f64 output
     timestamps (ns) -> (S, ...) f64 sample timestamps (pixel_bandwidth.py:311-360,
-    before the clamp to min_ts)."""
-    _require_device(gen, output_ts)
-    S = gen.shape[0] + 1
-    batch = output_ts.shape
-    N = output_ts.numel()
-    g = gen.reshape(S - 1, N).to(torch.float64).contiguous()
-    o = output_ts.reshape(N).to(torch.float64).contiguous()
-    ts = torch.empty(S, N, dtype=torch.float64, device=gen.device)
-    _check(lib().den_pixbw_sample_ts(S, N, _ptr(g), _ptr(o), float(omega_c_min), float(max_cumprob), _ptr(ts),
-                                     _stream(gen.device)))
-    return ts.reshape(S, *batch)
+    before the clamp to min_ts); differentiable in output_ts."""
+    return SampleTsFunction.apply(gen, output_ts, omega_c_min, max_cumprob)
 
 
 class PixelBandwidthFunction(torch.autograd.Function):
@@ -558,6 +623,8 @@ class PixelBandwidthFunction(torch.autograd.Function):
         ctx.reset = bool(reset)
         ctx.in_dtype, ctx.in_shape, ctx.p_dtype = intensity.dtype, intensity.shape, params.dtype
         ctx.din_shape = None if reset else delta_in.shape
+        ctx.ts_meta = (output_ts.shape, output_ts.dtype, None if reset else reset_ts.shape,
+                       None if reset else reset_ts.dtype)
         if not reset:
             ctx.mark_non_differentiable(delta_out)
         batch = intensity.shape[1:]
@@ -581,8 +648,19 @@ class PixelBandwidthFunction(torch.autograd.Function):
                                _ptr(g), _ptr(dd), _ptr(ws), _ptr(d_it), _ptr(d_din), _ptr(part), _stream(dev)))
         d_prm = torch.empty(PIXBW_NPARAM, dtype=torch.float32, device=dev)
         sum_partials(part, PIXBW_NPARAM, nb, d_prm)
+        # the offset decay's dependence on the output / reset timestamps (non-reset calls; the
+        # reset call's output_ts is the later calls' reset_ts)
+        d_ots = d_rts = None
+        if not ctx.reset and (ctx.needs_input_grad[4] or ctx.needs_input_grad[5]):
+            d_ots = torch.empty(N, dtype=torch.float64, device=dev) if ctx.needs_input_grad[4] else None
+            d_rts = torch.empty(N, dtype=torch.float64, device=dev) if ctx.needs_input_grad[5] else None
+            _check(L.den_pixbw_decay_ts_bwd(N, _ptr(ots), _ptr(rts), _ptr(prm), _ptr(din), _ptr(g), _ptr(d_ots),
+                                            _ptr(d_rts), _stream(dev)))
+            ots_shape, ots_dt, rts_shape, rts_dt = ctx.ts_meta
+            d_ots = None if d_ots is None else d_ots.reshape(ots_shape).to(ots_dt)
+            d_rts = None if d_rts is None else d_rts.reshape(rts_shape).to(rts_dt)
         return (d_it.reshape(ctx.in_shape).to(ctx.in_dtype), d_prm.to(ctx.p_dtype),
-                None if d_din is None else d_din.reshape(ctx.din_shape), None, None, None, None)
+                None if d_din is None else d_din.reshape(ctx.din_shape), None, d_ots, d_rts, None)
 
 
 # ----------------------------------------------------------------------------- event preparation
@@ -617,21 +695,60 @@ def event_prep(num_pos, num_neg, end_ts, start_ts, normalized, ct, refractory, n
     return out
 
 
-def pixel_rays(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation, out=None):
-    """den_pixel_rays (NeRF.pixel_params_to_ray, nerf.py:206-228): K^-1 (3,3),
-    pixels (N,2), poses ([M,] N, 3) / ([M,] N, 3, 3) -> origins, unit directions
-    ([M,] N, 3) f32.  Pixels broadcast over the leading render-group dim M."""
-    _require_device(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
-    ts = (intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
-    if any(t.dtype != torch.float32 for t in ts):
-        raise DenError("pixel_rays: expected f32 tensors")
-    intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation = (t.contiguous() for t in ts)
+def _pixel_rays_shapes(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation):
     N = pixel_position.shape[0]
     lead = T_wc_position.shape[:-1]
     M = T_wc_position.numel() // (3 * N) if N else 0
     if (intrinsics_inverse.shape != (3, 3) or pixel_position.shape != (N, 2) or lead[-1:] != (N,)
             or T_wc_orientation.shape != (*lead, 3, 3) or M * N * 3 != T_wc_position.numel()):
         raise DenError("pixel_rays: bad shapes")
+    return M, N
+
+
+class PixelRaysFunction(torch.autograd.Function):
+    """den_pixel_rays, differentiable in the poses (den_pixel_rays_bwd): the reference's autograd of
+    NeRF.pixel_params_to_ray (nerf.py:206-228), the link from the rays back to the trajectory."""
+
+    @staticmethod
+    def forward(ctx, intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation):
+        M, N = _pixel_rays_shapes(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
+        o, d = torch.empty_like(T_wc_position), torch.empty_like(T_wc_position)
+        _check(lib().den_pixel_rays(M, N, _ptr(intrinsics_inverse), _ptr(pixel_position), _ptr(T_wc_position),
+                                    _ptr(T_wc_orientation), _ptr(o), _ptr(d), _stream(pixel_position.device)))
+        ctx.save_for_backward(intrinsics_inverse, pixel_position, T_wc_orientation)
+        ctx.MN = (M, N)
+        return o, d
+
+    @staticmethod
+    def backward(ctx, g_o, g_d):
+        k_inv, pix, rot = ctx.saved_tensors
+        M, N = ctx.MN
+        d_pos = torch.empty(rot.shape[:-1], dtype=torch.float32, device=rot.device) if ctx.needs_input_grad[2] else None
+        d_rot = torch.empty_like(rot) if ctx.needs_input_grad[3] else None
+        if d_pos is None and d_rot is None:
+            return None, None, None, None
+        g_o = None if g_o is None else g_o.to(torch.float32).contiguous()
+        g_d = None if g_d is None else g_d.to(torch.float32).contiguous()
+        _check(lib().den_pixel_rays_bwd(M, N, _ptr(k_inv), _ptr(pix), _ptr(rot), _ptr(g_o), _ptr(g_d), _ptr(d_pos),
+                                        _ptr(d_rot), _stream(rot.device)))
+        return None, None, d_pos, d_rot
+
+
+def pixel_rays(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation, out=None):
+    """den_pixel_rays (NeRF.pixel_params_to_ray, nerf.py:206-228): K^-1 (3,3),
+    pixels (N,2), poses ([M,] N, 3) / ([M,] N, 3, 3) -> origins, unit directions
+    ([M,] N, 3) f32.  Pixels broadcast over the leading render-group dim M.  Differentiable in
+    the poses when they require grad (``out`` must then be None)."""
+    _require_device(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
+    ts = (intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
+    if any(t.dtype != torch.float32 for t in ts):
+        raise DenError("pixel_rays: expected f32 tensors")
+    intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation = (t.contiguous() for t in ts)
+    if torch.is_grad_enabled() and (T_wc_position.requires_grad or T_wc_orientation.requires_grad):
+        if out is not None:
+            raise DenError("pixel_rays: `out` buffers are for the no-grad path")
+        return PixelRaysFunction.apply(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
+    M, N = _pixel_rays_shapes(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation)
     if out is None:
         out = (torch.empty_like(T_wc_position), torch.empty_like(T_wc_position))
     _check(lib().den_pixel_rays(M, N, _ptr(intrinsics_inverse), _ptr(pixel_position), _ptr(T_wc_position),
@@ -640,22 +757,48 @@ def pixel_rays(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientati
     return out
 
 
+class TrajectoryFunction(torch.autograd.Function):
+    """den_trajectory, differentiable in the query timestamps (den_trajectory_bwd): the autograd of
+    LinearTrajectory.forward (trajectories.py:30-90, tensor_ops.py:118-184) through its interpolation
+    weight -- the refractory period's path to the poses."""
+
+    @staticmethod
+    def forward(ctx, cam_ts, cam_pos, cam_quat, query_ts, status):
+        shape = query_ts.shape
+        q = query_ts.reshape(-1).to(torch.float64).contiguous()
+        n = q.numel()
+        C = cam_ts.numel()
+        ct = cam_ts.to(torch.int64).contiguous()
+        cp = cam_pos.to(torch.float32).contiguous()
+        cq = cam_quat.to(torch.float32).contiguous()
+        pos = torch.empty(n, 3, dtype=torch.float32, device=q.device)
+        rot = torch.empty(n, 3, 3, dtype=torch.float32, device=q.device)
+        _check(lib().den_trajectory(n, C, _ptr(ct), _ptr(cp), _ptr(cq), _ptr(q), _ptr(pos), _ptr(rot), _ptr(status),
+                                    _stream(q.device)))
+        ctx.save_for_backward(ct, cp, cq, q)
+        ctx.meta = (shape, query_ts.dtype)
+        return pos.reshape(*shape, 3), rot.reshape(*shape, 3, 3)
+
+    @staticmethod
+    def backward(ctx, g_pos, g_rot):
+        ct, cp, cq, q = ctx.saved_tensors
+        shape, dt = ctx.meta
+        n = q.numel()
+        d = torch.empty(n, dtype=torch.float64, device=q.device)
+        gp = None if g_pos is None else g_pos.reshape(n, 3).to(torch.float32).contiguous()
+        gr = None if g_rot is None else g_rot.reshape(n, 9).to(torch.float32).contiguous()
+        _check(lib().den_trajectory_bwd(n, ct.numel(), _ptr(ct), _ptr(cp), _ptr(cq), _ptr(q), _ptr(gp), _ptr(gr),
+                                        _ptr(d), _stream(q.device)))
+        return None, None, None, d.reshape(shape).to(dt), None
+
+
 def trajectory(cam_ts, cam_pos, cam_quat, query_ts, status=None):
     """den_trajectory (LinearTrajectory.forward): pose stamps (C) i64, positions (C,3) f32, XYZW
     quaternions (C,4) f32, query timestamps (...) f64 -> positions (..., 3), rotations (..., 3, 3).
-    ``status`` (device i32, optional) gets bit 0 for queries outside the pose span."""
+    ``status`` (device i32, optional) gets bit 0 for queries outside the pose span.
+    Differentiable in query_ts."""
     _require_device(cam_ts, cam_pos, cam_quat, query_ts, status)
-    shape = query_ts.shape
-    q = query_ts.reshape(-1).to(torch.float64).contiguous()
-    n = q.numel()
-    C = cam_ts.numel()
-    pos = torch.empty(n, 3, dtype=torch.float32, device=q.device)
-    rot = torch.empty(n, 3, 3, dtype=torch.float32, device=q.device)
-    _check(lib().den_trajectory(n, C, _ptr(cam_ts.to(torch.int64).contiguous()),
-                                _ptr(cam_pos.to(torch.float32).contiguous()),
-                                _ptr(cam_quat.to(torch.float32).contiguous()), _ptr(q), _ptr(pos), _ptr(rot),
-                                _ptr(status), _stream(q.device)))
-    return pos.reshape(*shape, 3), rot.reshape(*shape, 3, 3)
+    return TrajectoryFunction.apply(cam_ts, cam_pos, cam_quat, query_ts, status)
 
 
 class EventTargetFunction(torch.autograd.Function):
@@ -708,6 +851,9 @@ class EventPrepFunction(torch.autograd.Function):
                          None if norm_c is None else norm_c.detach().float().reshape(1).contiguous(),
                          has_diff=has_diff, has_tv=has_tv)
         tgt = out["target"] if out["target"] is not None else torch.zeros_like(out["lid"])
+        if not ctx.needs_input_grad[6]:
+            # tau_r frozen: the timestamps are constants (no pose chain behind the renders)
+            ctx.mark_non_differentiable(out["start_ts"], out["render_ts"], out["ts_diff"], out["ts_subdiff"])
         ctx.save_for_backward(num_pos, num_neg, end_ts, start_ts, normalized, ct.detach().float().contiguous(),
                               refractory.detach().double().reshape(1).contiguous(),
                               None if norm_c is None else norm_c.detach().float().reshape(1).contiguous())

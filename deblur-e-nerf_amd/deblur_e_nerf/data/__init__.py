@@ -1,1 +1,1 @@
-from . import datasets  # noqa: F401
+from . import datamodule, datasets, samplers  # noqa: F401

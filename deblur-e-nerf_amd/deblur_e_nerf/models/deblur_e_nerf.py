@@ -41,6 +41,7 @@ import torch.distributed as dist
 
 from .. import _native
 from ..data import datasets
+from ..external import marching
 from ..loss_metric import loss as loss_lib
 from ..loss_metric import metric as metric_lib
 from ..optim import Adam
@@ -416,11 +417,14 @@ class DeblurENeRF(_Base):
                                                          "interval": self.hparams.lr_scheduler.interval}}
 
     def fit_step(self, batch, batch_index, optimizer):
-        """One optimisation step without a Trainer: training_step, backward, the DDP gradient
+        """One optimisation step without a Trainer: the occupancy grid from rank 0 when it changed
+        (DDP's buffer broadcast), training_step, backward, the DDP gradient
         all-reduce (mean over ranks, one flat buffer), optimizer step on the last micro-batch of
         an accumulation group (PL's accumulate_grad_batches semantics: gradients summed over the
         group, each micro-batch loss scaled by 1 / accumulate_grad_batches)."""
         acc = self.trainer.accumulate_grad_batches
+        # DDP broadcasts the buffers from rank 0 before each forward (broadcast_buffers=True)
+        marching.sync_grid(getattr(self.nerf, "occupancy_grid", None))
         loss = self.training_step(batch, batch_index)
         (loss / acc).backward()
         if (batch_index + 1) % acc == 0:

@@ -72,6 +72,9 @@ class NeRF(torch.nn.Module):
         if sampler == "fixed" and contraction_id(contraction_type) != 0:
             raise NotImplementedError("the fixed-count sampler marches the AABB: use contraction_type AABB")
         self.register_buffer("aabb", torch.tensor(aabb), persistent=False)
+        # host copies of the constants the marcher takes by value (no device -> host copy per render)
+        self._aabb_host = [float(v) for v in aabb]
+        self._step_host = float(render_step_size)
         self.contraction_type = contraction_type
         self.occ_grid_config = occ_grid_config
         self.near_plane = near_plane
@@ -156,8 +159,8 @@ class NeRF(torch.nn.Module):
     @staticmethod
     def pixel_params_to_ray(intrinsics_inverse, pixel_position, T_wc_position, T_wc_orientation):
         """nerf.py:206-228 on the device (den_pixel_rays): (3,3), (N,2), ([M,] N, 3),
-        ([M,] N, 3, 3) -> ray origins, unit directions ([M,] N, 3).  Forward only:
-        pose refinement (gradients into the trajectory) is out of scope."""
+        ([M,] N, 3, 3) -> ray origins, unit directions ([M,] N, 3); differentiable in the poses
+        (den_pixel_rays_bwd) when they require grad."""
         return _native.pixel_rays(intrinsics_inverse.float().contiguous(), pixel_position.float().contiguous(),
                                   T_wc_position.float().contiguous(), T_wc_orientation.float().contiguous())
 
@@ -188,10 +191,10 @@ class NeRF(torch.nn.Module):
             radiance, opacity, depth, num_samples_across_rays = self._forward_fixed(ray_origin, ray_direction)
         else:
             rays = utils.Rays(origins=ray_origin, viewdirs=ray_direction)
-            ray_marching_aabb = self.aabb if contraction_id(self.contraction_type) == 0 else None
+            ray_marching_aabb = self._aabb_host if contraction_id(self.contraction_type) == 0 else None
             radiance, opacity, depth, num_samples_across_rays = utils.render_image(
                 self.radiance_field, self.occupancy_grid, rays, ray_marching_aabb, self.near_plane, self.far_plane,
-                self.render_step_size, self.render_bkgd, self.cone_angle, self.early_stop_eps, self.alpha_thre,
+                self._step_host, self.render_bkgd, self.cone_angle, self.early_stop_eps, self.alpha_thre,
                 self.test_chunk_size)
         # nerf.py:279-286
         radiance = radiance.squeeze(dim=-1)

@@ -105,11 +105,12 @@ class PixelBandwidth(torch.nn.Module):
 
     @torch.no_grad()
     def sample_intensity(self, normalized_interval_gen, output_ts, intensity_sampling_fn):
-        """pixel_bandwidth.py:298-367: sample timestamps (den_pixbw_sample_ts), then the
+        """pixel_bandwidth.py:298-367: sample timestamps (den_pixbw_sample_ts; like the reference's
+        ``output_ts - sample_lifetime`` they are differentiable in output_ts only), then the
         intensity at the timestamps clamped to min_ts (with gradients enabled)."""
-        sample_ts = _native.pixbw_sample_ts(normalized_interval_gen, output_ts, self.omega_c_dominant_min,
-                                            float(self.target_cumprob_max_sample_lifetime))
         with torch.enable_grad():
+            sample_ts = _native.pixbw_sample_ts(normalized_interval_gen, output_ts, self.omega_c_dominant_min,
+                                                float(self.target_cumprob_max_sample_lifetime))
             sampling_output = intensity_sampling_fn(sample_ts.clamp(min=self.min_ts))
         return sampling_output[0], sample_ts, sampling_output[1:]
 

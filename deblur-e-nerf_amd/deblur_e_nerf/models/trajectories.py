@@ -7,7 +7,9 @@ Same constructor (a ``datasets.CameraPose``-like object holding ``camera_poses.T
 buffers (``T_wc_position``, ``T_wc_orientation_quat``, ``T_wc_timestamp``, ``bin_width``) and
 the same ``forward(input_timestamp) -> (position (..., 3), orientation (..., 3, 3))``.  The
 arithmetic (searchsorted, lerp, slerp with RoMa's formulas, quaternion -> matrix) is one HIP
-kernel, den_trajectory.  Forward only: pose refinement is not part of the path.
+kernel, den_trajectory; its reverse mode with respect to the query timestamps (den_trajectory_bwd)
+carries the refractory period's gradient from the poses back to the render timestamps, as the
+reference's autograd does through the interpolation weight.
 """
 import torch
 

@@ -1,1 +1,1 @@
-from . import modules  # noqa: F401
+from . import datasets, easydict, modules  # noqa: F401

@@ -34,6 +34,9 @@
  *                       deblur_e_nerf/models/deblur_e_nerf.py:418-455 training_step
  *   den_pixel_rays   <- deblur_e_nerf/models/nerf.py:206-228 NeRF.pixel_params_to_ray
  *   den_trajectory   <- deblur_e_nerf/models/trajectories.py:30-90 LinearTrajectory.forward
+ *   den_*_ray_grad / den_pixel_rays_bwd / den_trajectory_bwd / den_pixbw_*_ts_bwd
+ *                    <- torch autograd from the renders back to the render timestamps (the
+ *                       refractory-period gradient through the camera pose, deblur_e_nerf.py:419-455)
  *   den_event_loss_* <- deblur_e_nerf/loss_metric/loss.py:34-96 Loss.compute
  *   den_event_target
  *   den_image_error  <- deblur_e_nerf/loss_metric/metric.py:28-92 (L1, PSNR)
@@ -60,7 +63,7 @@
 extern "C" {
 #endif
 
-#define DEN_VERSION 2
+#define DEN_VERSION 3
 
 enum den_status {
   DEN_OK = 0,
@@ -189,6 +192,31 @@ int den_render_bwd(const den_render_desc* desc, const den_render_io* io,
 int den_render_bwd_part(const den_render_desc* desc, const den_render_io* io,
                         const den_render_grad* grad, int32_t part, void* stream);
 
+/* Gradient of the render with respect to its rays (the rays' part of the reference's autograd:
+ * positions o + d (t0 + t1) / 2 and view direction d, external/utils.py:83-96, with the marching
+ * intervals detached as nerfacc returns them).  After den_render_bwd on the same desc / io
+ * (train = 1): reads the layer gradients it left in the workspace and the flat parameters
+ * (reference order, den_param_offset).  points 0: d_rays_o / d_rays_d (n_rays, 3) of the fixed-count
+ * rays; points 2: (n_rays_out, 3) of the rays the packed samples index, whose first n_valid samples
+ * have sorted ray_indices (the rest is padding without gradient); points 1: (n, 3) per point /
+ * direction.  Overwritten.  rg_workspace: den_render_ray_grad_workspace_bytes(desc) bytes.
+ * Replaces: the autograd of origins[ray_indices] + viewdirs * t and of the encoders / MLP inputs. */
+size_t den_render_ray_grad_workspace_bytes(const den_render_desc* desc);
+int den_render_ray_grad(const den_render_desc* desc, const den_render_io* io, const float* params,
+                        int32_t n_rays_out, int64_t n_valid, void* rg_workspace, float* d_rays_o, float* d_rays_d,
+                        void* stream);
+/* Reverse mode of den_pixel_rays with respect to the poses (nerf.py:206-228 autograd):
+ * g_ray_o / g_ray_d (M,N,3) (either may be NULL = 0) -> d_t_pos (M,N,3), d_t_rot (M,N,3,3)
+ * (either may be NULL; overwritten). */
+int den_pixel_rays_bwd(int32_t M, int32_t N, const float* k_inv, const float* pixel, const float* t_rot,
+                       const float* g_ray_o, const float* g_ray_d, float* d_t_pos, float* d_t_rot, void* stream);
+/* Reverse mode of den_trajectory with respect to the query timestamps (trajectories.py:30-90 +
+ * tensor_ops.py:118-184 autograd; the pose samples are buffers): g_position (n,3), g_rotation
+ * (n,3,3) (either may be NULL) -> d_query_ts (n) f64, overwritten. */
+int den_trajectory_bwd(int64_t n, int32_t C, const int64_t* cam_ts, const float* cam_pos, const float* cam_quat,
+                       const double* query_ts, const float* g_position, const float* g_rotation, double* d_query_ts,
+                       void* stream);
+
 /* ---------------------------------------------------------------- pixel bandwidth
  * Per-event pixel-bandwidth model (pixel_bandwidth.py).  Parameters are the
  * post-softplus values (the module's parametrised attributes) in this order:
@@ -200,6 +228,10 @@ int den_render_bwd_part(const den_render_desc* desc, const den_render_io* io,
  * (pixel_bandwidth.py:311-360; un-clamped). */
 int den_pixbw_sample_ts(int32_t S, int32_t N, const double* gen, const double* output_ts,
                         double omega_c_min, double max_cumprob, double* sample_ts, void* stream);
+
+/* Reverse mode of den_pixbw_sample_ts with respect to output_ts (the lifetimes are out of autograd,
+ * pixel_bandwidth.py:298-367): d_output_ts (N) f64 = sum_k g_sample_ts (k, n), overwritten. */
+int den_pixbw_sample_ts_bwd(int32_t S, int32_t N, const double* g_sample_ts, double* d_output_ts, void* stream);
 
 /* Forward.  intensity (S,N) f32, sample_ts (S,N) f64.  reset != 0: writes
  * delta_out (N) and returns out = sf log-intensity; otherwise reads delta_in
@@ -223,6 +255,13 @@ int den_pixbw_bwd(int32_t S, int32_t N, int32_t reset, const float* intensity,
                   const float* delta_in, const double* reset_ts, const float* d_out,
                   const float* d_delta_out, void* workspace, float* d_intensity, float* d_delta_in,
                   float* d_params_partial, void* stream);
+
+/* Timestamp gradients of a non-reset call's offset decay (pixel_bandwidth.py:435-446):
+ * out = y - delta_in exp(-1e-9 f32(output_ts - reset_ts) / tau_diff) -> d_output_ts = -d_reset_ts =
+ * d_out delta_in e 1e-9 / tau_diff (N) f64, either may be NULL. */
+int den_pixbw_decay_ts_bwd(int32_t N, const double* output_ts, const double* reset_ts, const float* params,
+                           const float* delta_in, const float* d_out, double* d_output_ts, double* d_reset_ts,
+                           void* stream);
 
 /* ---------------------------------------------------------------- event loss
  * One term of Loss.compute (loss.py:62-96) over N events:
@@ -360,6 +399,15 @@ int den_composite_bwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const 
                       const float* sigmas, const float* rgbs, const float* bkgd, const float* d_colors,
                       const float* d_opacities, const float* d_depths, float* d_sigmas, float* d_rgbs, float* d_bkgd,
                       void* workspace, void* stream);
+/* The same from alphas (nerfacc render_weight_from_alpha: w_i = alpha_i prod_{j<i} (1 - alpha_j); the
+ * rgb_alpha_fn branch of vol_rendering.py:16-27,96-106): `alphas` in place of the sigmas, d_alphas out. */
+int den_composite_alpha_fwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts,
+                            const float* t_ends, const float* alphas, const float* rgbs, const float* bkgd,
+                            float* colors, float* opacities, float* depths, void* stream);
+int den_composite_alpha_bwd(int32_t n_rays, int32_t rd, const int64_t* offsets, const float* t_starts,
+                            const float* t_ends, const float* alphas, const float* rgbs, const float* bkgd,
+                            const float* d_colors, const float* d_opacities, const float* d_depths, float* d_alphas,
+                            float* d_rgbs, float* d_bkgd, void* workspace, void* stream);
 /* OccupancyGrid._update, part 1: world positions of the sampled cells (cell index + jitter in
  * [0,1)^3, / res, inverse contraction); mask = 0 for cells outside the unit sphere (sphere
  * contraction); marks the sampled cells in `sampled` (cells bytes, zero on entry). */
@@ -435,6 +483,14 @@ int den_ngp_fwd(const den_ngp_desc* desc, int64_t n, int32_t points, const float
  * cleared on the stream, then scattered with f32 atomics as tcnn does). */
 int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* workspace, const float* d_rgb,
                 const float* d_sigma, float* grad_params, void* stream);
+/* Gradient of the same field with respect to its inputs, after den_ngp_bwd on the same workspace:
+ * tcnn's input gradient of the Linear grid encoding + the SH encoder and the contraction.  points 1:
+ * d_x, d_d (n,3) per point; points 2: (n_rays, 3) per ray (sorted ray_idx), position o + d (t0+t1)/2
+ * and view direction d as in den_ngp_fwd.  rg_workspace: den_ngp_ray_grad_workspace_bytes(n). */
+size_t den_ngp_ray_grad_workspace_bytes(int64_t n);
+int den_ngp_ray_grad(const den_ngp_desc* desc, int64_t n, int32_t points, int32_t n_rays, const float* x,
+                     const float* d, const int32_t* ray_idx, const float* t0, const float* t1, const float* params,
+                     void* workspace, void* rg_workspace, float* d_x, float* d_d, void* stream);
 /* tcnn.Encoding alone: x (n,3) in [0,1] -> out (n, 2 n_levels); backward accumulates
  * (atomic adds, caller zeroes) d_table += dL/dtable. */
 int den_hashgrid_fwd(const den_ngp_desc* desc, int64_t n, const float* x, const float* table, float* out,

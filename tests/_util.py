@@ -80,3 +80,36 @@ def ngp_table_grad(z, n):
     g = torch.zeros(n)
     g[torch.from_numpy(z["table_grad_idx"]).long()] = torch.from_numpy(z["table_grad_val"])
     return g
+
+
+# the chair-like synthetic sequence of tests/golden/make_golden.py (EDS sensor constants)
+EDS = dict(input_time_const_eff_it_prod=(35e-12 * 25e-3) / 2000e-12,
+           miller_time_const_eff_it_prod=(0.6e-12 * 25e-3) / 2000e-12, amplifier_gain=140.0,
+           closed_loop_gain=1 / 0.7, output_time_const=25e-6, sf_cutoff_freq=16400.0, diff_amp_cutoff_freq=82000.0)
+
+
+def synthetic_dataset_arrays(rd=1, seed=61, C=64):
+    """camera_calibration.npz + camera_poses.npz contents of a chair-like synthetic sequence:
+    EDS-assumed sensor constants, contrast thresholds 0.25 / 0.2, refractory period 1 us, an
+    800 x 800 f = 1111 camera circling the AABB at radius 4.03 (looking at the origin) over
+    [0.05 s, 1.05 s]."""
+    from scipy.spatial.transform import Rotation
+    g = torch.Generator().manual_seed(seed)
+    K = np.array([[1111.0, 0.0, 400.0], [0.0, 1111.0, 400.0], [0.0, 0.0, 1.0]], dtype=np.float32)
+    cal = {k: np.array(v, dtype=np.float32) for k, v in EDS.items()}
+    cal.update(pos_contrast_threshold=np.array(0.25, np.float32), neg_contrast_threshold=np.array(0.2, np.float32),
+               refractory_period=np.array(1000, np.int64), intrinsics=K,
+               bayer_pattern=np.array("RGGB" if rd == 3 else ""), img_height=np.array(800), img_width=np.array(800))
+    ts = np.linspace(5e7, 1.05e9, C).astype(np.int64)
+    ang = np.linspace(0.0, 1.2, C) + float(torch.rand(1, generator=g)) * 6.28
+    pos = np.stack([4.03 * np.cos(ang), 4.03 * np.sin(ang), 0.6 + 0.2 * np.sin(3 * ang)], -1).astype(np.float32)
+    rots = []
+    for p in pos:
+        z = -p / np.linalg.norm(p)
+        x = np.cross(z, [0.0, 0.0, 1.0])
+        x /= np.linalg.norm(x)
+        y = np.cross(z, x)
+        rots.append(np.stack([x, y, z], -1))
+    quat = Rotation.from_matrix(np.stack(rots)).as_quat().astype(np.float32)  # XYZW
+    poses = dict(T_wc_position=pos, T_wc_orientation=quat, T_wc_timestamp=ts)
+    return cal, poses

@@ -591,7 +591,23 @@ def synthetic_event_batch(N, S, seed, img=800, ts_lo=1.5e8, ts_hi=9.5e8):
     return dict(event=ev, normalized=nz)
 
 
-def ref_deblur_step_module(d, rd, seed, pixbw, S, ct_free, refr_free, res=24, arch="mlp"):
+STEP_DEFAULT = dict(rd=1, pixbw=False, S=8, arch="mlp", N=40, contraction="aabb", aabb=None, near=None, far=None,
+                    cone=0.0, res=24, tv=1e-3, pixbw_free=False)
+
+
+def _step_cfg(**kw):
+    c = dict(STEP_DEFAULT, **kw)
+    rc = RENDER_CFG
+    c["aabb"] = list(rc["aabb"]) if c["aabb"] is None else list(c["aabb"])
+    c["near"] = rc["near"] if c["near"] is None else c["near"]
+    c["far"] = rc["far"] if c["far"] is None else c["far"]
+    # render_step_size "auto" (deblur_e_nerf.py:277-283): sqrt(3) max extent / 1024
+    a = np.asarray(c["aabb"], np.float64)
+    c["step"] = float(np.sqrt(3) * float((a[3:] - a[:3]).max()) / 1024)
+    return c
+
+
+def ref_deblur_step_module(d, seed, cfg, ct_free=True, refr_free=True):
     """The reference DeblurENeRF's training-path methods bound to a module assembled from the
     reference's own components (the constructor needs eval images and Lightning)."""
     dm = _refload.load("models.deblur_e_nerf")
@@ -601,6 +617,7 @@ def ref_deblur_step_module(d, rd, seed, pixbw, S, ct_free, refr_free, res=24, ar
     lossm = _refload.load("loss_metric.loss")
     ED = sys.modules["easydict"].EasyDict
     datasets = _refload.load("data.datasets")
+    rd, pixbw, S = cfg["rd"], cfg["pixbw"], cfg["S"]
     m = dm.DeblurENeRF.__new__(dm.DeblurENeRF)
     torch.nn.Module.__init__(m)
     m.hparams = ED(min_modeled_intensity=0.001,
@@ -608,7 +625,7 @@ def ref_deblur_step_module(d, rd, seed, pixbw, S, ct_free, refr_free, res=24, ar
                    refractory_period=ED(freeze=not refr_free),
                    pixel_bandwidth=ED(enable=pixbw, it_sample_size=S, f_c_dominant_min=21,
                                       target_cumprob=ED(max_sample_lifetime=0.95)),
-                   loss=ED(weight=ED(log_intensity_diff=1.0, log_intensity_tv=1e-3, nerf_mlp_weight_decay=1e-6),
+                   loss=ED(weight=ED(log_intensity_diff=1.0, log_intensity_tv=cfg["tv"], nerf_mlp_weight_decay=1e-6),
                            error_fn=ED(log_intensity_diff="huber", log_intensity_tv="l1"),
                            normalize=ED(log_intensity_diff=True, log_intensity_tv=True)))
     cal = datasets.Event.load_camera_calibration(d)
@@ -627,8 +644,8 @@ def ref_deblur_step_module(d, rd, seed, pixbw, S, ct_free, refr_free, res=24, ar
         m.MODEL_COMPONENTS.append("pixel_bandwidth")
         m.MULTI_PARAM_MODEL_COMPONENTS.append("pixel_bandwidth")
         for p in m.pixel_bandwidth.parameters():
-            p.requires_grad_(False)
-    m.nerf = _ref_nerf(rd, seed, res) if arch == "mlp" else _ref_nerf_ngp(rd, seed, res)[0]
+            p.requires_grad_(bool(cfg["pixbw_free"]))
+    m.nerf = _ref_nerf(rd, seed, cfg["res"]) if cfg["arch"] == "mlp" else _ref_nerf_ngp(rd, seed, cfg["res"], cfg)[0]
     m.trajectory = trm.LinearTrajectory(cp)
     for c, free in (("contrast_threshold", ct_free), ("refractory_period", refr_free)):
         for p in getattr(m, c).parameters():
@@ -644,48 +661,107 @@ def ref_deblur_step_module(d, rd, seed, pixbw, S, ct_free, refr_free, res=24, ar
     return m
 
 
-def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp"):
+def _step_grads(m, cfg):
+    """The gradients a step fixture records (the reference's parameter names)."""
+    out = {}
+    if cfg["arch"] == "mlp":
+        out.update(_grad_pick(m.nerf))
+    else:
+        out.update({f"grad:{k}": prm.grad.detach().numpy() for k, prm in m.nerf.radiance_field.named_parameters()})
+    out["grad_bkgd_orig"] = m.nerf.parametrizations.render_bkgd.original.grad.numpy()
+    ctp = m.contrast_threshold.parametrizations
+    out["d_p2n_orig"] = ctp.p2n_contrast_threshold_ratio.original.grad.numpy()
+    out["d_mean_ct_orig"] = ctp.mean_contrast_threshold.original.grad.numpy()
+    out["dtau_orig"] = m.refractory_period.parametrizations._refractory_period.original.grad.numpy()
+    if cfg["pixbw"] and cfg["pixbw_free"]:
+        for name in ("tau_mil_it_eff_prod", "A_amp_inv", "A_loop_inv", "tau_out", "tau_sf", "tau_diff"):
+            out[f"dpixbw:{name}"] = getattr(m.pixel_bandwidth.parametrizations, name).original.grad.numpy()
+    return out
+
+
+def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra):
     """step_*.npz -- the reference DeblurENeRF.training_step (deblur_e_nerf.py:396-586) run on a
     reference-shaped batch: event correction, supervision timestamps, the occupancy-grid update,
     render_log_intensity x 4 (trajectory, rays, NeRF.forward through render_image with the nerfacc
     stand-in; the pixel-bandwidth model when on), update_train_batch_size, Loss.compute; then the
-    backward.  Contrast thresholds and refractory period learnable (07_ziggy_and_fuzz_hdr.yaml:172);
-    the dtau gradient is also recorded with the trajectory's interpolation weight detached
-    (``dtau_nopose``: the part that does not flow through the camera pose)."""
+    backward.  Contrast thresholds and refractory period learnable (07_ziggy_and_fuzz_hdr.yaml:172).
+    Three runs of the same step:
+      * "full": the reference as configured (f32) -- the fixture's main values;
+      * "nopose": the trajectory's interpolation weight detached (``dtau_orig_nopose``: the part of the
+        tau_r gradient that does not flow through the camera pose);
+      * "f64": the whole module and batch in float64 on the f32 run's recorded occupancy grid and
+        marched samples (``*_f64``): the reference's own f32 rounding error, the floor of the
+        tolerances in tests/test_deblur_gpu.py."""
     from oracle import nerfacc as onerfacc
+    cfg = _step_cfg(pixbw=pixbw, rd=rd, S=S, arch=arch, N=N, **extra)
     cal, poses = synthetic_dataset_arrays(rd)
     d = tempfile.mkdtemp(prefix="den_step_")
     write_dataset(d, cal, poses)
     batch = synthetic_event_batch(N, S if pixbw else 0, seed + 100)
-    out = dict(rd=rd, seed=seed, N=N, S=S, pixbw=pixbw, res=24, sigma_bias_shift=2.0, arch=np.array(arch),
+    out = dict(rd=rd, seed=seed, N=N, S=S, pixbw=pixbw, res=cfg["res"], sigma_bias_shift=2.0, arch=np.array(arch),
+               contraction=np.array(cfg["contraction"]), aabb=np.array(cfg["aabb"], np.float32), near=cfg["near"],
+               far=cfg["far"], cone=cfg["cone"], tv=cfg["tv"], pixbw_free=cfg["pixbw_free"],
                **{f"cal:{k}": v for k, v in cal.items()}, **{f"pose:{k}": v for k, v in poses.items()},
                **{f"event:{k}": v.numpy() for k, v in batch["event"].items()},
                **{f"normalized:{k}": v.numpy() for k, v in batch["normalized"].items()})
-    for variant in ("full", "nopose"):
-        m = ref_deblur_step_module(d, rd, seed, pixbw, S, True, True, arch=arch)
+    kept = []
+    real = onerfacc.ray_marching
+    for variant in ("full", "nopose", "f64"):
+        m = ref_deblur_step_module(d, seed, cfg)
+        dmod = sys.modules["deblur_e_nerf.external.utils"]
         with torch.no_grad():
             if arch == "mlp":
                 m.nerf.radiance_field.mlp.sigma_layer.output_layer.bias.add_(2.0)
             else:
                 m.nerf.radiance_field.mlp_base[1].output_layer.bias[0] += 2.0
         m.train()
+        b = {k: {kk: vv.clone() for kk, vv in v.items()} for k, v in batch.items()}
+        jit = []
+        if variant == "f64":
+            m.double()
+            b["event"]["position"] = b["event"]["position"].double()
+            grid = m.nerf.occupancy_grid
+
+            def replay_grid(step, T_wc_position, g=grid):
+                g.occs.copy_(torch.from_numpy(out["occs"]))
+                g._binary.copy_(torch.from_numpy(out["binary"]))
+            m.nerf.update_occ_grid = replay_grid
+            calls = iter(kept)
+
+            def rec(*a, **k):
+                ri, t0, t1 = next(calls)
+                return ri.clone(), t0.clone(), t1.clone()
+        else:
+            def rec(*a, **k):
+                r = real(*a, **k)
+                jit.append(onerfacc.LAST["jitter"].clone())
+                if variant == "full":
+                    kept.append(tuple(t.clone() for t in r))
+                return r
         if variant == "nopose":
             orig_forward = type(m.trajectory).forward
             m.trajectory.forward = lambda ts, f=orig_forward, t=m.trajectory: f(t, ts.detach())
-        jit = []
-        real = onerfacc.ray_marching
-
-        def rec(*a, **k):
-            r = real(*a, **k)
-            jit.append(onerfacc.LAST["jitter"].clone())
-            return r
-        dmod = sys.modules["deblur_e_nerf.external.utils"]
         dmod.ray_marching = rec
+        # d loss / d render timestamps of each render_log_intensity call (the pose path's input)
+        dts = []
+        orig_rli = m.render_log_intensity
+
+        def rli(timestamp, *a, _f=orig_rli, **k):
+            if timestamp.requires_grad:
+                slot = len(dts)
+                dts.append(None)
+                timestamp.register_hook(lambda g, i=slot: dts.__setitem__(i, g.detach().clone()))
+            return _f(timestamp, *a, **k)
+        m.render_log_intensity = rli
         torch.manual_seed(200)
-        b = {k: {kk: vv.clone() for kk, vv in v.items()} for k, v in batch.items()}
-        loss = m.training_step(b, 0)
-        loss.backward()
-        dmod.ray_marching = real
+        try:
+            loss = m.training_step(b, 0)
+            loss.backward()
+        finally:
+            dmod.ray_marching = real
+        if variant != "nopose":
+            sfx = "" if variant == "full" else "_f64"
+            out.update({f"dts_g{i}{sfx}": g.numpy() for i, g in enumerate(dts) if g is not None})
         if variant == "full":
             grid = m.nerf.occupancy_grid
             out.update(occ_u=grid.last_u.numpy(), occs=grid.occs.numpy(), binary=grid.binary.numpy(),
@@ -693,23 +769,21 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp"):
                            m, "train_batch_size") else 0.0),
                        new_batch_size=np.array(m.trainer.datamodule.train_dataset.batch_size),
                        **{f"jitter_{i}": j.numpy() for i, j in enumerate(jit)})
-            if arch == "mlp":
-                out.update(_grad_pick(m.nerf))
-            else:
+            out.update(_step_grads(m, cfg))
+            if arch != "mlp":
                 rf = m.nerf.radiance_field
-                out.update({f"grad:{k}": prm.grad.detach().numpy() for k, prm in rf.named_parameters()})
                 out.update({f"param:{k}": prm.detach().numpy() for k, prm in rf.named_parameters()
                             if k != "mlp_base.0.params"})
                 out["table"] = rf.mlp_base[0].params.detach().numpy()
                 out["pos_encoding"] = np.array(json.dumps(NGP_SMALL))
-            out["grad_bkgd_orig"] = m.nerf.parametrizations.render_bkgd.original.grad.numpy()
-            ctp = m.contrast_threshold.parametrizations
-            out["d_p2n_orig"] = ctp.p2n_contrast_threshold_ratio.original.grad.numpy()
-            out["d_mean_ct_orig"] = ctp.mean_contrast_threshold.original.grad.numpy()
-            out["dtau_orig"] = m.refractory_period.parametrizations._refractory_period.original.grad.numpy()
-        else:
+        elif variant == "nopose":
             out["dtau_orig_nopose"] = m.refractory_period.parametrizations._refractory_period.original.grad.numpy()
             out["loss_nopose"] = loss.detach().numpy()
+        else:
+            out["loss_f64"] = loss.detach().numpy()
+            for k, v in _step_grads(m, cfg).items():
+                if k != "grad_pick_idx":
+                    out[k + "_f64"] = v
     save(tag or f"step_{'pixbw' if pixbw else 'nopixbw'}_rd{rd}.npz", **out)
 
 
@@ -795,19 +869,23 @@ def gen_ngp(rd=1, seed=21, cfg="small", contraction="aabb", hidden="softplus", r
          **out, **extra, **mlp_w)
 
 
-def _ref_nerf_ngp(rd, seed, res):
-    """The reference NeRF with arch "ngp" (models/nerf.py:105-142) in the chair configuration,
-    oracle/tcnn.py as tcnn.Encoding (NGP_SMALL: 8 levels of 2^12 entries), weights from
-    oracle/ngp.build_params(seed) with the table x 1e3 -> (nerf, params)."""
+def _ref_nerf_ngp(rd, seed, res, cfg=None):
+    """The reference NeRF with arch "ngp" (models/nerf.py:105-142) in the chair configuration (or
+    a step config's aabb / contraction / near / far / cone), oracle/tcnn.py as tcnn.Encoding
+    (NGP_SMALL: 8 levels of 2^12 entries), weights from oracle/ngp.build_params(seed) with the
+    table x 1e3 -> (nerf, params)."""
     from oracle import ngp as ongp
     from oracle import tcnn as otcnn
     nerfm = _refload.load("models.nerf")
     sys.modules["tinycudann"].Encoding = otcnn.Encoding
     ED = sys.modules["easydict"].EasyDict
     CT = sys.modules["nerfacc"].ContractionType
-    c = RENDER_CFG
+    c = RENDER_CFG if cfg is None else cfg
+    ctype = {"aabb": CT.AABB, "sphere": CT.UN_BOUNDED_SPHERE, "tanh": CT.UN_BOUNDED_TANH}[
+        "aabb" if cfg is None else cfg["contraction"]]
+    cone = 0.0 if cfg is None else cfg["cone"]
     occ = ED(resolution=res, occ_thre=0.01, ema_decay=0.95, warmup_steps=256, n=16)
-    nerf = nerfm.NeRF(c["aabb"], CT.AABB, occ, c["near"], c["far"], c["step"], "parameter", 0.0, 1e-4, 0.0, 16384,
+    nerf = nerfm.NeRF(c["aabb"], ctype, occ, c["near"], c["far"], c["step"], "parameter", cone, 1e-4, 0.0, 16384,
                       "ngp", ED(NGP_ARCH), 3, rd)
     p = ongp.build_params(rd, seed, dict(NGP_SMALL))
     p["mlp_base.0.params"] = p["mlp_base.0.params"] * 1e3
@@ -873,6 +951,20 @@ def gen_ngp_all():
     gen_render_ngp(1, 25)
     gen_render_ngp(3, 26)
     gen_step(False, 1, seed=7, tag="step_ngp_nopixbw_rd1.npz", arch="ngp")
+
+
+def gen_step_ngp():
+    gen_step(False, 1, seed=7, tag="step_ngp_nopixbw_rd1.npz", arch="ngp")
+
+
+def gen_step_ziggy():
+    """step_ziggy_rd1.npz -- configs[3]'s model composition (07_ziggy_and_fuzz_hdr.yaml:28-139): the
+    ngp arch with the unbounded-sphere contraction of its aabb, near 0.01 / far 13, cone-angle
+    marching (0.004), pixel bandwidth with S = 30 samples and every sensor parameter learnable,
+    learnable contrast thresholds and refractory period, TV weight 0.1 -- through the reference's
+    training_step (16 events, a 32^3 occupancy grid instead of 256^3 so the CPU run finishes)."""
+    gen_step(True, 1, seed=9, N=16, S=30, tag="step_ziggy_rd1.npz", arch="ngp", contraction="sphere",
+             aabb=[0.2, -0.4, 0.0, 3.7, 3.7, 1.8], near=0.01, far=13.0, cone=0.004, res=32, tv=0.1, pixbw_free=True)
 
 
 if __name__ == "__main__" and len(sys.argv) > 1:

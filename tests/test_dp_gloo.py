@@ -135,3 +135,43 @@ def test_pixbw_event_sharding_partitions_the_global_batch():
         assert torch.equal(torch.cat([p[k] for p in parts], dim=1), full[k]), k
     j = torch.cat([p["jitter"].reshape(4, S, N_PER_RANK) for p in parts], dim=2)
     assert torch.equal(j, full["jitter"].reshape(4, S, -1))
+
+
+def _grid_worker(rank, world, port, out):
+    import sys
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deblur_e_nerf.external.marching import OccupancyGrid, sync_grid
+    grid = OccupancyGrid([-1.5] * 3 + [1.5] * 3, resolution=16)
+    g = torch.Generator().manual_seed(100 + rank)  # per-rank draws, as DataModule.setup seeds them
+    history = []
+    for step in range(5):
+        # a rank-local update (den_occ_update runs on the GPU; here its effect: new EMA values and a
+        # new threshold, different per rank), then fit_step's sync at the next step's start
+        if step % 2 == 0:
+            grid.occs.copy_(torch.rand(grid.num_cells, generator=g))
+            grid._binary.copy_((grid.occs > 0.5).reshape(grid._binary.shape))
+            grid._dirty = True
+        synced = sync_grid(grid)
+        history.append((synced, grid.occs.clone(), grid._binary.clone()))
+    out[rank] = history
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_occupancy_grid_sync_broadcasts_rank0_after_updates():
+    """DDP broadcast_buffers semantics (scripts/run.py:86-88, PyTorch default): after each
+    rank-local occupancy-grid update with different per-rank draws, fit_step's sync_grid leaves
+    every rank holding rank 0's occs / binary; steps without an update do not communicate."""
+    port = _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_grid_worker, args=(WORLD, port, out), nprocs=WORLD, join=True)
+    h0, h1 = out[0], out[1]
+    for step, ((s0, o0, b0), (s1, o1, b1)) in enumerate(zip(h0, h1)):
+        assert s0 == s1 == (step % 2 == 0)
+        assert torch.equal(o0, o1) and torch.equal(b0, b1)
+    assert not torch.equal(h0[0][1], h0[2][1])  # the grid did change between updates

@@ -177,8 +177,9 @@ def test_vol_rendering_matches_reference(golden_dir, rd):
     sig = T("vr_sigma").requires_grad_(True)
     rgb = T("vr_rgb").requires_grad_(True)
     bk = T("vr_bkgd").requires_grad_(True)
-    col, op, dp = marching.rendering(T("vr_t0"), T("vr_t1"), T("vr_ri"), 24, rgb_sigma_fn=lambda a, b, c: (rgb, sig),
-                                     render_bkgd=bk)
+    from deblur_e_nerf.external.vol_rendering import rendering
+    col, op, dp = rendering(T("vr_t0"), T("vr_t1"), T("vr_ri"), 24, rgb_sigma_fn=lambda a, b, c: (rgb, sig),
+                            render_bkgd=bk)
     for a, k in ((col, "vr_color"), (op, "vr_opacity"), (dp, "vr_depth")):
         e = rel_err(a, z[k])
         assert e <= 1e-5, (k, e)
@@ -187,6 +188,30 @@ def test_vol_rendering_matches_reference(golden_dir, rd):
         e = norm_rel(a, z[k])
         print(f"[rd={rd}] {k} err {e:.2e}")
         assert e <= 1e-5, (k, e)
+
+
+@pytest.mark.parametrize("rd", [1, 3])
+def test_vol_rendering_alpha_matches_density(golden_dir, rd):
+    """rendering(rgb_alpha_fn=...) (nerfacc render_weight_from_alpha, vol_rendering.py:96-106) on
+    alpha_i = 1 - exp(-sigma_i (t1 - t0)) renders what rgb_sigma_fn renders from sigma_i, and its
+    alpha gradient maps to the sigma gradient by the chain rule (d alpha / d sigma = dt exp(-sigma dt))."""
+    from deblur_e_nerf.external.vol_rendering import rendering
+    z = np.load(os.path.join(golden_dir, f"render_rd{rd}.npz"))
+    T = lambda k: torch.from_numpy(z[k]).to(DEV)  # noqa: E731
+    t0, t1 = T("vr_t0"), T("vr_t1")
+    sig = T("vr_sigma").requires_grad_(True)
+    rgb = T("vr_rgb")
+    dt = (t1 - t0).reshape(sig.shape)
+    alpha = (1 - torch.exp(-sig.detach() * dt)).requires_grad_(True)
+    grads = (T("vr_gc"), T("vr_go"), T("vr_gd"))
+    outs_s = rendering(t0, t1, T("vr_ri"), 24, rgb_sigma_fn=lambda a, b, c: (rgb, sig), render_bkgd=T("vr_bkgd"))
+    outs_a = rendering(t0, t1, T("vr_ri"), 24, rgb_alpha_fn=lambda a, b, c: (rgb, alpha), render_bkgd=T("vr_bkgd"))
+    for a, b in zip(outs_a, outs_s):
+        assert rel_err(a.detach(), b.detach().cpu().numpy()) <= 1e-5
+    sum((o * g.reshape(o.shape)).sum() for o, g in zip(outs_s, grads)).backward()
+    sum((o * g.reshape(o.shape)).sum() for o, g in zip(outs_a, grads)).backward()
+    mapped = alpha.grad * dt * torch.exp(-sig.detach() * dt)
+    assert norm_rel(mapped, sig.grad.detach().cpu().numpy()) <= 1e-4
 
 
 @pytest.mark.parametrize("rd", [1, 3])

@@ -177,6 +177,49 @@ def test_ngp_packed_samples_match_points():
     assert torch.equal(f.packed_samples(o, dd, ri, t0, t1, density_only=True)[:, 0], sig_p[:, 0].detach())
 
 
+def test_ngp_sparse_gradient_scatter_matches_oracle():
+    """The workgroup-aggregated table scatter (ngp_scatter_kernel) with ray-ordered samples whose
+    upstream gradient is zero on every other sample (masked losses, dead samples): same-cell lanes
+    fold before the scatter, and a zero-gradient lane must neither drop its partners' values nor
+    absorb them.  Table gradient vs oracle/ngp.field at 1e-4 tensor-wise."""
+    pos = dict(ongp.POS_ENCODING, n_levels=8, log2_hashmap_size=14)
+    base = dict(ongp.MLP_BASE, hidden_activation="softplus")
+    head = dict(ongp.MLP_HEAD, hidden_activation="softplus", radiance_activation="softplus")
+    aabb = [-1.5, -1.5, -1.5, 1.5, 1.5, 1.5]
+    rd = 3
+    p = ongp.build_params(rd, 77, pos, table_scale=0.1)
+    f = _field(p, pos, base, head, rd, 0, aabb)
+    g = torch.Generator().manual_seed(78)
+    R, per = 16, 256  # ray-ordered: 256 closely spaced samples per ray share the coarse cells
+    o = torch.rand(R, 3, generator=g) * 0.4 - 0.2
+    dd = torch.nn.functional.normalize(torch.randn(R, 3, generator=g), dim=-1)
+    t = (torch.arange(per, dtype=torch.float32) * 0.004)[None].expand(R, -1)
+    x = (o[:, None, :] + dd[:, None, :] * t[..., None]).reshape(-1, 3)
+    d = dd[:, None, :].expand(-1, per, -1).reshape(-1, 3).contiguous()
+    n = x.shape[0]
+    keep = (torch.arange(n) % 2 == 1).float()[:, None]
+    g_sig = torch.randn(n, 1, generator=g) * keep
+    rgb, sig = f(x.to(DEV), d.to(DEV))
+    (sig * g_sig.to(DEV)).sum().backward()
+    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    _, sig_r = ongp.field(pr, x, d, rd, torch.tensor(aabb), 0, pos, base, head)
+    (sig_r * g_sig).sum().backward()
+    k = "mlp_base.0.params"
+    e = _tensor_rel(dict(f.named_parameters())[k].grad, pr[k].grad)
+    assert e < 1e-4, e
+
+
+def test_ngp_density_only_refuses_grad():
+    """query_density's density-only pass keeps no backward state: under autograd it raises
+    instead of returning a zero gradient."""
+    from deblur_e_nerf.external import ngp
+    f = ngp.NGPradianceField(aabb=[-1.5, -1.5, -1.5, 1.5, 1.5, 1.5]).to(DEV)
+    with pytest.raises(NotImplementedError):
+        f.query_density(torch.zeros(64, 3, device=DEV))
+    with torch.no_grad():
+        assert f.query_density(torch.zeros(64, 3, device=DEV)).shape[0] == 64
+
+
 def test_ngp_rejects_host_tensors():
     from deblur_e_nerf import _native
     from deblur_e_nerf.external import ngp

@@ -256,3 +256,14 @@ def test_tcnn_grid_levels_follow_tcnn_sizing():
     assert [e for _, _, e, _ in levels[:5]] == [4096, 13824, 39304, 117656, 357912]
     assert all(e == 1 << 19 for _, _, e, _ in levels[5:])
     assert total * 2 == otcnn.n_params(c) == 12599920
+
+
+def test_trajectory_oracle_matches_reference(golden_dir):
+    """oracle/trajectory.linear_trajectory (the differentiable restatement the trajectory-backward
+    tests check against) reproduces the reference LinearTrajectory's outputs (traj.npz) exactly."""
+    from oracle import trajectory as otr
+    z = np.load(os.path.join(golden_dir, "traj.npz"))
+    T, P, Q = (torch.from_numpy(z[k]) for k in ("T_wc_timestamp", "T_wc_position", "T_wc_orientation"))
+    for q, kp, kr in (("query_ts", "position", "rotation"), ("query_ts_2d", "position_2d", "rotation_2d")):
+        p, r = otr.linear_trajectory(T, P, Q, torch.from_numpy(z[q]))
+        assert torch.equal(p, torch.from_numpy(z[kp])) and torch.equal(r, torch.from_numpy(z[kr]))
