@@ -50,7 +50,59 @@ def parse():
     ap.add_argument("--it-samples", type=int, default=16)
     ap.add_argument("--cpu-rays", type=int, default=2048,
                     help="rays of the bounded pixel-bandwidth-on CPU-baseline sample (--pixbw)")
+    ap.add_argument("--no-extra-legs", action="store_true",
+                    help="skip the configs[2] (pixel bandwidth on) and F32-mode legs of the N = 1 line")
     return ap.parse_args()
+
+
+BASELINE_METRIC = "train-step rays/sec at 131072 rays \u00d7 128 samples; PSNR vs ref"
+
+
+def metric_name(a):
+    """BASELINE.json's metric string on its own workload, else the workload actually run."""
+    if (a.rays, a.samples) == (131072, 128):
+        return json.loads(f'"{BASELINE_METRIC}"')
+    return f"train-step rays/sec at {a.rays} rays x {a.samples} samples"
+
+
+def build_step(a, dev, rank=0, world=1, pixbw=None, mode=None):
+    from deblur_e_nerf.train import PixbwTrainStep, TrainStep, synthetic_events, synthetic_pixbw_events
+    pixbw = a.pixbw if pixbw is None else pixbw
+    mode = a.mode if mode is None else mode
+    per_event = 4 * a.it_samples if pixbw else 4
+    assert a.rays % (per_event * world) == 0
+    n_events = a.rays // per_event // world
+    if pixbw:
+        ts = PixbwTrainStep(n_events, it_sample_size=a.it_samples, n_samples=a.samples, radiance_dim=a.rd,
+                            mode=mode, device=dev)
+        ts.load_events(**synthetic_pixbw_events(n_events, a.it_samples, rank=rank, world=world))
+    else:
+        ts = TrainStep(n_events, n_samples=a.samples, radiance_dim=a.rd, mode=mode, device=dev)
+        ts.load_events(**synthetic_events(n_events, rank=rank, world=world))
+    return ts, per_event
+
+
+def extra_leg(a, dev, pixbw, mode, steps, warmup=2):
+    """A second workload in the same run (N = 1): BASELINE configs[2] (pixel bandwidth on,
+    it_sample_size 16) or configs[1] in F32 (the reference's arithmetic), timed like the main line."""
+    ts, per_event = build_step(a, dev, pixbw=pixbw, mode=mode)
+    for _ in range(warmup):
+        ts.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ts.step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = {"value": round(a.rays * steps / el, 1), "unit": "rays/s", "ms_per_step": round(el / steps * 1e3, 3),
+           "steps": steps, "warmup": warmup, "dtype": mode,
+           "workload": f"chair synthetic, pixel-bandwidth {'on (it_sample_size=%d)' % a.it_samples if pixbw else 'off'}, "
+                       f"{a.rays} rays x {a.samples} samples, mlp 8x256 rd={a.rd}, "
+                       f"{a.rays // per_event} events, event prep+rays+fwd+bwd+Adam",
+           "loss": [round(x, 6) for x in ts.loss[:3].tolist()]}
+    del ts
+    torch.cuda.empty_cache()
+    return out
 
 
 PHASE_REPS = 3
@@ -357,18 +409,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     from deblur_e_nerf import _native as nat
-    from deblur_e_nerf.train import PixbwTrainStep, TrainStep, synthetic_events, synthetic_pixbw_events
 
-    per_event = 4 * a.it_samples if a.pixbw else 4
-    assert a.rays % (per_event * world) == 0
-    n_events = a.rays // per_event // world
-    if a.pixbw:
-        ts = PixbwTrainStep(n_events, it_sample_size=a.it_samples, n_samples=a.samples, radiance_dim=a.rd,
-                            mode=a.mode, device=dev)
-        ts.load_events(**synthetic_pixbw_events(n_events, a.it_samples, rank=rank, world=world))
-    else:
-        ts = TrainStep(n_events, n_samples=a.samples, radiance_dim=a.rd, mode=a.mode, device=dev)
-        ts.load_events(**synthetic_events(n_events, rank=rank, world=world))
+    ts, per_event = build_step(a, dev, rank, world)
     for _ in range(a.warmup):
         ts.step()
     torch.cuda.synchronize()
@@ -440,6 +482,16 @@ def main():
     roofline["kernels"] = kernels
     roofline["phases_ms"] = {k: round(v, 3) for k, v in phases.items()}
 
+    legs = None
+    if world == 1 and not a.no_extra_legs and not a.pixbw and a.mode == "bf16":
+        del ts
+        torch.cuda.empty_cache()
+        legs = {}
+        for name, pb, mode, k in (("configs2_pixbw_on", True, "bf16", 10), ("configs1_f32", False, "f32", 3)):
+            try:
+                legs[name] = extra_leg(a, dev, pb, mode, k)
+            except Exception as e:  # pragma: no cover - reported, not fatal
+                legs[name] = {"error": repr(e)}
     cpu = None
     psnr_info = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -456,7 +508,7 @@ def main():
                 psnr_info = {"error": repr(e)}
     if rank == 0:
         out = {
-            "metric": "train-step rays/sec at 131072 rays x 128 samples",
+            "metric": metric_name(a),
             "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": a.mode, "data": "synthetic (chair-like raw events + camera poses, PyTorch default-init weights)",
@@ -469,6 +521,7 @@ def main():
             "loss": [round(x, 6) for x in loss],
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "extra_legs": legs,
             "psnr": psnr_info,
         }
         print(json.dumps(out), flush=True)

@@ -174,6 +174,10 @@ __device__ __forceinline__ float dsoftplus_b100_from_out(float s) {
 __device__ __forceinline__ float softplus2_scaled(float t) {
 #ifdef DEN_EXP_CHEAP_ACT  // measurement experiment only (never in libden.so): VALU cost of the epilogue
   return __builtin_amdgcn_fmed3f(t, 0.0f, 3.4028235e38f);
+#elif DEN_SP_DIRECT
+  // log2(1 + 2^t) directly, t clamped below the exp2 overflow (for t > 24 the sum rounds to 2^t and
+  // the log returns t): one VALU op per element fewer than the max + log1p form
+  return __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(t, -3.4028235e38f, 64.0f)));
 #else
   return __builtin_amdgcn_fmed3f(t, 0.0f, 3.4028235e38f) +
          __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(-fabsf(t)));

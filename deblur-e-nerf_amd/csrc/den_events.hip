@@ -161,6 +161,11 @@ __device__ __forceinline__ void max_bwd(double a, double b, double g, double* ga
   else if (b > a) *gb += g;
   else { *ga += 0.5 * g; *gb += 0.5 * g; }
 }
+__device__ __forceinline__ void min_bwd(double a, double b, double g, double* ga, double* gb) {
+  if (a < b) *ga += g;
+  else if (b < a) *gb += g;
+  else { *ga += 0.5 * g; *gb += 0.5 * g; }
+}
 
 constexpr int PREP_BWD_BLOCK = 256;
 
@@ -196,7 +201,7 @@ __global__ void event_prep_bwd_kernel(EventPrepBwdArgs B) {
       // e2 = min(s2 + dt2, tve)
       {
         double ga = 0.0, gb = 0.0;
-        max_bwd(tve, s2 + dt2, a_e2, &gb, &ga);  // min(x, y) = the smaller: swap the roles of max
+        min_bwd(s2 + dt2, tve, a_e2, &ga, &gb);
         a_sum += ga;
         a_tve += gb;
       }
@@ -234,7 +239,7 @@ __global__ void event_prep_bwd_kernel(EventPrepBwdArgs B) {
       double a_sum = 0.0;
       {
         double ga = 0.0, gb = 0.0;
-        max_bwd(end, s + dt, a_e, &gb, &ga);
+        min_bwd(s + dt, end, a_e, &ga, &gb);
         a_sum += ga;
         a_end += gb;
       }

@@ -24,7 +24,10 @@ constexpr int HB_THREADS = 64 * HB_WAVES;
 constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
 constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
 constexpr int HB_SLOT = 2 * HB_BLOCK;  // LDS ring slot: [dz_l block | S'_{l-1} block]
-constexpr int HB_GRID_MAX = 256;
+#ifndef DEN_HB_GRID
+#define DEN_HB_GRID 256  // persistent workgroups (one per CU)
+#endif
+constexpr int HB_GRID_MAX = DEN_HB_GRID;
 #ifndef DEN_HB_NT
 #define DEN_HB_NT 1  // non-temporal dz_l / S'_{l-1} loads and dz_{l-1} stores (streamed once)
 #endif

@@ -669,7 +669,7 @@ __global__ __launch_bounds__(NSC_THREADS) void ngp_scatter_kernel(NgpArgs A) {
 // layer 3 rows 0..31 and 32..63 (x 2 column tiles each), layer 4 (rd x 2).  Lane (j, h) loads row j
 // of a 32-row block at samples 8 u + 4 h .. + 3 (one 16-B load per operand row block and 4 steps;
 // any sample-to-k assignment works as long as A and B agree), so the feature-major rows stream in
-// without LDS.  The bias is the row sum of the A operand, accumulated from the same registers.
+// without LDS.  The bias is the row sum of the A operand, accumulated (in f64) from the same registers.
 // Workgroup = (split, task), 4 waves over interleaved 32-sample chunks, reduced through LDS into
 // partials [task][split][2][32][32] + [64]; a second kernel sums the splits in a fixed order.
 #ifndef DEN_NGP_DW_MFMA
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P, int tas
   const int64_t s0 = (int64_t)blockIdx.x * P.per_split;
   const int64_t s1 = s0 + P.per_split < P.n ? s0 + P.per_split : P.n;
   f32x16 acc[2] = {ngp_zero16(), ngp_zero16()};
-  float bsum[2] = {0.0f, 0.0f};
+  double bsum[2] = {0.0, 0.0};  // f64: the bias is a long sum of cancelling terms
   // the operands of chunk c + 128 load while chunk c's MFMAs run (two register sets, unrolled by 2)
   auto load = [&](int64_t c, f32x4 (&a)[mt][4], f32x4 (&b)[nt][4]) {
 #pragma unroll
@@ -741,12 +741,12 @@ __global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P, int tas
         if constexpr (mt == 2) {
           acc[0] = ngp_mfma(a[0][u][e], b[0][u][e], acc[0]);
           acc[1] = ngp_mfma(a[1][u][e], b[0][u][e], acc[1]);
-          bsum[1] += a[1][u][e];
+          bsum[1] += (double)a[1][u][e];
         } else {
           acc[0] = ngp_mfma(a[0][u][e], b[0][u][e], acc[0]);
           acc[1] = ngp_mfma(a[0][u][e], b[1][u][e], acc[1]);
         }
-        bsum[0] += a[0][u][e];
+        bsum[0] += (double)a[0][u][e];
       }
   };
   f32x4 a0[mt][4], b0[nt][4], a1[mt][4], b1[nt][4];
@@ -762,7 +762,7 @@ __global__ __launch_bounds__(256) void ngp_dw_mfma_kernel(NgpDwMfArgs P, int tas
   // waves 0, 1 add theirs: the split's partial is (w0 + w2) + (w1 + w3), a fixed order.
   float bias[2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) bias[t] = bsum[t] + __shfl_xor(bsum[t], 32);
+  for (int t = 0; t < 2; ++t) bias[t] = (float)(bsum[t] + __shfl_xor(bsum[t], 32));
   float* R = red[wave & 1];
   if (wave >= 2) {
 #pragma unroll

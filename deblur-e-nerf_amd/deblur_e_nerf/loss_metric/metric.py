@@ -37,7 +37,9 @@ class Metric(torch.nn.Module):
         pix = target_img[0].numel()
         err = _native.image_error(pred_img, target_img).cpu()
         rng = float(max_target_val - min_target_val)
-        psnr = [10.0 * math.log10(rng * rng / (float(err[b, 0]) / pix)) for b in range(B)]
+        # a zero MSE gives +inf, as torchmetrics' psnr does (a division by zero in torch)
+        psnr = [10.0 * math.log10(rng * rng / (float(err[b, 0]) / pix)) if float(err[b, 0]) > 0 else math.inf
+                for b in range(B)]
         metric = EasyDict({})
         metric.l1 = torch.tensor(float(err[:, 1].sum()) / (B * pix))
         metric.psnr = torch.tensor(sum(psnr) / B)

@@ -506,6 +506,48 @@ def gen_render(rd=1, seed=4, R=64, sigma_bias_shift=3.5):
     save(f"render_rd{rd}.npz", **out)
 
 
+def gen_fixed(rd=1, seed=4, R=64, S=128, sigma_bias_shift=3.5):
+    """fixed_rd*.npz -- the benchmark's fixed-count sampler (S stratified samples
+    t = t_min + (k + u) dt in AABB n [near, far], oracle/nerf.stratified_samples) packed as nerfacc
+    samples and rendered by the reference's own glue: the rgb_sigma_fn closure of external/utils.py
+    (positions o + d (t0 + t1) / 2, view directions d) over its VanillaNeRFRadianceField, then
+    external/vol_rendering.rendering (weights, accumulation, background); colour / opacity / depth
+    and the gradients of a random projection of them."""
+    from oracle import nerf as onerf
+    nerf = _ref_nerf(rd, seed, RENDER_CFG["res"])
+    rf = nerf.radiance_field
+    with torch.no_grad():
+        rf.mlp.sigma_layer.output_layer.bias.add_(sigma_bias_shift)
+    o, d = _chair_rays(R, 33)
+    u = torch.rand(R, generator=torch.Generator().manual_seed(34))
+    t0, t1 = onerf.stratified_samples(o, d, u, torch.tensor(RENDER_CFG["aabb"]), RENDER_CFG["near"],
+                                      RENDER_CFG["far"], S)
+    ri = torch.arange(R, dtype=torch.int32).repeat_interleave(S)
+    ts, te = t0.reshape(-1, 1), t1.reshape(-1, 1)
+    vr = _refload.load("external.vol_rendering")
+
+    def rgb_sigma_fn(t_starts, t_ends, ray_indices):
+        ray_indices = ray_indices.long()
+        pos = o[ray_indices] + d[ray_indices] * (t_starts + t_ends) / 2.0
+        return rf(pos, d[ray_indices])
+    bk = torch.tensor([0.7] * rd, requires_grad=True)
+    col, opa, dep = vr.rendering(ts, te, ri, R, rgb_sigma_fn=rgb_sigma_fn, render_bkgd=bk)
+    g = torch.Generator().manual_seed(35)
+    gc, go, gd = torch.randn(R, rd, generator=g), torch.randn(R, 1, generator=g), torch.randn(R, 1, generator=g)
+    ((col * gc).sum() + (opa * go).sum() + (dep * gd).sum()).backward()
+    out = dict(seed=seed, rd=rd, S=S, sigma_bias_shift=sigma_bias_shift, aabb=np.array(RENDER_CFG["aabb"]),
+               near=RENDER_CFG["near"], far=RENDER_CFG["far"], rays_o=o.numpy(), rays_d=d.numpy(), jitter=u.numpy(),
+               color=col.detach().numpy(), opacity=opa.detach().numpy(), depth=dep.detach().numpy(), gc=gc.numpy(),
+               go=go.numpy(), gd=gd.numpy(), grad_bkgd=bk.grad.numpy())
+    out.update(_grad_pick(nerf))
+    save(f"fixed_rd{rd}.npz", **out)
+
+
+def gen_fixed_all():
+    gen_fixed(1, seed=4)
+    gen_fixed(3, seed=5)
+
+
 def gen_traj():
     """traj.npz -- models/trajectories.py LinearTrajectory (searchsorted, lerp, the shortest-path
     full-angle slerp of utils/tensor_ops.py:118-184, quaternion -> rotation matrix) with RoMa
@@ -679,6 +721,23 @@ def _step_grads(m, cfg):
     return out
 
 
+class _GradTap(torch.autograd.Function):
+    """Identity whose backward hands the incoming gradient to ``fn``."""
+
+    @staticmethod
+    def forward(ctx, x, fn):
+        ctx.fn = fn
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.fn(g)
+        return g, None
+
+
+N_PERM = 3  # event-permuted f32 reruns of each step fixture
+
+
 def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra):
     """step_*.npz -- the reference DeblurENeRF.training_step (deblur_e_nerf.py:396-586) run on a
     reference-shaped batch: event correction, supervision timestamps, the occupancy-grid update,
@@ -706,7 +765,7 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra
                **{f"normalized:{k}": v.numpy() for k, v in batch["normalized"].items()})
     kept = []
     real = onerfacc.ray_marching
-    for variant in ("full", "nopose", "f64"):
+    for variant in ("full", "nopose", "f64") + tuple(f"f32p{k}" for k in range(N_PERM)):
         m = ref_deblur_step_module(d, seed, cfg)
         dmod = sys.modules["deblur_e_nerf.external.utils"]
         with torch.no_grad():
@@ -717,9 +776,19 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra
         m.train()
         b = {k: {kk: vv.clone() for kk, vv in v.items()} for k, v in batch.items()}
         jit = []
+        perm = inv = None
+        if variant.startswith("f32p"):
+            # the same step with the events in another order: every sum over events / rays / samples
+            # runs in another order, the f64 result does not change -- the spread of these f32 runs is
+            # the reference's own f32 rounding noise (tests/test_deblur_gpu.py bounds)
+            perm = torch.randperm(N, generator=torch.Generator().manual_seed(400 + int(variant[4:])))
+            inv = torch.argsort(perm)
+            b = {k: {kk: vv[..., perm].clone() if kk != "position" else vv[:, perm].clone() for kk, vv in v.items()}
+                 for k, v in b.items()}
         if variant == "f64":
             m.double()
             b["event"]["position"] = b["event"]["position"].double()
+        if variant != "full" and variant != "nopose":
             grid = m.nerf.occupancy_grid
 
             def replay_grid(step, T_wc_position, g=grid):
@@ -728,9 +797,14 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra
             m.nerf.update_occ_grid = replay_grid
             calls = iter(kept)
 
-            def rec(*a, **k):
-                ri, t0, t1 = next(calls)
-                return ri.clone(), t0.clone(), t1.clone()
+            def rec(*a, _inv=inv, **k):
+                ri, t0, t1 = (t.clone() for t in next(calls))
+                if _inv is not None:  # ray s N + e of the original order is ray s N + inv[e] here
+                    r = ri.long()
+                    new = (r // N) * N + _inv[r % N]
+                    order = torch.sort(new, stable=True).indices
+                    ri, t0, t1 = new[order].to(ri.dtype), t0[order], t1[order]
+                return ri, t0, t1
         else:
             def rec(*a, **k):
                 r = real(*a, **k)
@@ -742,7 +816,10 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra
             orig_forward = type(m.trajectory).forward
             m.trajectory.forward = lambda ts, f=orig_forward, t=m.trajectory: f(t, ts.detach())
         dmod.ray_marching = rec
-        # d loss / d render timestamps of each render_log_intensity call (the pose path's input)
+        # d loss / d render timestamps of each render_log_intensity call, the part that flows
+        # through the call itself (trajectory -> rays -> render, the pose path's input): an identity
+        # in front of the call records it, the timestamp's other uses (diff end / subdiff
+        # timestamps derived from it) do not reach it
         dts = []
         orig_rli = m.render_log_intensity
 
@@ -750,7 +827,7 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra
             if timestamp.requires_grad:
                 slot = len(dts)
                 dts.append(None)
-                timestamp.register_hook(lambda g, i=slot: dts.__setitem__(i, g.detach().clone()))
+                timestamp = _GradTap.apply(timestamp, lambda g, i=slot: dts.__setitem__(i, g.detach().clone()))
             return _f(timestamp, *a, **k)
         m.render_log_intensity = rli
         torch.manual_seed(200)
@@ -760,8 +837,10 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra
         finally:
             dmod.ray_marching = real
         if variant != "nopose":
-            sfx = "" if variant == "full" else "_f64"
-            out.update({f"dts_g{i}{sfx}": g.numpy() for i, g in enumerate(dts) if g is not None})
+            sfx = "" if variant == "full" else "_" + variant
+            # per-event timestamp gradients back in the original event order
+            out.update({f"dts_g{i}{sfx}": (g if inv is None else g[..., inv]).numpy() for i, g in enumerate(dts)
+                        if g is not None})
         if variant == "full":
             grid = m.nerf.occupancy_grid
             out.update(occ_u=grid.last_u.numpy(), occs=grid.occs.numpy(), binary=grid.binary.numpy(),
@@ -780,15 +859,59 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra
             out["dtau_orig_nopose"] = m.refractory_period.parametrizations._refractory_period.original.grad.numpy()
             out["loss_nopose"] = loss.detach().numpy()
         else:
-            out["loss_f64"] = loss.detach().numpy()
+            sfx = "_" + variant
+            out["loss" + sfx] = loss.detach().numpy()
             for k, v in _step_grads(m, cfg).items():
                 if k != "grad_pick_idx":
-                    out[k + "_f64"] = v
+                    out[k + sfx] = v
     save(tag or f"step_{'pixbw' if pixbw else 'nopixbw'}_rd{rd}.npz", **out)
+
+
+def gen_eval(rd=1, seed=6, H=20, W=24):
+    """eval_rd*.npz -- the reference DeblurENeRF.evaluation_step's render (deblur_e_nerf.py:602-652):
+    render_pixels of an H x W image (the meshgrid pixel positions of :120-127) at one camera pose,
+    eval mode (no jitter, chunked marching), after one occupancy-grid update at step 0 (its U[0,1)
+    draws recorded).  Small intrinsics (f = 1.4 W) so the image covers the AABB."""
+    cfg = _step_cfg(rd=rd)
+    cal, poses = synthetic_dataset_arrays(rd)
+    d = tempfile.mkdtemp(prefix="den_eval_")
+    write_dataset(d, cal, poses)
+    m = ref_deblur_step_module(d, seed, cfg)
+    with torch.no_grad():
+        m.nerf.radiance_field.mlp.sigma_layer.output_layer.bias.add_(2.0)
+    torch.manual_seed(300)
+    m.nerf.update_occ_grid(step=0, T_wc_position=m.trajectory.T_wc_position)
+    grid = m.nerf.occupancy_grid
+    m.eval()
+    K = torch.tensor([[1.4 * W, 0.0, W / 2.0], [0.0, 1.4 * W, H / 2.0], [0.0, 0.0, 1.0]])
+    kinv = torch.linalg.inv(K)
+    i = 17
+    pos = m.trajectory.T_wc_position[i]
+    from oracle import roma as oroma
+    rot = oroma.unitquat_to_rotmat(m.trajectory.T_wc_orientation_quat[i])
+    pix = torch.stack(torch.meshgrid(torch.arange(W), torch.arange(H), indexing="xy"), dim=2).to(torch.float32)
+    P = pos.view(1, 1, 3).expand(H, W, -1)
+    R = rot.view(1, 1, 3, 3).expand(H, W, -1, -1)
+    with torch.no_grad():
+        img, opacity, depth, mspr, _ = m.render_pixels(kinv, pix, P, R)
+    save(f"eval_rd{rd}.npz", rd=rd, seed=seed, N=0, S=8, pixbw=False, res=cfg["res"], sigma_bias_shift=2.0,
+         **{f"cal:{k}": v for k, v in cal.items()}, **{f"pose:{k}": v for k, v in poses.items()},
+         occ_u=grid.last_u.numpy(), occs=grid.occs.numpy(), kinv=kinv.numpy(), pos=pos.detach().numpy(),
+         rot=rot.detach().numpy(), H=H, W=W, img=img.numpy(), opacity=opacity.numpy(), depth=depth.numpy(),
+         mean_samples_per_ray=np.array(float(mspr)))
+
+
+def gen_eval_all():
+    gen_eval(1, seed=6)
+    gen_eval(3, seed=8)
 
 
 def gen_step_pixbw():
     gen_step(True, 1)
+
+
+def gen_step_nopixbw():
+    gen_step(False, 1)
 
 
 def gen_mlp_unbounded():

@@ -209,3 +209,36 @@ def test_render_survives_density_overflow(mode):
     tol = 1e-4 if mode == "f32" else 1e-3
     assert rel_err(c, ref_c) <= tol
     assert torch.isfinite(flat.grad).all()
+
+
+# ----------------------------------------------------------------------------- benchmark sampler vs reference rendering
+@pytest.mark.parametrize("rd", [1, 3])
+@pytest.mark.parametrize("mode,tol_out,tol_grad", [("f32", 1e-4, 1e-4), ("bf16", 1e-3, 3e-2)])
+def test_fixed_sampler_matches_reference_rendering(golden_dir, rd, mode, tol_out, tol_grad):
+    """The benchmark's fused fixed-count path (den_render points = 0: stratified sampler, field,
+    wave-scan compositing, background) against the reference's own rendering glue on the same
+    stratified samples packed as nerfacc samples (make_golden.gen_fixed: external/utils.py's
+    rgb_sigma_fn closure over VanillaNeRFRadianceField, then external/vol_rendering.rendering):
+    colour / opacity / depth at the north-star 1e-4 in F32 (image-wise relative), and the parameter
+    and background gradients of a random projection of them (BF16: its stated bounds)."""
+    nat = _nat()
+    z = np.load(os.path.join(golden_dir, f"fixed_rd{rd}.npz"))
+    p = onerf.build_params(rd, int(z["seed"]))
+    p["mlp.sigma_layer.output_layer.bias"] = p["mlp.sigma_layer.output_layer.bias"] + float(z["sigma_bias_shift"])
+    flat = flat_from_params(p, rd).to(DEV).requires_grad_(True)
+    packed = nat.PackedWeights(mode, rd, DEV)
+    packed.pack(flat.detach())
+    bk = torch.full((rd,), 0.7, device=DEV, requires_grad=True)
+    o, d, u = (torch.from_numpy(z[k]).to(DEV) for k in ("rays_o", "rays_d", "jitter"))
+    cfg = dict(_cfg(mode, rd, float(z["near"]), float(z["far"])), aabb=[float(v) for v in z["aabb"]])
+    col, opa, dep = nat.render(o, d, u, bk, flat, cfg, packed, int(z["S"]))
+    e = [norm_rel(col, z["color"]), norm_rel(opa, z["opacity"][:, 0]), norm_rel(dep, z["depth"][:, 0])]
+    ((col * torch.from_numpy(z["gc"]).to(DEV)).sum() + (opa * torch.from_numpy(z["go"][:, 0]).to(DEV)).sum()
+     + (dep * torch.from_numpy(z["gd"][:, 0]).to(DEV)).sum()).backward()
+    pick = flat.grad.detach().cpu()[torch.from_numpy(z["grad_pick_idx"])]
+    eg = norm_rel(pick, z["grad_pick"])
+    eb = norm_rel(bk.grad, z["grad_bkgd"])
+    print(f"[fixed {mode} rd={rd}] colour {e[0]:.2e} opacity {e[1]:.2e} depth {e[2]:.2e}; "
+          f"MLP grad (4096 picks) {eg:.2e}, background grad {eb:.2e}")
+    assert max(e) <= tol_out
+    assert eg <= tol_grad and eb <= tol_grad
