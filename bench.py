@@ -17,6 +17,7 @@ accounting.
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -50,6 +51,8 @@ def parse():
     ap.add_argument("--it-samples", type=int, default=16)
     ap.add_argument("--cpu-rays", type=int, default=2048,
                     help="rays of the bounded pixel-bandwidth-on CPU-baseline sample (--pixbw)")
+    ap.add_argument("--psnr-steps", type=int, default=2000, help="Adam steps of the converged-PSNR leg (0: skip)")
+    ap.add_argument("--psnr-only", action="store_true", help="run the converged-PSNR leg alone and print it")
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the configs[2] (pixel bandwidth on) and F32-mode legs of the N = 1 line")
     return ap.parse_args()
@@ -367,6 +370,101 @@ def psnr_vs_oracle(rd, threads, dev, steps=8, n_events=1024, n_samples=64, view=
                                         f"{view}x{view} view, PSNR vs the teacher render (data range 1)")
 
 
+def _teacher_batch(gen, n_events, dev, motion=0.3, radius=4.03):
+    """Events of a camera circling the AABB: per event a pixel direction seen from 4 poses (diff
+    start / end, TV start / end inside it) moving by up to `motion` along a random direction."""
+    N = n_events
+    v = torch.randn(N, 3, generator=gen, device=dev)
+    c0 = v / v.norm(dim=-1, keepdim=True) * radius
+    look = -c0 / c0.norm(dim=-1, keepdim=True) + (torch.rand(N, 3, generator=gen, device=dev) * 2 - 1) * math.sin(0.3)
+    look = look / look.norm(dim=-1, keepdim=True)
+    m = torch.randn(N, 3, generator=gen, device=dev)
+    m = m / m.norm(dim=-1, keepdim=True) * motion * torch.rand(N, 1, generator=gen, device=dev)
+    s = torch.rand(2, N, 1, generator=gen, device=dev).sort(dim=0).values
+    o = torch.cat([c0, c0 + m, c0 + s[0] * m, c0 + s[1] * m])
+    d = look.repeat(4, 1)
+    jit = torch.rand(4 * N, generator=gen, device=dev)
+    end = torch.full((N,), 10 ** 9, dtype=torch.int64, device=dev)
+    start = end.double() - 1e6
+    return dict(rays_o=o.contiguous(), rays_d=d.contiguous(), jitter=jit, end_ts=end, start_ts=start,
+                ts_diff=end.double() - start)
+
+
+VIEW_DIRS = ((0.62, -0.55, 0.56), (-0.7, 0.3, 0.4), (0.1, 0.8, -0.5), (-0.4, -0.6, -0.3))
+
+
+def psnr_long(rd, dev, steps=2000, n_events=1024, n_samples=64, view=64, modes=("f32", "bf16"), milestones=(0.5, 0.8)):
+    """BASELINE's "PSNR vs ref" at convergence: the HIP TrainStep in F32 (the reference's arithmetic,
+    pinned to the reference at 1e-4 by tests/) and in BF16 (the benchmark's mode) train from ONE init
+    on a teacher scene for `steps` Adam steps, each on a fresh batch of configs[0]'s shape (1024
+    events = 4096 rays x 64 samples) whose measured log-intensity changes are the teacher's; a
+    learning rate is cut x0.3 at the `milestones` fractions (the reference's multi_step_lr); four
+    held-out views of each are aligned to the teacher's by the reference's affine log-intensity
+    correction (deblur_e_nerf.py:705-833, one correction over the batch of views) and scored with
+    its PSNR (metric.py:68-72, data range [0, max target], mean over the views).
+    delta_db = BF16 - F32."""
+    from deblur_e_nerf import _native as nat
+    from deblur_e_nerf.external import mlp, ngp
+    from deblur_e_nerf.loss_metric.metric import psnr
+    from deblur_e_nerf.models.deblur_e_nerf import affine_log_intensity_correction
+    from deblur_e_nerf.train import TrainStep
+    # the teacher: the same architecture, another seeded init, density raised (an opaque scene)
+    torch.manual_seed(77)
+    field = mlp.VanillaNeRFRadianceField([-1.5, -1.5, -1.5, 1.5, 1.5, 1.5], radiance_dim=rd,
+                                         hidden_activation=torch.nn.Softplus(beta=100),
+                                         density_activation=ngp.shifted_trunc_exp,
+                                         radiance_activation=torch.nn.Softplus(beta=1), mode="f32")
+    with torch.no_grad():
+        field.mlp.sigma_layer.output_layer.bias.add_(3.0)
+    tflat = field.flat_params.detach().to(dev).contiguous()
+    tcfg = dict(mode=nat.mode_id("f32"), rd=rd, aabb=[-1.5, -1.5, -1.5, 1.5, 1.5, 1.5], near=1.43, far=6.63)
+    tpacked = nat.PackedWeights("f32", rd, dev)
+    tpacked.pack(tflat)
+    ones = torch.ones(rd, device=dev)
+    rays = [_view_rays(view, direction=v) for v in VIEW_DIRS]
+    vo = torch.cat([r[0] for r in rays]).to(dev)
+    vd = torch.cat([r[1] for r in rays]).to(dev)
+    vu = torch.full((vo.shape[0],), 0.5, device=dev)
+    nv = len(VIEW_DIRS)
+    with torch.no_grad():
+        target, _, _ = nat.render(vo, vd, vu, ones, tflat, tcfg, tpacked, n_samples)
+    out = {}
+    for mode in modes:
+        ts = TrainStep(n_events, n_samples=n_samples, radiance_dim=rd, mode=mode, device=dev, seed=0)
+        gen = torch.Generator(device=dev).manual_seed(123)
+        t0 = time.perf_counter()
+        lr0 = ts.lr
+        for it in range(steps):
+            ts.lr = lr0 * 0.3 ** sum(it >= int(m * steps) for m in milestones)
+            b = _teacher_batch(gen, n_events, dev)
+            with torch.no_grad():
+                col, _, _ = nat.render(b["rays_o"], b["rays_d"], b["jitter"], ones, tflat, tcfg, tpacked, n_samples)
+            y = torch.log(col[:, 0] + 1e-3).view(4, n_events)
+            ts.load_batch(lid=(y[1] - y[0]).float().contiguous(), **b)
+            ts.step()
+        torch.cuda.synchronize()
+        train_s = time.perf_counter() - t0
+        with torch.no_grad():
+            hv, _, _ = nat.render(vo, vd, vu, torch.nn.functional.softplus(ts.bkgd_orig.detach()), ts.flat.detach(),
+                                  dict(ts.cfg), ts.packed, n_samples)
+        tgt = target[:, 0].reshape(nv, view, view).clamp_min(1e-6)
+        pred = hv[:, 0].reshape(nv, view, view).clamp_min(1e-6)
+        corr, gamma, scale = affine_log_intensity_correction(pred, tgt)
+        rng = float(tgt.max())
+        out[mode] = {"psnr_db": round(psnr(corr.float().to(dev), tgt[:, None], rng), 3),
+                     "psnr_uncorrected_db": round(psnr(pred[:, None], tgt[:, None], rng), 3),
+                     "gamma": round(float(gamma[0]), 4), "scale": round(float(scale[0]), 4),
+                     "train_s": round(train_s, 2), "final_loss": [round(x, 6) for x in ts.loss[:3].tolist()]}
+        del ts
+        torch.cuda.empty_cache()
+    if "f32" in out and "bf16" in out:
+        out["delta_db"] = round(out["bf16"]["psnr_db"] - out["f32"]["psnr_db"], 4)
+    return dict(out, steps=steps, setup=f"teacher scene, {steps} Adam steps from one init (lr x0.3 at "
+                                        f"{list(milestones)} of the run), each on a fresh batch of {n_events} events = "
+                                        f"{4 * n_events} rays x {n_samples} samples; {nv} held-out {view}x{view} views, "
+                                        f"affine log-intensity correction, mean PSNR vs the teacher")
+
+
 def cpu_baseline_pixbw(n_rays, n_samples, rd, S, threads):
     """Bounded CPU sample of the pixel-bandwidth-on step (oracle): median of 3 after 1 warm-up."""
     from oracle import nerf as onerf
@@ -409,6 +507,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     from deblur_e_nerf import _native as nat
+    if a.psnr_only:
+        print(json.dumps(psnr_long(a.rd, dev, steps=a.psnr_steps)), flush=True)
+        return
 
     ts, per_event = build_step(a, dev, rank, world)
     for _ in range(a.warmup):
@@ -506,6 +607,11 @@ def main():
                 psnr_info = psnr_vs_oracle(a.rd, cpu_threads(), dev)
             except Exception as e:  # pragma: no cover - reported, not fatal
                 psnr_info = {"error": repr(e)}
+            if a.psnr_steps > 0:
+                try:  # converged: HIP BF16 vs HIP F32 after psnr_steps steps on fresh teacher batches
+                    psnr_info = dict(psnr_info or {}, converged=psnr_long(a.rd, dev, steps=a.psnr_steps))
+                except Exception as e:  # pragma: no cover - reported, not fatal
+                    psnr_info = dict(psnr_info or {}, converged={"error": repr(e)})
     if rank == 0:
         out = {
             "metric": metric_name(a),

@@ -78,6 +78,10 @@ __device__ __forceinline__ typename Tr<MODE>::Acc acc_zero() {
 // so every store / load instruction of a wave moves 1 KiB of consecutive bytes.
 // `tile` is the (wave-uniform) base of the tile; each lane adds its own offset.
 
+// BF16 hidden softplus as log2(1 + 2^t) (softplus2_scaled)
+#ifndef DEN_SP_DIRECT
+#define DEN_SP_DIRECT 1
+#endif
 // Activation / dz tiles are written once and read once, by a later kernel, after far more data
 // than the caches hold: BF16 stores and loads of them go non-temporal (DEN_NT_STREAMS).
 #ifndef DEN_NT_STREAMS
@@ -174,7 +178,7 @@ __device__ __forceinline__ float dsoftplus_b100_from_out(float s) {
 __device__ __forceinline__ float softplus2_scaled(float t) {
 #ifdef DEN_EXP_CHEAP_ACT  // measurement experiment only (never in libden.so): VALU cost of the epilogue
   return __builtin_amdgcn_fmed3f(t, 0.0f, 3.4028235e38f);
-#elif DEN_SP_DIRECT
+#elif DEN_SP_DIRECT  // default; 0: the max + log1p form (r03 A/B: render_fwd 24.9 -> 24.0 ms per step)
   // log2(1 + 2^t) directly, t clamped below the exp2 overflow (for t > 24 the sum rounds to 2^t and
   // the log returns t): one VALU op per element fewer than the max + log1p form
   return __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(t, -3.4028235e38f, 64.0f)));

@@ -453,6 +453,47 @@ class DeblurENeRF(_Base):
         return intensity
 
 
+def affine_log_intensity_correction(pred_intensity_img, target_intensity_img, gain_exposure_prod=None,
+                                    has_bayer_filter=False, per_channel_log_it_scale=False):
+    """The evaluation's affine log-intensity alignment (deblur_e_nerf.py:705-833, without the joint
+    black-level refinement, the LM step of :835-900, out of scope): the predicted log intensities
+    mapped by the least-squares (f64) scale and offset -- per channel, or one scale and per-channel
+    offsets for a Bayer sensor without ``per_channel_log_it_scale`` -- onto the targets'
+    (normalised by the mean-normalised gain-exposure product).  Images ([B,] [1/3,] H, W) ->
+    (corrected predicted intensities (B, 1/3, H, W), gamma, scale)."""
+    pred, target = pred_intensity_img.detach().cpu(), target_intensity_img.detach().cpu()
+    while target.dim() < 3:
+        pred, target = pred[None], target[None]
+    if target.dim() == 3:  # (B, H, W): grayscale -> a channel dim of 1 (:722-725)
+        pred, target = pred.unsqueeze(1), target.unsqueeze(1)
+    B, C, H, W = target.shape
+    gep = torch.ones(B, dtype=torch.float64) if gain_exposure_prod is None else \
+        torch.as_tensor(gain_exposure_prod, dtype=torch.float64).reshape(B)
+    log_gep = (gep / gep.mean()).log().view(B, 1, 1, 1)
+    plog = pred.to(torch.float64).log()
+    tlog = target.to(torch.float64).log() - log_gep
+    per_channel = (not has_bayer_filter) or per_channel_log_it_scale
+    if per_channel:
+        A = torch.nn.functional.pad(plog.unsqueeze(-1), (0, 1), value=1.0)  # (B, C, H, W, 2)
+    else:
+        A = torch.nn.functional.pad(plog.unsqueeze(-1), (0, 3), value=0.0)  # (B, 3, H, W, 4)
+        for c in range(3):
+            A[:, c, ..., c + 1] = 1.0
+    A = A.transpose(0, 1).flatten(1, 3)                                      # (C, B H W, 2 | 4)
+    y = tlog.unsqueeze(-1).transpose(0, 1).flatten(1, 3)                     # (C, B H W, 1)
+    if not per_channel:
+        A, y = A.flatten(0, 1), y.flatten(0, 1)
+    sol = torch.linalg.lstsq(A, y).solution
+    corr = (A @ sol)
+    corr = corr.view(C, B, H, W).transpose(0, 1)
+    if per_channel:
+        gamma, scale = sol[:, 0, 0], sol[:, 1, 0].exp()
+    else:
+        gamma, scale = sol[0, :], sol[1:, 0].exp()
+    # black_level_offset off: the gain-exposure normalisation undone on the prediction (:819-826)
+    return (corr + log_gep).exp(), gamma, scale
+
+
 def allreduce_gradients(module):
     """DDP gradient semantics over the ranks of the default process group: the mean of each
     gradient, as one all-reduce of one flat buffer (RCCL over xGMI on the GPU box)."""

@@ -161,7 +161,20 @@ class NeRF(torch.nn.Module):
         """nerf.py:206-228 on the device (den_pixel_rays): (3,3), (N,2), ([M,] N, 3),
         ([M,] N, 3, 3) -> ray origins, unit directions ([M,] N, 3); differentiable in the poses
         (den_pixel_rays_bwd) when they require grad."""
-        return _native.pixel_rays(intrinsics_inverse.float().contiguous(), pixel_position.float().contiguous(),
+        pix = pixel_position.float()
+        lead = T_wc_position.shape[:-1]
+        if pix.dim() > 2:
+            # an image grid of pixels (H, W, 2) with poses (..., H, W, 3) (evaluation_step,
+            # deblur_e_nerf.py:620-634): flatten the grid, render groups stay in front
+            n = pix.shape[:-1]
+            if tuple(lead[len(lead) - len(n):]) != tuple(n):
+                raise _native.DenError("pixel_params_to_ray: pixel grid and pose grid differ")
+            N = pix[..., 0].numel()
+            o, d = _native.pixel_rays(intrinsics_inverse.float().contiguous(), pix.reshape(N, 2).contiguous(),
+                                      T_wc_position.float().reshape(-1, N, 3).contiguous(),
+                                      T_wc_orientation.float().reshape(-1, N, 3, 3).contiguous())
+            return o.reshape(*lead, 3), d.reshape(*lead, 3)
+        return _native.pixel_rays(intrinsics_inverse.float().contiguous(), pix.contiguous(),
                                   T_wc_position.float().contiguous(), T_wc_orientation.float().contiguous())
 
     def _forward_fixed(self, ray_origin, ray_direction):

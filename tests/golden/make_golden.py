@@ -506,7 +506,7 @@ def gen_render(rd=1, seed=4, R=64, sigma_bias_shift=3.5):
     save(f"render_rd{rd}.npz", **out)
 
 
-def gen_fixed(rd=1, seed=4, R=64, S=128, sigma_bias_shift=3.5):
+def gen_fixed(rd=1, seed=4, R=64, S=128, sigma_bias_shift=0.0):
     """fixed_rd*.npz -- the benchmark's fixed-count sampler (S stratified samples
     t = t_min + (k + u) dt in AABB n [near, far], oracle/nerf.stratified_samples) packed as nerfacc
     samples and rendered by the reference's own glue: the rgb_sigma_fn closure of external/utils.py
@@ -849,6 +849,8 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra
                        new_batch_size=np.array(m.trainer.datamodule.train_dataset.batch_size),
                        **{f"jitter_{i}": j.numpy() for i, j in enumerate(jit)})
             out.update(_step_grads(m, cfg))
+            for i, (ri, t0, t1) in enumerate(kept):  # the marched samples of each render call
+                out.update({f"kept_ri_{i}": ri.numpy(), f"kept_t0_{i}": t0.numpy(), f"kept_t1_{i}": t1.numpy()})
             if arch != "mlp":
                 rf = m.nerf.radiance_field
                 out.update({f"param:{k}": prm.detach().numpy() for k, prm in rf.named_parameters()
