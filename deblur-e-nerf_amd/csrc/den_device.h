@@ -80,7 +80,7 @@ __device__ __forceinline__ typename Tr<MODE>::Acc acc_zero() {
 
 // BF16 hidden softplus as log2(1 + 2^t) (softplus2_scaled)
 #ifndef DEN_SP_DIRECT
-#define DEN_SP_DIRECT 1
+#define DEN_SP_DIRECT 0
 #endif
 // Activation / dz tiles are written once and read once, by a later kernel, after far more data
 // than the caches hold: BF16 stores and loads of them go non-temporal (DEN_NT_STREAMS).

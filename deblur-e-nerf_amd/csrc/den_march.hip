@@ -494,6 +494,21 @@ __global__ void composite_fwd_kernel(CompArgs C) {
 
 // adjoint: with g_i = dC.rgb_i + (dO - dC.bkgd) + dD t_mid_i,
 //   dL/dsigma_i = delta_i (T_{i+1} g_i - sum_{k>i} w_k g_k),  dL/drgb_i = w_i dC,  dL/dbkgd = dC (1 - O)
+// The suffix sums run back to front (the reverse cumulative sum torch's autograd of the reference's
+// cumsum takes): total - prefix cancels to eps * total for the late samples of a saturated ray, whose
+// dL/dsigma then carries that error times their large delta sigma into the density gradients.
+// Pass 1 (front to back) keeps each sample's exclusive optical depth in d_sigma and w_i g_i in
+// d_rgb[.][0] (scratch); pass 2 (back to front) reads them and overwrites both with the gradients.
+__device__ __forceinline__ float wave_incl_suffix(float v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float o = __shfl_down(v, off, 64);
+    if (lane + off < 64) v += o;
+  }
+  return v;
+}
+
 __global__ void composite_bwd_kernel(CompArgs C) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
@@ -508,8 +523,13 @@ __global__ void composite_bwd_kernel(CompArgs C) {
   if (C.bkgd)
     for (int ch = 0; ch < C.rd; ++ch) bk_dot += dC[ch] * C.bkgd[ch];
   const float dO_eff = dO - bk_dot;
-  // pass 1: opacity and S = sum_k w_k g_k
-  float carry = 0.0f, op = 0.0f, wg = 0.0f;
+  auto g_of = [&](int64_t s, float tmid) {
+    float g = dO_eff + dD * tmid;
+    for (int ch = 0; ch < C.rd; ++ch) g += dC[ch] * C.rgb[s * C.rd + ch];
+    return g;
+  };
+  // pass 1: exclusive optical depth and w g per sample, the opacity
+  float carry = 0.0f, op = 0.0f;
   for (int64_t b = s0; b < s1; b += 64) {
     const int64_t s = b + lane;
     const bool in = s < s1;
@@ -518,47 +538,41 @@ __global__ void composite_bwd_kernel(CompArgs C) {
     const float excl = carry + wave_excl_scan(tau);
     if (in) {
       const float w = expf(-excl) * comp_alpha(C, s, tau);
-      float g = dO_eff + dD * tmid;
-      for (int ch = 0; ch < C.rd; ++ch) g += dC[ch] * C.rgb[s * C.rd + ch];
       op += w;
-      wg += w * g;
+      C.d_sigma[s] = excl;
+      C.d_rgb[s * C.rd] = w * g_of(s, tmid);
     }
     carry += wave_sum(tau);
   }
   const float opacity = wave_sum(op);
-  const float total = wave_sum(wg);
-  // pass 2: the gradients, suffix sums as total - inclusive prefix
-  carry = 0.0f;
-  float prefix = 0.0f;
-  for (int64_t b = s0; b < s1; b += 64) {
-    const int64_t s = b + lane;
+  // pass 2: back to front, suffix_i = sum_{k > i} w_k g_k accumulated directly
+  float later = 0.0f;  // sum of w g over the blocks after this one
+  const int64_t nb = (s1 - s0 + 63) / 64;
+  for (int64_t q = nb - 1; q >= 0; --q) {
+    const int64_t s = s0 + q * 64 + lane;
     const bool in = s < s1;
     float tau, dlt, tmid;
     comp_sample(C, s, in, &tau, &dlt, &tmid);
-    const float ex = wave_excl_scan(tau);
-    const float excl = carry + ex;
-    float w = 0.0f, g = 0.0f;
+    const float excl = in ? C.d_sigma[s] : 0.0f;
+    const float wg = in ? C.d_rgb[s * C.rd] : 0.0f;
+    const float incl = wave_incl_suffix(wg);     // sum over lanes >= this one
+    const float nxt = __shfl_down(incl, 1, 64);  // sum over lanes > this one (adds only)
+    const float suffix = later + (lane < 63 ? nxt : 0.0f);
     if (in) {
-      w = expf(-excl) * comp_alpha(C, s, tau);
-      g = dO_eff + dD * tmid;
-      for (int ch = 0; ch < C.rd; ++ch) g += dC[ch] * C.rgb[s * C.rd + ch];
-    }
-    const float wgi = wave_incl_scan(w * g);
-    if (in) {
-      const float suffix = total - (prefix + wgi);
-      const float Tnext = expf(-(excl + tau));
+      const float g = g_of(s, tmid);
+      const float w = expf(-excl) * comp_alpha(C, s, tau);
       if (C.alpha) {
         // dL/dalpha_i = T_i g_i - suffix_i / (1 - alpha_i); at alpha = 1 every later weight is 0
         const float a = fminf(C.sigma[s], 1.0f);
         C.d_sigma[s] = expf(-excl) * g - (a < 1.0f ? __fdiv_rn(suffix, 1.0f - a) : 0.0f);
       } else {
+        const float Tnext = expf(-(excl + tau));
         const float dtau = Tnext * g - suffix;
         C.d_sigma[s] = (dlt > 0.0f) ? dtau * dlt : 0.0f;
       }
       for (int ch = 0; ch < C.rd; ++ch) C.d_rgb[s * C.rd + ch] = w * dC[ch];
     }
-    prefix += __shfl(wgi, 63, 64);
-    carry += wave_sum(tau);
+    later += __shfl(incl, 0, 64);
   }
   if (lane == 0 && C.bkgd_partial)
     for (int ch = 0; ch < C.rd; ++ch)

@@ -245,7 +245,28 @@ def test_full_size_step_properties():
         assert torch.equal(a, t_sub.reshape(4, n, -1).cpu())
     p64 = {k: v.double() for k, v in unflat(sub.flat.detach().cpu(), 1).items()}
     b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in b.items()}
-    _, (Ld, Lt, tot) = flat_grad(p64, sub.bkgd_orig.detach().cpu().double(), b64, 128, 1)
+    g64, (Ld, Lt, tot) = flat_grad(p64, sub.bkgd_orig.detach().cpu().double(), b64, 128, 1)
     loss = sub.loss[:3].cpu().tolist()
-    print(f"full-size loss {full.loss[:3].cpu().tolist()}; sub-batch {loss} vs f64 oracle {(Ld, Lt, tot)}")
+    e_sub = norm_rel(sub.gbuf, g64)
+    print(f"full-size loss {full.loss[:3].cpu().tolist()}; sub-batch {loss} vs f64 oracle {(Ld, Lt, tot)}; "
+          f"sub-batch gradient vs f64 oracle {e_sub:.2e}")
     assert abs(loss[2] - tot) <= 3e-2 * abs(tot)
+    assert e_sub <= 6e-2  # the BF16 gradient bound of this file
+    # linearity at full size: the 2^24-sample gradient (persistent split-K over every CU, one
+    # reduction) equals the event-weighted sum of the gradients of its K sub-batches computed
+    # separately -- the loss is a mean over events, so g_full = sum_k (n_k / N) g_k (BF16
+    # summation-order noise: 1e-2)
+    K = 8
+    acc = torch.zeros_like(full.gbuf, dtype=torch.float64)
+    g_full = full.gbuf.detach().double().clone()
+    del full
+    torch.cuda.empty_cache()
+    part = TrainStep(N // K, n_samples=128, radiance_dim=1, mode="bf16", device=DEV, seed=5)
+    for k in range(K):
+        part.load_batch(**synthetic_batch(N // K, seed=5, rank=k, world=K))
+        part.forward()
+        part.backward()
+        acc += part.gbuf.double() / K
+    e_lin = norm_rel(acc, g_full)
+    print(f"full-size gradient vs the mean of {K} sub-batch gradients: {e_lin:.2e}")
+    assert e_lin <= 1e-2
