@@ -85,9 +85,13 @@ def build_step(a, dev, rank=0, world=1, pixbw=None, mode=None):
     return ts, per_event
 
 
-def extra_leg(a, dev, pixbw, mode, steps, warmup=2):
+def extra_leg(a, dev, pixbw, mode, steps, warmup=2, rays=None):
     """A second workload in the same run (N = 1): BASELINE configs[2] (pixel bandwidth on,
-    it_sample_size 16) or configs[1] in F32 (the reference's arithmetic), timed like the main line."""
+    it_sample_size 16) or configs[1] in F32 (the reference's arithmetic), timed like the main line.
+    ``rays``: a smaller batch where the F32 workspace (~20 KB per sample kept for the backward) would not fit one GPU
+    at 2^17 rays x 128 samples (314 GiB): the rate is per ray, the batch only has to fill the chip."""
+    if rays is not None:
+        a = argparse.Namespace(**dict(vars(a), rays=rays))
     ts, per_event = build_step(a, dev, pixbw=pixbw, mode=mode)
     for _ in range(warmup):
         ts.step()
@@ -588,9 +592,10 @@ def main():
         del ts
         torch.cuda.empty_cache()
         legs = {}
-        for name, pb, mode, k in (("configs2_pixbw_on", True, "bf16", 10), ("configs1_f32", False, "f32", 3)):
+        for name, pb, mode, k, rays in (("configs2_pixbw_on", True, "bf16", 10, None),
+                                        ("configs1_f32_65536_rays", False, "f32", 3, a.rays // 2)):
             try:
-                legs[name] = extra_leg(a, dev, pb, mode, k)
+                legs[name] = extra_leg(a, dev, pb, mode, k, rays=rays)
             except Exception as e:  # pragma: no cover - reported, not fatal
                 legs[name] = {"error": repr(e)}
     cpu = None

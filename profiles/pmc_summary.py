@@ -82,10 +82,10 @@ def mfma_summary(out_dir, tag, n_simd=1024):
     return res
 
 
-def main(out_dir, tag):
+def main(out_dir, tag, prefix=""):
     here = os.path.dirname(os.path.abspath(__file__))
-    fetch = per_launch(os.path.join(out_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write = per_launch(os.path.join(out_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    fetch = per_launch(os.path.join(out_dir, prefix + "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_launch(os.path.join(out_dir, prefix + "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     kern = {}
     for k in sorted(set(fetch) & set(write)):
         rd, wr = 2.0 * fetch[k] * 1024, write[k] * 1024
@@ -94,18 +94,19 @@ def main(out_dir, tag):
                    "hbm_bytes_per_launch": rd + wr}
     res = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes ({tag}); "
                      "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes",
-           "command": "bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak (profiles/gpu_r02a.sh)",
+           "command": f"bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak ({'profiles/gpu_r03c.sh' if prefix else 'profiles/gpu_r02a.sh'})",
            "workload": {"rays": 131072, "samples": 128, "mode": "bf16", "rd": 1},
            "kernels": kern}
     with open(os.path.join(here, "pmc_traffic.json"), "w") as f:
         json.dump(res, f, indent=1)
     rows = []
-    with open(os.path.join(out_dir, "prof", "run_kernel_stats.csv")) as f:
+    with open(os.path.join(out_dir, prefix + "prof", "run_kernel_stats.csv")) as f:
         for r in csv.DictReader(f):
             rows.append(r)
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
              "Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python bench.py --steps 5 --warmup 2 "
-             "--no-cpu-baseline --no-gemm-peak` (profiles/gpu_r02a.sh, gpu_r02g.sh); 7 train steps + 3 phase-timing reps per kernel.", "",
+             "--no-cpu-baseline --no-gemm-peak` (" + ("profiles/gpu_r03c.sh" if prefix else "profiles/gpu_r02a.sh, gpu_r02g.sh")
+             + "); 7 train steps + 3 phase-timing reps per kernel.", "",
              "| kernel | calls | avg ms | total % |", "|---|---|---|---|"]
     for r in rows[:20]:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | "
@@ -115,7 +116,7 @@ def main(out_dir, tag):
     for k, v in kern.items():
         lines.append(f"| `{k}` | {v['hbm_read_bytes_per_launch'] / 1e9:.2f} | "
                      f"{v['hbm_write_bytes_per_launch'] / 1e9:.2f} | {v['hbm_bytes_per_launch'] / 1e9:.2f} |")
-    if os.path.exists(os.path.join(out_dir, "pmc_mfma", "run_counter_collection.csv")):
+    if not prefix and os.path.exists(os.path.join(out_dir, "pmc_mfma", "run_counter_collection.csv")):
         mf = mfma_summary(out_dir, tag)
         lines += ["", f"MFMA utilisation and wave-time breakdown (separate SQ passes, profiles/{tag}_pmc_mfma.json):",
                   "", "| kernel | MFMA util | wait (waitcnt/barrier) | issue stall | active | LDS-issue stall | "
@@ -131,4 +132,4 @@ def main(out_dir, tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "")
