@@ -432,7 +432,7 @@ int den_version(void) { return DEN_VERSION; }
 #ifdef DEN_FWD_PROF
 // experiment builds only: per-wave cycle split of the last render_fwd launch (512 WGs x 8 waves x 4)
 int den_debug_fwd_prof(uint64_t* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(den_fwd_prof), sizeof(uint64_t) * 512 * 8 * 4) == hipSuccess ? DEN_OK
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(den_fwd_prof), sizeof(uint64_t) * 512 * 8 * 8) == hipSuccess ? DEN_OK
                                                                                                         : DEN_EHIP;
 }
 #endif

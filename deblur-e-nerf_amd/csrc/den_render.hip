@@ -188,11 +188,16 @@ struct FwdVm {
   int issued;
   int mark[FWD_RING];
 #ifdef DEN_FWD_PROF
-  uint64_t prof[4];  // experiment builds only: cycles in body / vmcnt wait / barrier / whole kernel
+  // experiment builds only: cycles in body / vmcnt wait / barrier, kernel start, prologue end,
+  // layers end, kernel end, (unused)
+  uint64_t prof[8];
 #endif
 };
 #ifdef DEN_FWD_PROF
-__device__ uint64_t den_fwd_prof[512 * 8 * 4];
+#ifndef DEN_FWD_PROF_BASE
+#define DEN_FWD_PROF_BASE 0  // first workgroup recorded (512 of them): past the cold start, e.g. 32768
+#endif
+__device__ uint64_t den_fwd_prof[512 * 8 * 8];
 #endif
 
 // One forward step: issue chunk t+FWD_RING-1 into the slot chunk t-1 used (free since the last
@@ -340,6 +345,9 @@ __device__ __forceinline__ constexpr int fwd_tail_store_ops() {
 #ifndef DEN_FWD_PF
 #define DEN_FWD_PF 4
 #endif
+#ifndef DEN_FWD_LDS_OPAQUE
+#define DEN_FWD_LDS_OPAQUE 1  // r03 A/B: render_fwd 24.60 / 24.87 -> 24.38 / 24.39 ms per step
+#endif
 #ifndef DEN_FWD_SCHED
 #define DEN_FWD_SCHED 0  // r02 A/B: pinned schedule 25.8 ms vs 24.9 ms for the compiler's order (NB = 1)
 #endif
@@ -352,13 +360,25 @@ __device__ __forceinline__ void mfma_chunk_nb(const char* lds_chunk, const typen
     return;
   } else if constexpr (MODE == 1) {
     constexpr int PF = DEN_FWD_PF < KS ? DEN_FWD_PF : KS;
+#if DEN_FWD_LDS_OPAQUE
+    // the chunk's LDS address as a run-time VGPR: unrolled, the slot is a compile-time constant and
+    // the compiler folds it into every read's address -- past 64 KiB that no longer fits the 16-bit
+    // offset field, and each read of the third ring slot then costs a v_or (and a temporary)
+    typedef __attribute__((address_space(3))) const bf16x8 lds_frag_t;
+    uint32_t lb = (uint32_t)(uintptr_t)(lds_ptr_t)lds_chunk + (uint32_t)lane * 16u;
+    asm volatile("" : "+v"(lb));
+    const lds_frag_t* lq = (const lds_frag_t*)(uintptr_t)lb;
+    auto rd = [&](int k) -> bf16x8 { return lq[k * 64]; };
+#else
+    auto rd = [&](int k) -> bf16x8 { return *(const bf16x8*)(lds_chunk + k * 1024 + lane * 16); };
+#endif
     bf16x8 a[PF];
 #pragma unroll
-    for (int p = 0; p < PF; ++p) a[p] = *(const bf16x8*)(lds_chunk + (K0 + p) * 1024 + lane * 16);
+    for (int p = 0; p < PF; ++p) a[p] = rd(K0 + p);
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
       const bf16x8 cur = a[k % PF];
-      if (k + PF < KS) a[k % PF] = *(const bf16x8*)(lds_chunk + (K0 + k + PF) * 1024 + lane * 16);
+      if (k + PF < KS) a[k % PF] = rd(K0 + k + PF);
 #pragma unroll
       for (int b = 0; b < NB; ++b) acc[b] = Tr<1>::mfma(cur, x[b * S + K0 + k], acc[b]);
     }
@@ -522,7 +542,8 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
 #pragma unroll
   for (int ch = 0; ch < FWD_RING; ++ch) vm.mark[ch] = 0;
 #ifdef DEN_FWD_PROF
-  vm.prof[0] = vm.prof[1] = vm.prof[2] = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) vm.prof[q] = 0;
   vm.prof[3] = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -572,8 +593,19 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
       acc_to_frags<MODE>(a, pe + b * PE_S + p * FPT);
     }
   }
-  wait_vm_lgkm0<0>();  // the untracked prologue DMAs landed (and the pe stores drained)
+#ifndef DEN_FWD_PE_INFLIGHT
+#define DEN_FWD_PE_INFLIGHT 1
+#endif
+  // the untracked prologue DMAs landed; the pe stores (the youngest vector-memory ops, issued after
+  // the DMAs and the ray loads) may stay in flight -- vmcnt is in-order, so waiting for all but them
+  // covers the DMAs (older ops left in flight only make the later counted waits stricter)
+  constexpr int PE_ST = (TRAIN && DEN_FWD_PE_INFLIGHT) ? NB * PE_T * (MODE == 1 ? 2 : 1) : 0;
+  static_assert(PE_ST < 64, "vmcnt is 6 bits");
+  wait_vm_lgkm0<PE_ST>();
   __syncthreads();
+#ifdef DEN_FWD_PROF
+  vm.prof[4] = __builtin_amdgcn_s_memtime();
+#endif
 
   constexpr int KS = WIDTH / T::KI;  // k-steps of a 256-wide input
   Frag xa[NB * KS], xb[NB * KS];
@@ -631,11 +663,15 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
 #undef DEN_PST
 
 #ifdef DEN_FWD_PROF
-  vm.prof[3] = __builtin_amdgcn_s_memtime() - vm.prof[3];
-  if (blockIdx.x < 512 && lane == 0) {
+  vm.prof[5] = __builtin_amdgcn_s_memtime();
+  auto prof_store = [&]() {
+    const int pb = (int)blockIdx.x - DEN_FWD_PROF_BASE;
+    if (pb >= 0 && pb < 512 && lane == 0) {
+      vm.prof[6] = __builtin_amdgcn_s_memtime();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) den_fwd_prof[(blockIdx.x * 8 + wave) * 4 + q] = vm.prof[q];
-  }
+      for (int q = 0; q < 8; ++q) den_fwd_prof[(pb * 8 + wave) * 8 + q] = vm.prof[q];
+    }
+  };
 #endif
   // per-sample sigma / rgb (lane group 0 holds rows 0..)
   if (grp == 0) {
@@ -659,6 +695,9 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
       }
     }
   }
+#ifdef DEN_FWD_PROF
+  if (A.points) prof_store();
+#endif
   if (A.points) return;
   __syncthreads();
 
@@ -726,6 +765,9 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
       A.out_depth[r] = dp;
     }
   }
+#ifdef DEN_FWD_PROF
+  prof_store();
+#endif
 }
 
 // ------------------------------------------------------------------ backward kernel

@@ -29,7 +29,7 @@ def main():
     cfg = dict(mode=nat.mode_id("bf16"), rd=rd, aabb=list(onerf.AABB_CHAIR), near=1.43, far=6.63)
     lib = nat.lib()
     lib.den_debug_fwd_prof.argtypes = [ctypes.c_void_p]
-    buf = np.zeros(512 * 8 * 4, dtype=np.uint64)
+    buf = np.zeros(512 * 8 * 8, dtype=np.uint64)
     ms = []
     for it in range(4):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -42,16 +42,23 @@ def main():
         del c, op, dp
     print(f"render call ms (incl. host glue): {['%.2f' % m for m in ms]}")
     assert lib.den_debug_fwd_prof(buf.ctypes.data) == 0
-    p = buf.reshape(512, 8, 4).astype(np.float64)
-    waves = p[:, :, 3] > 0
-    tot = p[:, :, 3][waves]
-    print(f"train={train} waves={waves.sum()} kernel cycles/wave mean {tot.mean():.0f}")
+    p = buf.reshape(512, 8, 8).astype(np.float64)
+    waves = p[:, :, 6] > 0
+    start, pro, lay, end = p[:, :, 3], p[:, :, 4], p[:, :, 5], p[:, :, 6]
+    tot = (end - start)[waves]
+    print(f"train={train} waves={waves.sum()} (workgroups from DEN_FWD_PROF_BASE) wave cycles mean {tot.mean():.0f}")
+    for name, v in (("prologue", (pro - start)[waves]), ("layers", (lay - pro)[waves]), ("tail", (end - lay)[waves])):
+        print(f"  {name:9s} {v.mean():10.0f} cyc/wave ({v.mean() / tot.mean() * 100:5.1f} %)")
     for q, name in enumerate(["body", "vm wait", "barrier"]):
         v = p[:, :, q][waves]
-        print(f"  {name:8s} {v.mean():10.0f} cyc/wave ({v.mean() / tot.mean() * 100:5.1f} %)")
+        print(f"    {name:8s} {v.mean():10.0f} cyc/wave ({v.mean() / tot.mean() * 100:5.1f} %)")
     per_wave = p[:, :, 0][waves]
     print(f"  body min/max over waves {per_wave.min():.0f} / {per_wave.max():.0f}")
-    print(f"  prologue+tail {tot.mean() - p[:, :, :3].sum(-1)[waves].mean():.0f} cyc/wave")
+    wg0 = start[:, 0][waves[:, 0]]
+    wg1 = end.max(1)[waves[:, 0]]
+    span = (wg1.max() - wg0.min())
+    print(f"  512 workgroups span {span:.0f} cycles; sum of their lifetimes / span = "
+          f"{(wg1 - wg0).sum() / span:.1f} workgroups resident on average")
 
 
 if __name__ == "__main__":
