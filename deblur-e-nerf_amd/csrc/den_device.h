@@ -328,6 +328,16 @@ __device__ __forceinline__ float wave_incl_scan(float v) {
   }
   return v;
 }
+// inclusive suffix sum over the wave (lane l gets the sum over lanes >= l)
+__device__ __forceinline__ float wave_incl_suffix(float v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float o = __shfl_down(v, off, 64);
+    if (lane + off < 64) v += o;
+  }
+  return v;
+}
 // exclusive prefix sum over the wave (lane 0 gets 0); adds only, no incl - v subtraction
 __device__ __forceinline__ float wave_excl_scan(float v) {
   const float incl = wave_incl_scan(v);

@@ -499,15 +499,6 @@ __global__ void composite_fwd_kernel(CompArgs C) {
 // dL/dsigma then carries that error times their large delta sigma into the density gradients.
 // Pass 1 (front to back) keeps each sample's exclusive optical depth in d_sigma and w_i g_i in
 // d_rgb[.][0] (scratch); pass 2 (back to front) reads them and overwrites both with the gradients.
-__device__ __forceinline__ float wave_incl_suffix(float v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float o = __shfl_down(v, off, 64);
-    if (lane + off < 64) v += o;
-  }
-  return v;
-}
 
 __global__ void composite_bwd_kernel(CompArgs C) {
 #pragma clang fp contract(off)

@@ -894,8 +894,8 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
     }
     float base = wave_excl_scan(run);
     float w[4], gv[4], op_part = 0.0f;
-    float wg_run = 0.0f, wgl[4];
-    
+    float wg_run = 0.0f, wgq[4];
+
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (q >= spl) break;
@@ -905,24 +905,32 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
     }
     const float opacity = wave_sum(op_part);
     const float dO_eff = dO - bk_dot;
-    
+
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (q >= spl) break;
       gv[q] = dC[0] * rc4[q][0] + dC[1] * rc4[q][1] + dC[2] * rc4[q][2] + dO_eff + dD * tmid[q];
-      wg_run += w[q] * gv[q];
-      wgl[q] = wg_run;
+      wgq[q] = w[q] * gv[q];
+      wg_run += wgq[q];
     }
-    // suffix sums of w*g: total - inclusive prefix
-    float wg_incl_lane = wave_incl_scan(wg_run);
-    float wg_total = __shfl(wg_incl_lane, 63, 64);
-    float wg_base = wg_incl_lane - wg_run;
-    
+    // suffix sums of w*g accumulated back to front (the reverse cumulative sum of torch's autograd of
+    // the reference's cumsum): total - prefix cancels to eps * total on the late samples of a
+    // saturated ray (den_march.hip composite_bwd_kernel)
+    const float wg_suf_incl = wave_incl_suffix(wg_run);            // lanes >= this one
+    const float wg_after = __shfl_down(wg_suf_incl, 1, 64);       // lanes > this one
+    float sfx[4] = {0.f, 0.f, 0.f, 0.f}, later = lane < 63 ? wg_after : 0.0f;
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+      if (q >= spl) continue;
+      sfx[q] = later;
+      later += wgq[q];
+    }
+
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (q >= spl) break;
       int kk = lane * spl + q;
-      float suffix = wg_total - (wg_base + wgl[q]);  // sum_{j>k} w_j g_j
+      float suffix = sfx[q];  // sum_{j>k} w_j g_j
       float incl = base + loc[q];
       float Tnext = expf(-incl);
       float dtau = Tnext * gv[q] - suffix;
