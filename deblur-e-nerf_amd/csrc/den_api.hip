@@ -76,6 +76,11 @@ struct TimedLaunch {
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+#ifndef DEN_LB_HIDDEN
+#define DEN_LB_HIDDEN 1  // BF16: Lb^T + its weight gradient as a layer-major launch (den_hidden.hip);
+                         // 0 = in render_bwd_kernel + a streamed weight gradient (r03: 1.6-2 ms slower)
+#endif
+
 #ifndef DEN_DW_STREAM
 #define DEN_DW_STREAM 1  // BF16: operand-sharing streamed weight gradients (den_dwstream.hip)
 #endif
@@ -279,13 +284,15 @@ int launch_dwstream_reduce(const den_render_desc* d, const WsLayout& L, char* ws
   return DEN_OK;
 }
 
-// Layer-major backward of hidden layer l (den_hidden.hip) + reduction of its weight/bias gradient.
+// Layer-major backward of hidden layer l (den_hidden.hip) + reduction of its weight/bias gradient;
+// l = 8 is the [bottleneck | sigma] layer Lb (input S7, dz_b with the sigma tile, 9 row tiles).
 int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLayout& L, char* ws, int l, float* grad,
                   hipStream_t s) {
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
+  const bool lb = l == 8;
   HiddenArgs H{};
   H.w = (const char*)io->w_bwd + bwd_layer_offset(DEN_MODE_BF16, 10 - l);
-  H.dz_in = ws + L.act[D_Z0 + l];
+  H.dz_in = ws + L.act[lb ? D_ZB : D_Z0 + l];
   H.s_in = ws + L.act[A_S0 + l - 1];
   H.dz_out = ws + L.act[D_Z0 + l - 1];
   H.partial = (float*)(ws + L.dw_partial);
@@ -294,9 +301,13 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   H.per_wg = (H.n_blocks + grid - 1) / grid;
   {
     DEN_TIMED(T_HIDDEN_BWD, s);
-    hipLaunchKernelGGL(hidden_bwd_kernel, dim3((unsigned)grid), dim3(HB_THREADS), 0, s, H);
+    if (lb)
+      hipLaunchKernelGGL(hidden_bwd_kernel<true>, dim3((unsigned)grid), dim3(HB_THREADS), 0, s, H);
+    else
+      hipLaunchKernelGGL(hidden_bwd_kernel<false>, dim3((unsigned)grid), dim3(HB_THREADS), 0, s, H);
   }
   DEN_LAUNCHED();
+  if (lb) return launch_dwstream_reduce(d, L, ws, 9, 8, 0, 9, L_B, WIDTH, 0, 1, grad, s);
   DwReduceArgs R{};
   R.partial = H.partial;
   R.splits = (int)grid;
@@ -355,14 +366,14 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
   if (parts & 1) {
     if constexpr (MODE == DEN_MODE_BF16) {
       if (hidden) {
-        // head (compositing adjoint, Lr^T, Lg^T, Lb^T) sample-major, then L7..L1 layer-major
+        // head (compositing adjoint, Lr^T, Lg^T[, Lb^T]) sample-major, then [Lb,] L7..L1 layer-major
         {
           DEN_TIMED(T_RENDER_BWD, s);
-          hipLaunchKernelGGL((render_bwd_kernel<MODE, 2>), dim3((unsigned)(n / wg_samples(MODE))), dim3(512), 0, s,
-                             A);
+          hipLaunchKernelGGL((render_bwd_kernel<MODE, DEN_LB_HIDDEN ? 1 : 2>), dim3((unsigned)(n / wg_samples(MODE))),
+                             dim3(512), 0, s, A);
         }
         DEN_LAUNCHED();
-        for (int l = 7; l >= 1; --l)
+        for (int l = DEN_LB_HIDDEN ? 8 : 7; l >= 1; --l)
           if ((rc = launch_hidden(d, io, L, ws, l, G, s)) != DEN_OK) return rc;
       }
     }
@@ -381,8 +392,10 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
       return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream<9, 9, 8, 8, DEN_DWS_NW2, 3>(d, L, ws, D_ZB, -1, A_S0 + 7, -1, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream_reduce(d, L, ws, 9, 8, 0, 9, L_B, 256, 0, 1, G, s)) != DEN_OK) return rc;
+    if (!DEN_LB_HIDDEN) {
+      if ((rc = launch_dwstream<9, 9, 8, 8, DEN_DWS_NW2, 3>(d, L, ws, D_ZB, -1, A_S0 + 7, -1, s)) != DEN_OK) return rc;
+      if ((rc = launch_dwstream_reduce(d, L, ws, 9, 8, 0, 9, L_B, 256, 0, 1, G, s)) != DEN_OK) return rc;
+    }
     if ((rc = launch_dwstream<4, 4, 8, 9, DEN_DWS_NW3, 4>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 4, 9, 0, 4, L_G, 256, WIDTH, 1, G, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK) return rc;

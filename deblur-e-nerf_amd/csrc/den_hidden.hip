@@ -1,6 +1,7 @@
-// den_hidden.hip -- layer-major backward of the hidden layers L7..L1 (BF16 mode).
+// den_hidden.hip -- layer-major backward of the [bottleneck | sigma] layer Lb and the hidden layers
+// L7..L1 (BF16 mode).
 //
-// One launch per hidden layer l (transposed layer j = 10 - l), one persistent workgroup per CU
+// One launch per layer l (transposed layer j = 10 - l; Lb = l 8, j 2), one persistent workgroup per CU
 // sweeping a contiguous range of 32-sample wave blocks of the wave-block-major activation tensors
 // (den_geom.h).  Per block, wave w of 4 (one per SIMD, 512 VGPRs) owns rows [64w, 64w + 64):
 //   chain : dS_{l-1} = W_l^T dz_l                (A = W_l^T row tiles 2w, 2w+1 held in VGPRs for
@@ -13,8 +14,9 @@
 // this moves 1.5 KiB of HBM (read dz_l and S'_{l-1}, write dz_{l-1}) where the sample-major chain
 // plus the split-K GEMM (den_render.hip + den_dw.hip; kept for the F32 parity mode) move 3 KiB.
 //
-// Reference: the nn.Linear backward of base.hidden_layers.{1..7} with softplus(beta=100)
-// (external/mlp.py:99-113, models/nerf.py:18), in the scaled base-2 units of den_geom.h.
+// Reference: the nn.Linear backward of base.hidden_layers.{1..7}, bottleneck_layer and sigma_layer
+// with softplus(beta=100) on their input (external/mlp.py:99-113, :155-186, models/nerf.py:18), in the
+// scaled base-2 units of den_geom.h.
 #include "den_device.h"
 
 namespace den {
@@ -23,7 +25,6 @@ constexpr int HB_WAVES = 4;
 constexpr int HB_THREADS = 64 * HB_WAVES;
 constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
 constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
-constexpr int HB_SLOT = 2 * HB_BLOCK;  // LDS ring slot: [dz_l block | S'_{l-1} block]
 #ifndef DEN_HB_GRID
 #define DEN_HB_GRID 256  // persistent workgroups (one per CU)
 #endif
@@ -42,13 +43,8 @@ constexpr int HB_GRID_MAX = DEN_HB_GRID;
 #endif
 constexpr int HB_PF = DEN_HB_PF;
 constexpr int HB_DEPTH = DEN_HB_DEPTH;                   // blocks in flight ahead of the computed one
-constexpr int HB_RING = HB_DEPTH + 1;                    // LDS slots (32 KiB each; <= 5 fit in 160 KiB)
-constexpr int HB_DMA_OPS = 2 * (16 / 4);                 // LDS-DMA instructions per wave per block
+constexpr int HB_RING = HB_DEPTH + 1;                    // LDS slots (32 KiB each, 33 for Lb; <= 4 fit in 160 KiB)
 constexpr int HB_STORE_OPS = 4;                          // dz_{l-1} stores per wave per block
-// vector-memory ops a wave issues after its DMA of block b+1 by the end of block b (issue order:
-// stores(b-2), DMA(b+2), stores(b-1), DMA(b+3), stores(b)); the asm DMAs clobber "memory", so the
-// stores keep their program order around them
-constexpr int HB_YOUNGER = HB_STORE_OPS + (HB_DEPTH - 1) * (HB_DMA_OPS + HB_STORE_OPS);
 
 typedef short hb_v4i16 __attribute__((ext_vector_type(4)));
 
@@ -108,6 +104,24 @@ __device__ __forceinline__ void hb_dma_untracked(const char* src, char* dst) {
   }
 }
 
+// The same for NP pieces of 1 KiB (NP not a multiple of the wave count: the last piece is fetched
+// again by the waves past it, so every wave issues ceil(NP / 4) DMA instructions -- a uniform count
+// for the counted vmcnt waits; the duplicates write the same bytes)
+template <int NP>
+__device__ __forceinline__ void hb_dma_untracked_n(const char* src, char* dst) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t off0 = (uint32_t)hb_slot(lane, 0) * 16, off1 = (uint32_t)hb_slot(lane, 1) * 16;
+#pragma unroll
+  for (int q = 0; q < (NP + HB_WAVES - 1) / HB_WAVES; ++q) {
+    const int pw = q * HB_WAVES + wave;
+    const int pc = __builtin_amdgcn_readfirstlane(pw < NP ? pw : NP - 1);
+    const char* base = src + pc * 1024;
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(dst + pc * 1024));
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"((pc & 1) ? off1 : off0),
+                 "s"(base), "s"(m0) : "memory", "m0");
+  }
+}
+
 // This lane's own fragment f of a tile in LDS (the chain's B operand / the stored activation).
 __device__ __forceinline__ bf16x8 hb_frag(const char* tile, int f) {
   return *(const bf16x8*)(tile + f * 1024 + hb_slot(threadIdx.x & 63, f) * 16);
@@ -131,6 +145,22 @@ __device__ __forceinline__ bf16x8 hb_tr_frag(const char* tile, int kk) {
   return out;
 }
 
+// hb_tr_frag with the two 16-feature halves exchanged: column (l & 31) holds feature (l & 31) ^ 16.
+__device__ __forceinline__ bf16x8 hb_tr_frag_swapped(const char* tile, int kk) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const int hq = (g & 1) ^ 1, p = i & 3, f = p >> 1;
+  bf16x8 out;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int c = 16 * kk + 8 * (g >> 1) + 4 * r + (i >> 2);
+    const char* a = tile + f * 1024 + hb_slot(c + 32 * hq, f) * 16 + (p & 1) * 8;
+    const hb_v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) hb_v4i16*)a);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[4 * r + e] = __builtin_bit_cast(__bf16, (short)v[e]);
+  }
+  return out;
+}
+
 // s_waitcnt vmcnt(VM) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14;
 // expcnt left at its maximum).
 template <int VM>
@@ -140,11 +170,37 @@ __device__ __forceinline__ void hb_wait_vm_lgkm0() {
 }
 
 // One 32-sample block from its LDS slot: the chain (dz_{l-1} stored), then the dW / db accumulation.
-__device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, int64_t b, const bf16x8 (&wt)[2][16],
-                                         f32x16 (&dw)[2][8], float (&db)[2]) {
+// Sigma's weight-gradient row of one block (LB, see hb_block): S7 tiles 2w, 2w + 1 (transposed
+// reads, k = samples) against the sigma tile read plainly (sigma in column 0) and with its halves
+// exchanged (column 16), into one accumulator.
+__device__ __forceinline__ void hb_sigma_dw(const char* dzb, const char* sb, f32x16& sacc) {
+  const int wave = threadIdx.x >> 6;
+  const char* st = dzb + 8 * HB_TILE;
+  __builtin_amdgcn_sched_barrier(0);  // its operands are not read ahead into the previous phase (registers)
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hb_tr_frag(sb + (2 * wave) * HB_TILE, kk), hb_tr_frag(st, kk), sacc,
+                                                   0, 0, 0);
+    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hb_tr_frag(sb + (2 * wave + 1) * HB_TILE, kk),
+                                                   hb_tr_frag_swapped(st, kk), sacc, 0, 0, 0);
+  }
+}
+
+// LB: the [bottleneck | sigma] layer (Lb, den_render.hip's transposed layer j = 2): dz_b has a ninth
+// tile (staged after the 8 bottleneck tiles) whose stored position 0 is sigma's dz and the rest zero;
+// the chain takes its first fragment as a 17th k-step (W_b^T's sigma column; the rest of that k-step
+// and the 18th are zero padding).  Sigma's weight-gradient row would be a ninth row tile of 8 more
+// accumulator tiles; instead wave w computes the transposed products S7 tile^T x sigma tile for its
+// S7 tiles 2w, 2w + 1 into one shared accumulator: the sigma tile read plainly puts sigma in column 0,
+// read with its halves exchanged in column 16, so tile 2w lands in column 0 and tile 2w + 1 in 16.
+template <bool LB>
+__device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, int64_t b,
+                                         const bf16x8 (&wt)[2][LB ? 17 : 16], f32x16 (&dw)[2][8], float (&db)[2],
+                                         f32x16& sacc, float& sdb) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int DZ_BYTES = LB ? HB_BLOCK + HB_TILE : HB_BLOCK;
   const char* dzb = cur;
-  const char* sb = cur + HB_BLOCK;
+  const char* sb = cur + DZ_BYTES;
   // chain: both row tiles of this wave share each dz_l fragment (K = 256, 16 k-steps): one LDS read
   // feeds two independent MFMAs, and the reads run HB_PF k-steps ahead of their use (issued
   // one per k-step, the compiler waited out the LDS latency before every MFMA)
@@ -165,6 +221,12 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
       accs[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[1][k], cur, accs[1], 0, 0, 0);
     }
   }
+  if constexpr (LB) {
+    const bf16x8 bs = hb_frag(dzb + 8 * HB_TILE, 0);
+    accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[0][16], bs, accs[0], 0, 0, 0);
+    accs[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[1][16], bs, accs[1], 0, 0, 0);
+    sdb += lane < 32 ? (float)bs[0] : 0.0f;  // sigma's dz of sample lane (stored position 0)
+  }
   // then the activation derivative
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -179,7 +241,7 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     // dz_{l-1} tile: stored now, the weight-gradient MFMAs below cover its write latency
     bf16x8 of[2];
     acc_to_frags<1>(acc, of);
-    char* d = P.dz_out + (b * 8 + 2 * wave + t) * HB_TILE + lane * 16;
+    char* d = P.dz_out + (b * 8 + 2 * wave + t) * HB_TILE + lane * 16;  // dz_{l-1}: 8 tiles per block
 #if DEN_HB_NT
     __builtin_nontemporal_store(of[0], (bf16x8*)d);
     __builtin_nontemporal_store(of[1], (bf16x8*)(d + 1024));
@@ -210,6 +272,9 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
       db[1] += (float)a1[j];
     }
   }
+  // sigma's weight-gradient row last (placed between the chain and the epilogue or before the dW
+  // MFMAs its operands spill registers or it measured slower: r03)
+  if constexpr (LB) hb_sigma_dw(dzb, sb, sacc);
 #if DEN_HB_OVL == 2
   // one wave per SIMD issues in order: the epilogue's VALU (derivative, bf16 packing) only overlaps
   // the weight-gradient MFMAs if it is interleaved with them in the instruction stream
@@ -223,29 +288,43 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
 #endif
 }
 
+template <bool LB>
 __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P) {
   // HB_RING LDS slots of [dz_l block | S'_{l-1} block]; HB_DEPTH blocks in flight ahead of the one
   // being computed.  Each wave waits for its own part of block b+1 at the end of block b (vmcnt; the
   // younger prefetches and stores stay in flight), then the workgroup barrier publishes every part.
-  __shared__ __attribute__((aligned(16))) char lds[HB_RING * HB_SLOT];
+  constexpr int DZ_TILES = LB ? 9 : 8;           // dz_in tiles per wave block in HBM
+  constexpr int DZ_PIECES = 2 * DZ_TILES;         // KiB of them staged
+  constexpr int SLOT = DZ_PIECES * 1024 + HB_BLOCK;
+  constexpr int KST = LB ? 17 : 16;              // chain k-steps
+  constexpr int ROW_BYTES = (LB ? 288 : 256) * 64;  // packed W^T row tile (chunk_bytes_K(bwd_K))
+  constexpr int MTA = LB ? 9 : 8;                // partial row tiles
+  constexpr int DMA_OPS = (DZ_PIECES + HB_WAVES - 1) / HB_WAVES + HB_BLOCK / 1024 / HB_WAVES;  // per wave per block
+  // vector-memory ops a wave issues after its DMA of block b+1 by the end of block b (issue order:
+  // stores(b-2), DMA(b+2), stores(b-1), DMA(b+3), stores(b)); the asm DMAs clobber "memory", so the
+  // stores keep their program order around them
+  constexpr int YOUNGER = HB_STORE_OPS + (HB_DEPTH - 1) * (DMA_OPS + HB_STORE_OPS);
+  static_assert(HB_RING * SLOT <= 160 * 1024, "hidden ring exceeds the LDS");
+  __shared__ __attribute__((aligned(16))) char lds[HB_RING * SLOT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t b0 = (int64_t)blockIdx.x * P.per_wg;
   const int64_t b1 = b0 + P.per_wg < P.n_blocks ? b0 + P.per_wg : P.n_blocks;
   auto fetch = [&](int64_t b, char* dst) {
-    hb_dma_untracked(P.dz_in + b * HB_BLOCK, dst);
-    hb_dma_untracked(P.s_in + b * HB_BLOCK, dst + HB_BLOCK);
+    if constexpr (LB) hb_dma_untracked_n<DZ_PIECES>(P.dz_in + b * DZ_TILES * HB_TILE, dst);
+    else hb_dma_untracked(P.dz_in + b * HB_BLOCK, dst);
+    hb_dma_untracked(P.s_in + b * HB_BLOCK, dst + DZ_PIECES * 1024);
   };
 #pragma unroll
   for (int u = 0; u < HB_DEPTH; ++u)
-    if (b0 + u < b1) fetch(b0 + u, lds + u * HB_SLOT);
+    if (b0 + u < b1) fetch(b0 + u, lds + u * SLOT);
 
   // W_l^T row tiles 2w, 2w+1: packed [row tile][kappa][lane][8] = the chain's A fragments
-  bf16x8 wt[2][16];
+  bf16x8 wt[2][KST];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-      wt[t][k] = *(const bf16x8*)(P.w + (int64_t)(2 * wave + t) * 16384 + k * 1024 + lane * 16);
+    for (int k = 0; k < KST; ++k)
+      wt[t][k] = *(const bf16x8*)(P.w + (int64_t)(2 * wave + t) * ROW_BYTES + k * 1024 + lane * 16);
   f32x16 dw[2][8];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -254,6 +333,10 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dw[t][n][r] = 0.0f;
   float db[2] = {0.0f, 0.0f};  // bias partial: feature (lane & 31) of row tile 2w + t, this lane's samples
+  f32x16 sacc;  // LB: sigma's weight-gradient row, S7 tile 2w in column 0, 2w + 1 in column 16
+#pragma unroll
+  for (int r = 0; r < 16; ++r) sacc[r] = 0.0f;
+  float sdb = 0.0f;  // LB: sigma's bias gradient (lanes 0..31)
   hb_wait_vm_lgkm0<0>();       // block b0 (and the prologue prefetches) landed
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -262,9 +345,9 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   for (int64_t b = b0; b < b1; ++b) {
     const int u = (int)((b - b0) % HB_RING);
     // prefetch block b + HB_DEPTH into the slot block b - 1 used (free since the last barrier)
-    if (b + HB_DEPTH < b1) fetch(b + HB_DEPTH, lds + ((u + HB_DEPTH) % HB_RING) * HB_SLOT);
-    hb_block(P, lds + u * HB_SLOT, b, wt, dw, db);
-    if (b + HB_DEPTH < b1) hb_wait_vm_lgkm0<HB_YOUNGER>();
+    if (b + HB_DEPTH < b1) fetch(b + HB_DEPTH, lds + ((u + HB_DEPTH) % HB_RING) * SLOT);
+    hb_block<LB>(P, lds + u * SLOT, b, wt, dw, db, sacc, sdb);
+    if (b + HB_DEPTH < b1) hb_wait_vm_lgkm0<YOUNGER>();
     else hb_wait_vm_lgkm0<0>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -278,15 +361,45 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
     const float bsum = db[t] + __shfl_xor(db[t], 32, 64);
     if (lane < 32) {
       const int m = lane;
-      float* o = P.partial + (((int64_t)blockIdx.x * 8 + 2 * wave + t) * 9 + 8) * 1024;
+      float* o = P.partial + (((int64_t)blockIdx.x * MTA + 2 * wave + t) * 9 + 8) * 1024;
       o[(32 * ((m >> 2) & 1)) * 16 + (m & 3) + 4 * (m >> 3)] = bsum;
+    }
+  }
+  if constexpr (LB) {
+    // row tile 8 = [sigma, 31 padding rows]: sigma is accumulator row 0 (lanes 0..31, register 0),
+    // column 32 n + lane; every other element of the tiles written as zero.  S7 feature q of tile
+    // 2w + nn sits in sacc's column 16 nn, row q = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn) {
+      const int q = lane & 31, rsel = (q & 3) + 4 * (q >> 3), src = 16 * nn + 32 * ((q >> 2) & 1);
+      float v = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float x = __shfl(sacc[r], src, 64);
+        v = r == rsel ? x : v;
+      }
+      float* o = P.partial + (((int64_t)blockIdx.x * MTA + 8) * 9 + 2 * wave + nn) * 1024 + lane * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4 z = {q == 0 && lane < 32 ? v : 0.0f, 0.0f, 0.0f, 0.0f};
+        *(f32x4*)(o + 4 * q) = z;
+      }
+    }
+    const float bs = wave_sum(sdb);
+    if (wave == 0) {
+      float* o = P.partial + (((int64_t)blockIdx.x * MTA + 8) * 9 + 8) * 1024 + lane * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4 z = {q == 0 && lane == 0 ? bs : 0.0f, 0.0f, 0.0f, 0.0f};
+        *(f32x4*)(o + 4 * q) = z;
+      }
     }
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
-      float* o = P.partial + (((int64_t)blockIdx.x * 8 + 2 * wave + t) * 9 + n) * 1024 + lane * 16;
+      float* o = P.partial + (((int64_t)blockIdx.x * MTA + 2 * wave + t) * 9 + n) * 1024 + lane * 16;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         f32x4 v = {dw[t][n][4 * q], dw[t][n][4 * q + 1], dw[t][n][4 * q + 2], dw[t][n][4 * q + 3]};
@@ -294,5 +407,8 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
       }
     }
 }
+
+template __global__ void hidden_bwd_kernel<false>(HiddenArgs);
+template __global__ void hidden_bwd_kernel<true>(HiddenArgs);
 
 }  // namespace den

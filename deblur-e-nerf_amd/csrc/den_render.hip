@@ -817,7 +817,8 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
 }
 
 // LAST_J = NBL - 1: the whole chain (F32 parity mode).  LAST_J = 2: stop after Lb^T (writes
-// dz_7); the hidden layers then run layer-major in den_hidden.hip (BF16 mode).
+// dz_7); the hidden layers then run layer-major in den_hidden.hip (BF16 mode).  LAST_J = 1: stop
+// after Lg^T (writes dz_b with the sigma tile; Lb^T runs layer-major too, DEN_LB_HIDDEN).
 template <int MODE, int LAST_J>
 __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) {
   using T = Tr<MODE>;
@@ -983,7 +984,8 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
     }
   }
   // j=2 Lb^T: dz_b (K = fwd_M(Lb)) -> dS7 * softplus'(S7) -> DZ7
-  bwd_layer_run<MODE, LAST_J, 2, fwd_M(MODE, L_B) / T::KI, 0>(A, lds, sample, xb, xa, A_S0 + 7, D_Z0 + 7);
+  if constexpr (LAST_J >= 2)
+    bwd_layer_run<MODE, LAST_J, 2, fwd_M(MODE, L_B) / T::KI, 0>(A, lds, sample, xb, xa, A_S0 + 7, D_Z0 + 7);
   if constexpr (LAST_J > 2) {
     // j=3.. L7^T..L1^T
     bwd_layer_run<MODE, LAST_J, 3, KS, 0>(A, lds, sample, xa, xb, A_S0 + 6, D_Z0 + 6);
