@@ -118,15 +118,16 @@ PHASE_REPS = 3
 #   render_fwd : the forward MLP, 2 x 593,152 MAC
 #   render_bwd : compositing adjoint + the head chain Lr^T (rd x 128), Lg^T (128 x 256, bottleneck
 #                part only): dX only
-#   hidden_bwd : 8 launches: Lb (dX 257 x 256 + dW 257 x 256) and L7..L1 (each dX 256 x 256 + dW
-#                256 x 256) MACs
+#   hidden_bwd : 7 launches (L7..L1), each dX (256 x 256) + dW (256 x 256) MACs
+#   hidden_bwd_lb : 1 launch (Lb), dX (256 x 257) + dW (257 x 256) MACs
 #   dw_gemm    : the weight gradients of L0 (256 x 63), L5's pe columns (256 x 63), Lg (128 x 283),
 #                Lr (rd x 128)
 # FLOP = 2 x MAC.  Per launch = per step / launches per step.
 def flop_per_sample(rd):
     return {"render_fwd_kernel": 2.0 * MAC_PER_SAMPLE[rd],
             "render_bwd_kernel": 2.0 * (rd * 128 + 128 * 256),
-            "hidden_bwd_kernel": 2.0 * (7 * 2 * 256 * 256 + 2 * 257 * 256),
+            "hidden_bwd_kernel": 2.0 * 7 * 2 * 256 * 256,
+            "hidden_bwd_lb_kernel": 2.0 * 2 * 257 * 256,
             "dw_gemm_kernel": 2.0 * (256 * 63 * 2 + 128 * 283 + rd * 128)}
 
 
@@ -136,7 +137,7 @@ def flop_per_sample(rd):
 # the backward; render_bwd: the record + G + the head activations read, dz_r, dz_g, dz_b written.
 # dw_gemm_kernel (the streamed weight-gradient kernels, den_dwstream.hip): dz_0 + dz_5 + pe,
 # dz_g + bottleneck + ve, dz_r + g = 1152 + 832 + 320 B per sample
-BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536 + 1538, "render_fwd_kernel": 5072, "render_bwd_kernel": 1168,
+BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "hidden_bwd_lb_kernel": 1538, "render_fwd_kernel": 5072, "render_bwd_kernel": 1168,
                     "dw_gemm_kernel": 2304}
 
 

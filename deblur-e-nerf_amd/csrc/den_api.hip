@@ -46,7 +46,7 @@ int fail(int code, const std::string& msg) {
 
 // ---- kernel timing (measurement only; bench.py).  When enabled, each render-path launch is
 // bracketed by a pair of hipEvents recorded on the launch stream itself.
-enum { T_RENDER_FWD = 0, T_RENDER_BWD = 1, T_HIDDEN_BWD = 2, T_DW_GEMM = 3, T_DW_REDUCE = 4, T_NCLASS = 5 };
+enum { T_RENDER_FWD = 0, T_RENDER_BWD = 1, T_HIDDEN_BWD = 2, T_DW_GEMM = 3, T_DW_REDUCE = 4, T_HIDDEN_LB = 5, T_NCLASS = 6 };
 struct TimingRec {
   int cls;
   hipEvent_t a, b;
@@ -110,6 +110,8 @@ WsLayout ws_layout(const den_render_desc* d) {
     // layer-major BF16 backward: dz_l (l = 0..6) is written in place over S_l, which the hidden
     // launch of layer l + 1 reads for the last time in the same pass (per 32-sample block, into
     // LDS before the block's dz_l leaves): 6.4 KB of workspace per sample instead of 10 KB
+    // (r03: separate dz buffers measured 0.1-0.5 ms per step faster, within noise: not worth 3.6 KB
+    // per sample)
     if (use_hidden_path(d) && a >= D_Z0 && a <= D_Z0 + 6) {
       L.act[a] = L.act[A_S0 + (a - D_Z0)];
       continue;
@@ -300,7 +302,7 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   const int64_t grid = hidden_grid(n);
   H.per_wg = (H.n_blocks + grid - 1) / grid;
   {
-    DEN_TIMED(T_HIDDEN_BWD, s);
+    TimedLaunch timed_(lb ? T_HIDDEN_LB : T_HIDDEN_BWD, s);
     if (lb)
       hipLaunchKernelGGL(hidden_bwd_kernel<true>, dim3((unsigned)grid), dim3(HB_THREADS), 0, s, H);
     else

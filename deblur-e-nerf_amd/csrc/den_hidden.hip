@@ -307,8 +307,11 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   static_assert(HB_RING * SLOT <= 160 * 1024, "hidden ring exceeds the LDS");
   __shared__ __attribute__((aligned(16))) char lds[HB_RING * SLOT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // a contiguous range of P.per_wg blocks per workgroup (r03: strided by the grid, so that all
+  // workgroups sweep one address window, measured the same)
   const int64_t b0 = (int64_t)blockIdx.x * P.per_wg;
-  const int64_t b1 = b0 + P.per_wg < P.n_blocks ? b0 + P.per_wg : P.n_blocks;
+  const int64_t n_it = b0 < P.n_blocks ? (b0 + P.per_wg < P.n_blocks ? P.per_wg : P.n_blocks - b0) : 0;
+  auto blk = [&](int64_t it) { return b0 + it; };
   auto fetch = [&](int64_t b, char* dst) {
     if constexpr (LB) hb_dma_untracked_n<DZ_PIECES>(P.dz_in + b * DZ_TILES * HB_TILE, dst);
     else hb_dma_untracked(P.dz_in + b * HB_BLOCK, dst);
@@ -316,7 +319,7 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   };
 #pragma unroll
   for (int u = 0; u < HB_DEPTH; ++u)
-    if (b0 + u < b1) fetch(b0 + u, lds + u * SLOT);
+    if (u < n_it) fetch(blk(u), lds + u * SLOT);
 
   // W_l^T row tiles 2w, 2w+1: packed [row tile][kappa][lane][8] = the chain's A fragments
   bf16x8 wt[2][KST];
@@ -342,12 +345,12 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  for (int64_t b = b0; b < b1; ++b) {
-    const int u = (int)((b - b0) % HB_RING);
-    // prefetch block b + HB_DEPTH into the slot block b - 1 used (free since the last barrier)
-    if (b + HB_DEPTH < b1) fetch(b + HB_DEPTH, lds + ((u + HB_DEPTH) % HB_RING) * SLOT);
-    hb_block<LB>(P, lds + u * SLOT, b, wt, dw, db, sacc, sdb);
-    if (b + HB_DEPTH < b1) hb_wait_vm_lgkm0<YOUNGER>();
+  for (int64_t it = 0; it < n_it; ++it) {
+    const int u = (int)(it % HB_RING);
+    // prefetch block it + HB_DEPTH into the slot block it - 1 used (free since the last barrier)
+    if (it + HB_DEPTH < n_it) fetch(blk(it + HB_DEPTH), lds + ((u + HB_DEPTH) % HB_RING) * SLOT);
+    hb_block<LB>(P, lds + u * SLOT, blk(it), wt, dw, db, sacc, sdb);
+    if (it + HB_DEPTH < n_it) hb_wait_vm_lgkm0<YOUNGER>();
     else hb_wait_vm_lgkm0<0>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();

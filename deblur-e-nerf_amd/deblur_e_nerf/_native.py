@@ -163,7 +163,7 @@ def exported_symbols():
 
 
 TIMING_CLASSES = ("render_fwd_kernel", "render_bwd_kernel", "hidden_bwd_kernel", "dw_gemm_kernel",
-                  "dw_reduce_kernel")
+                  "dw_reduce_kernel", "hidden_bwd_lb_kernel")
 
 
 def timing_enable(on=True):
