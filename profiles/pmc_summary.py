@@ -20,6 +20,8 @@ KERNELS = ("render_fwd_kernel", "render_bwd_kernel", "hidden_bwd_kernel", "dwstr
 
 
 def short(name):
+    if "hidden_bwd_kernel<true>" in name:  # the Lb launch (den_hidden.hip, LB = true)
+        return "hidden_bwd_lb_kernel"
     for k in KERNELS:
         if k in name:
             return k
@@ -49,15 +51,15 @@ def per_launch_all(path):
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
-def mfma_summary(out_dir, tag, n_simd=1024):
+def mfma_summary(out_dir, tag, n_simd=1024, prefix=""):
     """MFMA utilisation and stall breakdown per kernel from the two SQ passes of
     profiles/gpu_r02a.sh.  Calibration: SQ_VALU_MFMA_BUSY_CYCLES = 32 x SQ_INSTS_MFMA for
     v_mfma_f32_32x32x16_bf16 (MI355X_MICROARCH.md), summed over the SIMDs; GRBM_GUI_ACTIVE is the
     sum over the 8 XCDs, so the kernel's clock cycles are GRBM_GUI_ACTIVE / 8; utilisation =
     MFMA busy / (1024 SIMDs x kernel cycles).  SQ_WAVE_CYCLES and the SQ_WAIT_* / SQ_ACTIVE_*
     counters are in the same (quad-cycle) unit, so their ratios are wave-time fractions."""
-    a = per_launch_all(os.path.join(out_dir, "pmc_mfma", "run_counter_collection.csv"))
-    b = per_launch_all(os.path.join(out_dir, "pmc_mfma2", "run_counter_collection.csv"))
+    a = per_launch_all(os.path.join(out_dir, prefix + "pmc_mfma", "run_counter_collection.csv"))
+    b = per_launch_all(os.path.join(out_dir, prefix + "pmc_mfma2", "run_counter_collection.csv"))
     res = {}
     for k in a:
         c = dict(a[k])
@@ -74,7 +76,8 @@ def mfma_summary(out_dir, tag, n_simd=1024):
                   "wave_frac_wait_inst_lds": round(c["SQ_WAIT_INST_LDS"] / wave, 4),
                   "lds_bank_conflict_frac": round(c["SQ_LDS_BANK_CONFLICT"] / max(c.get("SQ_LDS_IDX_ACTIVE", 1), 1), 4),
                   "valu_mfma_coexec_frac": round(c.get("SQ_VALU_MFMA_COEXEC_CYCLES", 0) / max(
-                      c["SQ_VALU_MFMA_BUSY_CYCLES"], 1), 4)}
+                      c["SQ_VALU_MFMA_BUSY_CYCLES"], 1), 4),
+                  "valu_insts_per_mfma": round(c.get("SQ_INSTS_VALU", 0) / max(c.get("SQ_INSTS_MFMA", 1), 1), 2)}
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), f"{tag}_pmc_mfma.json"), "w") as f:
         json.dump({"source": f"rocprofv3 --pmc, two SQ passes ({tag}); see pmc_summary.mfma_summary",
                    "command": "bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak", "kernels": res}, f,
@@ -94,7 +97,7 @@ def main(out_dir, tag, prefix=""):
                    "hbm_bytes_per_launch": rd + wr}
     res = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes ({tag}); "
                      "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes",
-           "command": f"bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak ({'profiles/gpu_r03c.sh' if prefix else 'profiles/gpu_r02a.sh'})",
+           "command": f"bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-gemm-peak ({f'profiles/gpu_{prefix[:-1]}.sh' if prefix else 'profiles/gpu_r02a.sh'})",
            "workload": {"rays": 131072, "samples": 128, "mode": "bf16", "rd": 1},
            "kernels": kern}
     with open(os.path.join(here, "pmc_traffic.json"), "w") as f:
@@ -105,7 +108,7 @@ def main(out_dir, tag, prefix=""):
             rows.append(r)
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
              "Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python bench.py --steps 5 --warmup 2 "
-             "--no-cpu-baseline --no-gemm-peak` (" + ("profiles/gpu_r03c.sh" if prefix else "profiles/gpu_r02a.sh, gpu_r02g.sh")
+             "--no-cpu-baseline --no-gemm-peak` (" + (f"profiles/gpu_{prefix[:-1]}.sh" if prefix else "profiles/gpu_r02a.sh, gpu_r02g.sh")
              + "); 7 train steps + 3 phase-timing reps per kernel.", "",
              "| kernel | calls | avg ms | total % |", "|---|---|---|---|"]
     for r in rows[:20]:
@@ -116,16 +119,17 @@ def main(out_dir, tag, prefix=""):
     for k, v in kern.items():
         lines.append(f"| `{k}` | {v['hbm_read_bytes_per_launch'] / 1e9:.2f} | "
                      f"{v['hbm_write_bytes_per_launch'] / 1e9:.2f} | {v['hbm_bytes_per_launch'] / 1e9:.2f} |")
-    if not prefix and os.path.exists(os.path.join(out_dir, "pmc_mfma", "run_counter_collection.csv")):
-        mf = mfma_summary(out_dir, tag)
+    if os.path.exists(os.path.join(out_dir, prefix + "pmc_mfma", "run_counter_collection.csv")):
+        mf = mfma_summary(out_dir, tag, prefix=prefix)
         lines += ["", f"MFMA utilisation and wave-time breakdown (separate SQ passes, profiles/{tag}_pmc_mfma.json):",
                   "", "| kernel | MFMA util | wait (waitcnt/barrier) | issue stall | active | LDS-issue stall | "
-                  "LDS bank-conflict share | VALU-MFMA co-exec / MFMA busy |", "|---|---|---|---|---|---|---|---|"]
+                  "LDS bank-conflict share | VALU-MFMA co-exec / MFMA busy | VALU insts / MFMA |",
+                  "|---|---|---|---|---|---|---|---|---|"]
         for k, v in mf.items():
             lines.append(f"| `{k}` | {v['mfma_util']:.3f} | {v['wave_frac_wait_any']:.2f} | "
                          f"{v['wave_frac_wait_inst_any']:.2f} | {v['wave_frac_active_inst_any']:.2f} | "
                          f"{v['wave_frac_wait_inst_lds']:.3f} | {v['lds_bank_conflict_frac']:.2f} | "
-                         f"{v['valu_mfma_coexec_frac']:.2f} |")
+                         f"{v['valu_mfma_coexec_frac']:.2f} | {v['valu_insts_per_mfma']:.2f} |")
     with open(os.path.join(here, f"{tag}_kernel_stats.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print(json.dumps(kern, indent=1))
