@@ -233,7 +233,7 @@ int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, 
 }
 
 // One streamed weight-gradient launch (den_dwstream.hip) over the whole sample range.
-template <int MA, int MT, int NB, int NT, int NW, int DEPTH>
+template <int MA, int MT, int NB, int NT, int NW, int DEPTH, int U = 1>
 int launch_dwstream(const den_render_desc* d, const WsLayout& L, char* ws, int a0, int a1, int b0, int b1,
                     hipStream_t s) {
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
@@ -247,12 +247,13 @@ int launch_dwstream(const den_render_desc* d, const WsLayout& L, char* ws, int a
   P.b[1] = b1 >= 0 ? ws + L.act[b1] : nullptr;
   P.b_tiles[1] = b1 >= 0 ? act_width(DEN_MODE_BF16, b1) / 32 : 0;
   P.partial = (float*)(ws + L.dw_partial);
-  P.n_blocks = n / 32;
+  static_assert(U == 1 || U == 2 || U == 4 || U == 8, "U divides the wave blocks (n is a multiple of 256)");
+  P.n_blocks = n / 32 / U;
   const int64_t grid = hidden_grid(n);
   P.per_wg = (P.n_blocks + grid - 1) / grid;
   {
     DEN_TIMED(T_DW_GEMM, s);
-    hipLaunchKernelGGL((dwstream_kernel<MA, MT, NB, NT, NW, DEPTH>), dim3((unsigned)grid), dim3(64 * NW), 0, s, P);
+    hipLaunchKernelGGL((dwstream_kernel<MA, MT, NB, NT, NW, DEPTH, U>), dim3((unsigned)grid), dim3(64 * NW), 0, s, P);
   }
   DEN_LAUNCHED();
   return DEN_OK;
@@ -398,9 +399,9 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
       if ((rc = launch_dwstream<9, 9, 8, 8, DEN_DWS_NW2, 3>(d, L, ws, D_ZB, -1, A_S0 + 7, -1, s)) != DEN_OK) return rc;
       if ((rc = launch_dwstream_reduce(d, L, ws, 9, 8, 0, 9, L_B, 256, 0, 1, G, s)) != DEN_OK) return rc;
     }
-    if ((rc = launch_dwstream<4, 4, 8, 9, DEN_DWS_NW3, 4>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<4, 4, 8, 9, DEN_DWS_NW3, DEN_DWS_D3, DEN_DWS_U3>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 4, 9, 0, 4, L_G, 256, WIDTH, 1, G, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4, DEN_DWS_U4>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 1, 4, 0, 1, L_R, 128, 0, 1, G, s)) != DEN_OK) return rc;
     if (g->grad_bkgd) {
       hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(1024), 0, s, d->radiance_dim, d->n_rays,

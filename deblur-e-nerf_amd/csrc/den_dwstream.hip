@@ -32,7 +32,16 @@
 #define DEN_DWS_NW4 4
 #endif
 #ifndef DEN_DWS_D4
-#define DEN_DWS_D4 6  // blocks in flight of the Lr launch (10 KiB each)
+#define DEN_DWS_D4 3  // ring steps in flight of the Lr launch (U4 x 10 KiB each)
+#endif
+#ifndef DEN_DWS_U4
+#define DEN_DWS_U4 4  // wave blocks per ring step of the Lr launch (r03 A/B: U 1 -> 4 with U3 2: 7.6 -> 6.6 ms per step)
+#endif
+#ifndef DEN_DWS_D3
+#define DEN_DWS_D3 2  // ring steps in flight of the Lg launch (U3 x 26 KiB each)
+#endif
+#ifndef DEN_DWS_U3
+#define DEN_DWS_U3 2  // wave blocks per ring step of the Lg launch
 #endif
 
 namespace den {
@@ -57,12 +66,14 @@ __device__ __forceinline__ void dws_dma_piece(const char* tile_src, char* dst, i
                : "memory", "m0");
 }
 
-template <int MA, int MT, int NB, int NT, int NW, int DEPTH>
+// U: wave blocks per ring slot (one barrier per U blocks); P.n_blocks / P.per_wg count U-block steps
+template <int MA, int MT, int NB, int NT, int NW, int DEPTH, int U = 1>
 __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
   constexpr int TILES = MT + NT;
-  constexpr int SLOT = TILES * HB_TILE;
+  constexpr int BLK = TILES * HB_TILE;              // one wave block's tiles
+  constexpr int SLOT = U * BLK;
   constexpr int RING = DEPTH + 1;
-  constexpr int PIECES = 2 * TILES;                 // 1 KiB pieces per block
+  constexpr int PIECES = 2 * TILES * U;             // 1 KiB pieces per step
   constexpr int TPW = (MT * NT + NW - 1) / NW;      // output tiles per wave
   static_assert(RING * SLOT <= 160 * 1024, "ring exceeds the LDS");
   __shared__ __attribute__((aligned(16))) char lds[RING * SLOT];
@@ -75,12 +86,14 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
     for (int q = 0; q < (PIECES + NW - 1) / NW; ++q) {
       const int pc = __builtin_amdgcn_readfirstlane(q * NW + wave);
       if (pc < PIECES) {
-        const int t = pc >> 1, f = pc & 1;
+        const int ub = pc / (2 * TILES), tp = pc % (2 * TILES);
+        const int t = tp >> 1, f = tp & 1;
+        const int64_t wb = blk * U + ub;
         const char* src;
-        if (t < MA) src = P.a[0] + (blk * P.a_tiles[0] + t) * HB_TILE;
-        else if (t < MT) src = P.a[1] + (blk * P.a_tiles[1] + (t - MA)) * HB_TILE;
-        else if (t < MT + NB) src = P.b[0] + (blk * P.b_tiles[0] + (t - MT)) * HB_TILE;
-        else src = P.b[1] + (blk * P.b_tiles[1] + (t - MT - NB)) * HB_TILE;
+        if (t < MA) src = P.a[0] + (wb * P.a_tiles[0] + t) * HB_TILE;
+        else if (t < MT) src = P.a[1] + (wb * P.a_tiles[1] + (t - MA)) * HB_TILE;
+        else if (t < MT + NB) src = P.b[0] + (wb * P.b_tiles[0] + (t - MT)) * HB_TILE;
+        else src = P.b[1] + (wb * P.b_tiles[1] + (t - MT - NB)) * HB_TILE;
         dws_dma_piece(src, dst + pc * 1024, f);
       }
     }
@@ -109,7 +122,9 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
   for (int64_t blk = b0; blk < b1; ++blk) {
     const int u = (int)((blk - b0) % RING);
     if (blk + DEPTH < b1) fetch(blk + DEPTH, lds + ((u + DEPTH) % RING) * SLOT);
-    const char* cur = lds + u * SLOT;
+#pragma unroll
+    for (int ub = 0; ub < U; ++ub) {
+    const char* cur = lds + u * SLOT + ub * BLK;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
@@ -131,6 +146,7 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
           for (int e = 0; e < 8; ++e) db[j] += (float)a[e];
         }
       }
+    }
     }
     if (blk + DEPTH < b1) {
       if (extra) hb_wait_vm_lgkm0<(DEPTH - 1) * OPS_HI>();
@@ -176,7 +192,7 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
 // the four launches of a BF16 backward
 template __global__ void dwstream_kernel<8, 16, 2, 2, DEN_DWS_NW1, 3>(DwStreamArgs);  // L0 + L5 pe
 template __global__ void dwstream_kernel<9, 9, 8, 8, DEN_DWS_NW2, 3>(DwStreamArgs);    // Lb + sigma
-template __global__ void dwstream_kernel<4, 4, 8, 9, DEN_DWS_NW3, 4>(DwStreamArgs);    // Lg
-template __global__ void dwstream_kernel<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4>(DwStreamArgs);  // Lr
+template __global__ void dwstream_kernel<4, 4, 8, 9, DEN_DWS_NW3, DEN_DWS_D3, DEN_DWS_U3>(DwStreamArgs);    // Lg
+template __global__ void dwstream_kernel<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4, DEN_DWS_U4>(DwStreamArgs);  // Lr
 
 }  // namespace den
