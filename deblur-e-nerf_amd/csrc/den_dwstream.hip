@@ -3,7 +3,8 @@
 // over all ray samples, for the GEMMs the layer-major hidden backward (den_hidden.hip) does not
 // cover, fused by shared operand so that every operand byte is read from HBM once:
 //   {L0, L5's pe columns}  A = [dz_0 | dz_5] (16 row tiles), B = pe (2 column tiles)
-//   {Lb, sigma}            A = dz_b (9 row tiles: bottleneck + sigma), B = S'_7 (8 column tiles)
+//   {Lb, sigma}            A = dz_b (9 row tiles: bottleneck + sigma), B = S'_7 (8 column tiles) --
+//                          only in the DEN_LB_HIDDEN = 0 build (Lb runs layer-major in den_hidden.hip)
 //   Lg                     A = dz_g (4 row tiles), B = [bottleneck | ve] (9 column tiles)
 //   Lr                     A = dz_r (1 row tile),  B = g (4 column tiles)
 // Layout and machinery as den_hidden.hip: one persistent workgroup per CU sweeps a contiguous
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
   }
 }
 
-// the four launches of a BF16 backward
+// the launches of a BF16 backward (Lb + sigma: DEN_LB_HIDDEN = 0 only)
 template __global__ void dwstream_kernel<8, 16, 2, 2, DEN_DWS_NW1, 3>(DwStreamArgs);  // L0 + L5 pe
 template __global__ void dwstream_kernel<9, 9, 8, 8, DEN_DWS_NW2, 3>(DwStreamArgs);    // Lb + sigma
 template __global__ void dwstream_kernel<4, 4, 8, 9, DEN_DWS_NW3, DEN_DWS_D3, DEN_DWS_U3>(DwStreamArgs);    // Lg
