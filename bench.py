@@ -117,28 +117,27 @@ PHASE_REPS = 3
 # section 4), rd = 1 (rd = 3 adds 2 x 128 MACs to the forward and to the head backward).
 #   render_fwd : the forward MLP, 2 x 593,152 MAC
 #   render_bwd : compositing adjoint + the head chain Lr^T (rd x 128), Lg^T (128 x 256, bottleneck
-#                part only): dX only
+#                part only) + the fused Lr weight gradient (rd x 128)
 #   hidden_bwd : 7 launches (L7..L1), each dX (256 x 256) + dW (256 x 256) MACs
 #   hidden_bwd_lb : 1 launch (Lb), dX (256 x 257) + dW (257 x 256) MACs
-#   dw_gemm    : the weight gradients of L0 (256 x 63), L5's pe columns (256 x 63), Lg (128 x 283),
-#                Lr (rd x 128)
+#   dw_gemm    : the weight gradients of L0 (256 x 63), L5's pe columns (256 x 63), Lg (128 x 283)
 # FLOP = 2 x MAC.  Per launch = per step / launches per step.
 def flop_per_sample(rd):
     return {"render_fwd_kernel": 2.0 * MAC_PER_SAMPLE[rd],
-            "render_bwd_kernel": 2.0 * (rd * 128 + 128 * 256),
+            "render_bwd_kernel": 2.0 * (2 * rd * 128 + 128 * 256),
             "hidden_bwd_kernel": 2.0 * 7 * 2 * 256 * 256,
             "hidden_bwd_lb_kernel": 2.0 * 2 * 257 * 256,
-            "dw_gemm_kernel": 2.0 * (256 * 63 * 2 + 128 * 283 + rd * 128)}
+            "dw_gemm_kernel": 2.0 * (256 * 63 * 2 + 128 * 283)}
 
 
 # algorithmic HBM bytes per sample and STEP of each kernel class, BF16 layout:
 # hidden_bwd: L7..L1 each read dz_l + a_(l-1) and write dz_(l-1), 256 bf16 each = 1536 B; Lb reads
 # dz_b (257 bf16) + S7 and writes dz_7 = 1538 B; render_fwd: the activations + record it stores for
-# the backward; render_bwd: the record + G + the head activations read, dz_r, dz_g, dz_b written.
+# the backward; render_bwd: the record + G read, dz_g and dz_b written (16 + 256 + 256 + 576 B).
 # dw_gemm_kernel (the streamed weight-gradient kernels, den_dwstream.hip): dz_0 + dz_5 + pe,
-# dz_g + bottleneck + ve, dz_r + g = 1152 + 832 + 320 B per sample
-BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "hidden_bwd_lb_kernel": 1538, "render_fwd_kernel": 5072, "render_bwd_kernel": 1168,
-                    "dw_gemm_kernel": 2304}
+# dz_g + bottleneck + ve = 1152 + 832 B per sample
+BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "hidden_bwd_lb_kernel": 1538, "render_fwd_kernel": 5072,
+                    "render_bwd_kernel": 1104, "dw_gemm_kernel": 1984}
 
 
 def pmc_traffic(kernel, a):

@@ -87,7 +87,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct WsLayout {
   size_t act[NACT];
-  size_t rec, bkgd_partial, dw_partial, total;
+  size_t rec, bkgd_partial, dw_partial, lr_partial, lr_stage1, total;
   int splits;
   int64_t per_split;
 };
@@ -95,6 +95,7 @@ struct WsLayout {
 constexpr int64_t DW_BLOCK_MAX = 9LL * 11 * 1024;  // floats per split, bound over the shapes (L5: MT 8, NT+1 11; Lb: MT 9, NT+1 9)
 
 // persistent workgroups of the layer-major hidden backward: one per CU, at most one per wave block
+constexpr int LR_G1 = 1024;  // stage-1 rows of the fused Lr weight-gradient reduction (at most)
 inline int64_t hidden_grid(int64_t n_samples) { return std::min<int64_t>(HB_GRID_MAX, std::max<int64_t>(1, n_samples / 32)); }
 
 // BF16 backward: layer-major hidden layers (den_hidden.hip) unless the descriptor selects the
@@ -135,6 +136,15 @@ WsLayout ws_layout(const den_render_desc* d) {
   // weight gradients (den_dwstream.hip, at most 9 x 9 tiles per workgroup)
   const size_t hidden = (size_t)hidden_grid(n) * 9 * 9 * 1024;
   if (d->train) off += align256(std::max((size_t)splits * DW_BLOCK_MAX, hidden) * 4);
+  // fused Lr weight gradient (render_bwd_kernel<1, 1>): one LR_PART-float partial per render
+  // workgroup + the stage-1 rows of its reduction
+  L.lr_partial = off;
+  L.lr_stage1 = off;
+  if (d->train && use_hidden_path(d) && DEN_LR_FUSED) {
+    off += align256((size_t)(n / wg_samples(d->mode)) * LR_PART * 4);
+    L.lr_stage1 = off;
+    off += align256((size_t)LR_G1 * LR_PART * 4);
+  }
   L.total = off;
   return L;
 }
@@ -184,6 +194,7 @@ RenderArgs<MODE> make_args(const den_render_desc* d, const den_render_io* io, co
   for (int a = 0; a < NACT; ++a) A.act[a] = ws ? ws + L.act[a] : nullptr;
   A.rec = ws ? (float*)(ws + L.rec) : nullptr;
   A.bkgd_partial = ws ? (float*)(ws + L.bkgd_partial) : nullptr;
+  A.lr_partial = ws ? (float*)(ws + L.lr_partial) : nullptr;
   A.out_rgb = io->out_rgb;
   A.out_opacity = io->out_opacity;
   A.out_depth = io->out_depth;
@@ -287,6 +298,36 @@ int launch_dwstream_reduce(const den_render_desc* d, const WsLayout& L, char* ws
   return DEN_OK;
 }
 
+// Reduction of the fused Lr weight-gradient partials (render_bwd_kernel<1, 1>) into the gradient.
+int launch_lr_reduce(const den_render_desc* d, const WsLayout& L, char* ws, float* grad, hipStream_t s) {
+  const int64_t n_wg = (int64_t)d->n_rays * d->n_samples / wg_samples(DEN_MODE_BF16);
+  const int G1 = (int)std::min<int64_t>(LR_G1, n_wg);
+  DwReduceArgs R{};
+  R.MT = 1;
+  R.NT = 4;
+  R.m_off = 0;
+  R.layer = L_R;
+  R.mode = DEN_MODE_BF16;
+  R.rd = d->radiance_dim;
+  R.n1 = 128;
+  R.n1_feat = 0;
+  R.bias = 1;
+  R.grad = grad;
+  float* st1 = (float*)(ws + L.lr_stage1);
+  {
+    DEN_TIMED(T_DW_REDUCE, s);
+    hipLaunchKernelGGL(lr_reduce1_kernel, dim3((unsigned)G1), dim3(448), 0, s, (const float*)(ws + L.lr_partial), n_wg,
+                       G1, st1);
+  }
+  DEN_LAUNCHED();
+  {
+    DEN_TIMED(T_DW_REDUCE, s);
+    hipLaunchKernelGGL(lr_reduce2_kernel, dim3(LR_PART - 1), dim3(256), 0, s, (const float*)st1, G1, R);
+  }
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
 // Layer-major backward of hidden layer l (den_hidden.hip) + reduction of its weight/bias gradient;
 // l = 8 is the [bottleneck | sigma] layer Lb (input S7, dz_b with the sigma tile, 9 row tiles).
 int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLayout& L, char* ws, int l, float* grad,
@@ -376,6 +417,7 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
                              dim3(512), 0, s, A);
         }
         DEN_LAUNCHED();
+        if (DEN_LB_HIDDEN && DEN_LR_FUSED && (rc = launch_lr_reduce(d, L, ws, G, s)) != DEN_OK) return rc;
         for (int l = DEN_LB_HIDDEN ? 8 : 7; l >= 1; --l)
           if ((rc = launch_hidden(d, io, L, ws, l, G, s)) != DEN_OK) return rc;
       }
@@ -401,8 +443,11 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
     }
     if ((rc = launch_dwstream<4, 4, 8, 9, DEN_DWS_NW3, DEN_DWS_D3, DEN_DWS_U3>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 4, 9, 0, 4, L_G, 256, WIDTH, 1, G, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4, DEN_DWS_U4>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream_reduce(d, L, ws, 1, 4, 0, 1, L_R, 128, 0, 1, G, s)) != DEN_OK) return rc;
+    if (!(DEN_LB_HIDDEN && DEN_LR_FUSED)) {  // else inside render_bwd_kernel<1, 1>
+      if ((rc = launch_dwstream<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4, DEN_DWS_U4>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK)
+        return rc;
+      if ((rc = launch_dwstream_reduce(d, L, ws, 1, 4, 0, 1, L_R, 128, 0, 1, G, s)) != DEN_OK) return rc;
+    }
     if (g->grad_bkgd) {
       hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(1024), 0, s, d->radiance_dim, d->n_rays,
                          (const float*)(ws + L.bkgd_partial), g->grad_bkgd);

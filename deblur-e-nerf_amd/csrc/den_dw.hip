@@ -232,6 +232,8 @@ struct DwReduceArgs {
 // in a fixed order: deterministic.  (One thread per element walking all splits serially ran at
 // ~1 TB/s: 69 us per hidden layer of 256 x 288 KB partials.)
 constexpr int DWR_EL = 64, DWR_SG = 4, DWR_UNROLL = 16;
+// partial element e ([MT][NT + 1][64][16]: tile, lane, register) of sum s -> the flat gradient
+__device__ void dw_scatter(const DwReduceArgs& R, int64_t e, float s);
 constexpr int DWR_THREADS = DWR_EL * DWR_SG;
 
 __global__ __launch_bounds__(DWR_THREADS) void dw_reduce_kernel(DwReduceArgs R) {
@@ -263,6 +265,63 @@ __global__ __launch_bounds__(DWR_THREADS) void dw_reduce_kernel(DwReduceArgs R) 
   float s = red[0][el];
 #pragma unroll
   for (int q = 1; q < DWR_SG; ++q) s += red[q][el];
+  dw_scatter(R, e, s);
+}
+
+// Fused Lr weight gradient (render_bwd_kernel<1, 1>, den_render.hip): one LR_PART-float partial per
+// render workgroup, [tile t][ch][32 columns] + bias[ch] + pad.  Stage 1: workgroup y sums partials
+// y, y + G1, ... (one thread per element, eight loads in flight, fixed order); stage 2 sums the G1
+// stage-1 rows in order and scatters like dw_reduce_kernel (MT 1, NT 4: element (t, ch, col) is
+// register ch of lane col in column tile t; bias ch is register ch of lane 0 in the ones tile).
+constexpr int LRP = 388;  // = LR_PART
+__global__ __launch_bounds__(448) void lr_reduce1_kernel(const float* part, int64_t n_wg, int G1, float* st1) {
+  const int e = threadIdx.x;
+  if (e >= LRP) return;
+  float acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = 0.0f;
+  int64_t sp = blockIdx.x;
+  for (; sp + 7LL * G1 < n_wg; sp += 8LL * G1) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += part[(sp + (int64_t)u * G1) * LRP + e];
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (sp + (int64_t)u * G1 < n_wg) acc[u] += part[(sp + (int64_t)u * G1) * LRP + e];
+  float v = acc[0];
+#pragma unroll
+  for (int u = 1; u < 8; ++u) v += acc[u];
+  st1[(int64_t)blockIdx.x * LRP + e] = v;
+}
+
+// stage 2: workgroup e (one per element): thread t sums rows t, t + 256, ... then a fixed-order tree
+__global__ __launch_bounds__(256) void lr_reduce2_kernel(const float* st1, int G1, DwReduceArgs R) {
+  const int e = blockIdx.x, t = threadIdx.x;
+  float v = 0.0f;
+  for (int y = t; y < G1; y += 256) v += st1[(int64_t)y * LRP + e];
+  __shared__ float red[256];
+  red[t] = v;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  if (t != 0) return;
+  v = red[0];
+  int nt, lane, reg;
+  if (e < 384) {
+    nt = e / 96;
+    reg = (e % 96) / 32;
+    lane = e % 32;
+  } else {
+    nt = 4;
+    reg = e - 384;
+    lane = 0;
+  }
+  dw_scatter(R, ((int64_t)nt << 10) + lane * 16 + reg, v);
+}
+
+__device__ void dw_scatter(const DwReduceArgs& R, int64_t e, float s) {
   const int reg = (int)(e & 15), lane = (int)((e >> 4) & 63);
   const int64_t tile = e >> 10;
   const int nt = (int)(tile % (R.NT + 1)), mt = (int)(tile / (R.NT + 1));

@@ -19,6 +19,9 @@
 namespace den {
 
 constexpr int LDS_BUF = CHUNK_MAX;  // bytes per ring slot
+#ifndef DEN_LR_FUSED
+#define DEN_LR_FUSED 1  // BF16 layer-major path: the Lr weight gradient inside render_bwd_kernel<1, 1>
+#endif
 
 template <int MODE>
 struct RenderArgs {
@@ -50,6 +53,7 @@ struct RenderArgs {
   const float* d_opacity;
   const float* d_depth;
   float* bkgd_partial;    // [4][n_rays]
+  float* lr_partial;      // [workgroup][LR_PART]: the fused Lr weight gradient (render_bwd_kernel, LAST_J = 1)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -777,9 +781,13 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
 // DER: 0 = softplus(100) derivative from stored output, 1 = identity.
 // The stored activation of tile i is loaded before tile i's MFMA chain and
 // consumed by its epilogue one tile later (software pipeline, as forward).
-template <int MODE, int LAST_J, int J, int KS, int DER, typename Frag>
+struct NoTileHook {
+  template <typename Acc>
+  __device__ __forceinline__ void operator()(int, const Acc&) const {}
+};
+template <int MODE, int LAST_J, int J, int KS, int DER, typename Frag, typename Hook = NoTileHook>
 __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* lds, int64_t sample, const Frag* x,
-                                              Frag* xo, int SA, int DZ) {
+                                              Frag* xo, int SA, int DZ, Hook&& hook = Hook{}) {
   using T = Tr<MODE>;
   using Acc = typename T::Acc;
   constexpr int NT = bwd_tiles(MODE, J);
@@ -787,7 +795,9 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
   int cb = 0;
   for (int jj = 0; jj < J; ++jj) cb += bwd_tiles(MODE, jj);
   Acc prev, s_prev, s_cur;
+  // hook(i, stored activation of tile i): run in tile i's epilogue, when the load has landed
   auto epilogue = [&](Acc& acc, const Acc& sv, int i) {
+    if constexpr (DER == 0) hook(i, sv);
     if constexpr (DER == 0) {
 #pragma unroll
       for (int r = 0; r < T::REGS; ++r) acc[r] = acc[r] * hidden_dact<MODE>(sv[r]);
@@ -819,6 +829,16 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
 // LAST_J = NBL - 1: the whole chain (F32 parity mode).  LAST_J = 2: stop after Lb^T (writes
 // dz_7); the hidden layers then run layer-major in den_hidden.hip (BF16 mode).  LAST_J = 1: stop
 // after Lg^T (writes dz_b with the sigma tile; Lb^T runs layer-major too, DEN_LB_HIDDEN).
+// Fused Lr weight gradient (BF16, LAST_J = 1): dW_r = dz_r^T G over the workgroup's samples by MFMA
+// (k = samples, both operands by transposed LDS reads as in den_hidden.hip), instead of a streamed
+// launch that re-reads G and dz_r.  Per wave an LDS scratch holds a dz_r tile replicated at stored
+// positions 8t + ch (ch < rd) and the current G tile; the A operand of G tile t keeps rows 8t.. only,
+// so the four tiles share one accumulator (row 8t + ch, column = G feature of tile t).  The eight
+// waves' accumulators are summed in LDS into one partial per workgroup, [tile t][ch][32] + bias[ch]
+// (lr_reduce*_kernel, den_dw.hip, reduce them in a fixed order).
+constexpr int LRW_SCR = 4096;  // bytes of LDS scratch per wave
+constexpr int LR_PART = 388;   // floats per workgroup partial: 4 x 3 x 32 + 3 bias + 1 pad
+
 template <int MODE, int LAST_J>
 __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) {
   using T = Tr<MODE>;
@@ -826,7 +846,8 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
   using Acc = typename T::Acc;
   constexpr int TM = T::TM, FPT = T::FPT, REGS = T::REGS;
   constexpr int WGS = wg_samples(MODE);
-  __shared__ __attribute__((aligned(16))) char lds[2 * LDS_BUF + WGS * 16];
+  constexpr bool FUSE_LR = MODE == 1 && LAST_J == 1 && DEN_LR_FUSED;
+  __shared__ __attribute__((aligned(16))) char lds[2 * LDS_BUF + WGS * 16 + (FUSE_LR ? 8 * LRW_SCR : 0)];
   float* rec_lds = (float*)(lds + 2 * LDS_BUF);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -962,15 +983,54 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
     if (A.rd > 2) dzr[2] = g4[3];
     dzs[0] = g4[0];
   }
-  store_tile_vals<MODE>(act_ptr(A, D_ZR, sample, 0), dzr);
-  if constexpr (DZR_W / TM > 1) store_tile_vals<MODE>(act_ptr(A, D_ZR, sample, 1), acc_zero<MODE>());
+  if constexpr (!FUSE_LR) {
+    store_tile_vals<MODE>(act_ptr(A, D_ZR, sample, 0), dzr);
+    if constexpr (DZR_W / TM > 1) store_tile_vals<MODE>(act_ptr(A, D_ZR, sample, 1), acc_zero<MODE>());
+  }
+  f32x16 lacc;  // FUSE_LR: the shared dW_r accumulator
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lacc[r] = 0.0f;
+  float ldb[3] = {0.f, 0.f, 0.f};
+  char* lscr = lds + 2 * LDS_BUF + WGS * 16 + wave * LRW_SCR;
+  if constexpr (FUSE_LR) {
+    // dz_r (bf16, as the stored D_ZR tile) of sample c at stored positions 8t + ch of every fragment
+    const __bf16 z0 = (__bf16)g4[1], z1 = A.rd > 1 ? (__bf16)g4[2] : (__bf16)0.0f,
+                 z2 = A.rd > 2 ? (__bf16)g4[3] : (__bf16)0.0f, zz = (__bf16)0.0f;
+    const bf16x8 v = {z0, z1, z2, zz, zz, zz, zz, zz};
+    *(bf16x8*)(lscr + hb_slot(lane, 0) * 16) = v;
+    *(bf16x8*)(lscr + 1024 + hb_slot(lane, 1) * 16) = v;
+    if (grp == 0) {
+      ldb[0] = (float)z0;
+      ldb[1] = (float)z1;
+      ldb[2] = (float)z2;
+    }
+  }
+  auto lr_hook = [&](int i, const Acc& sv) {
+    if constexpr (FUSE_LR) {
+      // G tile i (exactly its stored bf16: sv came from it) into the scratch, then
+      // lacc += [dz_r rows 8i..] x G_i over the wave's 32 samples (two k-steps of 16)
+      Frag gf[FPT];
+      acc_to_frags<MODE>(sv, gf);
+      char* gs = lscr + 2048;
+      *(bf16x8*)(gs + hb_slot(lane, 0) * 16) = gf[0];
+      *(bf16x8*)(gs + 1024 + hb_slot(lane, 1) * 16) = gf[1];
+      const bool keep = ((lane & 31) >> 3) == i;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 a = hb_tr_frag(lscr, kk);
+        const bf16x8 zero = {};
+        a = keep ? a : zero;
+        lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hb_tr_frag(gs, kk), lacc, 0, 0, 0);
+      }
+    }
+  };
 
   constexpr int KS = WIDTH / T::KI;
   Frag fr[FPT];
   acc_to_frags<MODE>(dzr, fr);
   Frag xa[KS + 2 * FPT], xb[KS + 2 * FPT];
-  // j=0 Lr^T: dz_r -> dG * softplus'(G) -> DZG (128 rows)
-  bwd_layer_run<MODE, LAST_J, 0, FPT, 0>(A, lds, sample, fr, xa, A_G, D_ZG);
+  // j=0 Lr^T: dz_r -> dG * softplus'(G) -> DZG (128 rows) [+ the fused Lr weight gradient]
+  bwd_layer_run<MODE, LAST_J, 0, FPT, 0>(A, lds, sample, fr, xa, A_G, D_ZG, lr_hook);
   // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles 0..
   bwd_layer_run<MODE, LAST_J, 1, WIDTH_COND / T::KI, 1>(A, lds, sample, xa, xb, 0, D_ZB);
   // sigma head row(s) of Lb as extra fake tile(s) appended to the DZB fragments
@@ -981,6 +1041,30 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
       Acc t = e == 0 ? dzs : acc_zero<MODE>();
       store_tile_vals<MODE>(act_ptr(A, D_ZB, sample, WIDTH / TM + e), t);
       if (WIDTH + e * TM < fwd_M(MODE, L_B)) acc_to_frags<MODE>(t, xb + KS + e * FPT);
+    }
+  }
+  if constexpr (FUSE_LR) {
+    // the eight waves' dW_r (rows 8t + ch = register 4t + ch of lanes 0..31) and bias into one
+    // partial, through the weight ring (idle: the last chunk_step issued no DMA and ended in a barrier)
+    float* red = (float*)lds;
+    if (lane < 32) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) red[wave * LR_PART + (t * 3 + ch) * 32 + lane] = lacc[4 * t + ch];
+    }
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float b = wave_sum(ldb[ch]);
+      if (lane == 0) red[wave * LR_PART + 384 + ch] = b;
+    }
+    if (lane == 0) red[wave * LR_PART + 387] = 0.0f;
+    __syncthreads();
+    for (int e = threadIdx.x; e < LR_PART; e += blockDim.x) {
+      float v = red[e];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) v += red[w * LR_PART + e];
+      A.lr_partial[(int64_t)blockIdx.x * LR_PART + e] = v;
     }
   }
   // j=2 Lb^T: dz_b (K = fwd_M(Lb)) -> dS7 * softplus'(S7) -> DZ7
