@@ -133,11 +133,12 @@ def flop_per_sample(rd):
 # algorithmic HBM bytes per sample and STEP of each kernel class, BF16 layout:
 # hidden_bwd: L7..L1 each read dz_l + a_(l-1) and write dz_(l-1), 256 bf16 each = 1536 B; Lb reads
 # dz_b (257 bf16) + S7 and writes dz_7 = 1538 B; render_fwd: the activations + record it stores for
-# the backward; render_bwd: the record + G read, dz_g and dz_b written (16 + 256 + 256 + 576 B).
+# the backward; render_bwd: the record + G read, dz_g and dz_b (256 bottleneck + sigma) written
+# (16 + 256 + 256 + 514 B).
 # dw_gemm_kernel (the streamed weight-gradient kernels, den_dwstream.hip): dz_0 + dz_5 + pe,
 # dz_g + bottleneck + ve = 1152 + 832 B per sample
 BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "hidden_bwd_lb_kernel": 1538, "render_fwd_kernel": 5072,
-                    "render_bwd_kernel": 1104, "dw_gemm_kernel": 1984}
+                    "render_bwd_kernel": 1042, "dw_gemm_kernel": 1984}
 
 
 def pmc_traffic(kernel, a):

@@ -25,6 +25,7 @@ constexpr int HB_WAVES = 4;
 constexpr int HB_THREADS = 64 * HB_WAVES;
 constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
 constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
+constexpr int HB_SIG = 256;            // LB: LDS bytes for sigma's bf16[32] dz of a block (aligned)
 #ifndef DEN_HB_GRID
 #define DEN_HB_GRID 256  // persistent workgroups (one per CU)
 #endif
@@ -104,22 +105,14 @@ __device__ __forceinline__ void hb_dma_untracked(const char* src, char* dst) {
   }
 }
 
-// The same for NP pieces of 1 KiB (NP not a multiple of the wave count: the last piece is fetched
-// again by the waves past it, so every wave issues ceil(NP / 4) DMA instructions -- a uniform count
-// for the counted vmcnt waits; the duplicates write the same bytes)
-template <int NP>
-__device__ __forceinline__ void hb_dma_untracked_n(const char* src, char* dst) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t off0 = (uint32_t)hb_slot(lane, 0) * 16, off1 = (uint32_t)hb_slot(lane, 1) * 16;
-#pragma unroll
-  for (int q = 0; q < (NP + HB_WAVES - 1) / HB_WAVES; ++q) {
-    const int pw = q * HB_WAVES + wave;
-    const int pc = __builtin_amdgcn_readfirstlane(pw < NP ? pw : NP - 1);
-    const char* base = src + pc * 1024;
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(dst + pc * 1024));
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"((pc & 1) ? off1 : off0),
-                 "s"(base), "s"(m0) : "memory", "m0");
-  }
+// LB: sigma's 32 bf16 dz of a wave block (64 B, render_bwd_kernel<1, 1>) into LDS, by lanes 0..3;
+// every wave issues it (the same bytes), so each wave's DMA count per block stays uniform
+__device__ __forceinline__ void hb_dma_sigma(const char* src, char* dst) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)dst);
+  if (lane < 4)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"((uint32_t)lane * 16),
+                 "s"(src), "s"(m0) : "memory", "m0");
 }
 
 // This lane's own fragment f of a tile in LDS (the chain's B operand / the stored activation).
@@ -145,22 +138,6 @@ __device__ __forceinline__ bf16x8 hb_tr_frag(const char* tile, int kk) {
   return out;
 }
 
-// hb_tr_frag with the two 16-feature halves exchanged: column (l & 31) holds feature (l & 31) ^ 16.
-__device__ __forceinline__ bf16x8 hb_tr_frag_swapped(const char* tile, int kk) {
-  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
-  const int hq = (g & 1) ^ 1, p = i & 3, f = p >> 1;
-  bf16x8 out;
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int c = 16 * kk + 8 * (g >> 1) + 4 * r + (i >> 2);
-    const char* a = tile + f * 1024 + hb_slot(c + 32 * hq, f) * 16 + (p & 1) * 8;
-    const hb_v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) hb_v4i16*)a);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) out[4 * r + e] = __builtin_bit_cast(__bf16, (short)v[e]);
-  }
-  return out;
-}
-
 // s_waitcnt vmcnt(VM) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14;
 // expcnt left at its maximum).
 template <int VM>
@@ -171,35 +148,37 @@ __device__ __forceinline__ void hb_wait_vm_lgkm0() {
 
 // One 32-sample block from its LDS slot: the chain (dz_{l-1} stored), then the dW / db accumulation.
 // Sigma's weight-gradient row of one block (LB, see hb_block): S7 tiles 2w, 2w + 1 (transposed
-// reads, k = samples) against the sigma tile read plainly (sigma in column 0) and with its halves
-// exchanged (column 16), into one accumulator.
-__device__ __forceinline__ void hb_sigma_dw(const char* dzb, const char* sb, f32x16& sacc) {
-  const int wave = threadIdx.x >> 6;
-  const char* st = dzb + 8 * HB_TILE;
+// reads, k = samples) against sigma's dz as the B operand of a tile whose only nonzero feature is
+// sigma -- in column 0 for tile 2w, column 16 for tile 2w + 1 -- into one accumulator.  Column
+// (lane & 31) of a B operand holds k-slots 8 (lane >> 5) + j = samples 16 kk + 8 (lane >> 5) + j:
+// eight consecutive entries of the block's sigma array.
+__device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, f32x16& sacc) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   __builtin_amdgcn_sched_barrier(0);  // its operands are not read ahead into the previous phase (registers)
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
-    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hb_tr_frag(sb + (2 * wave) * HB_TILE, kk), hb_tr_frag(st, kk), sacc,
-                                                   0, 0, 0);
-    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hb_tr_frag(sb + (2 * wave + 1) * HB_TILE, kk),
-                                                   hb_tr_frag_swapped(st, kk), sacc, 0, 0, 0);
+    const bf16x8 sv = *(const bf16x8*)(sig + 32 * kk + 16 * (lane >> 5)), zero = {};
+    const bf16x8 b0 = (lane & 31) == 0 ? sv : zero, b1 = (lane & 31) == 16 ? sv : zero;
+    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hb_tr_frag(sb + (2 * wave) * HB_TILE, kk), b0, sacc, 0, 0, 0);
+    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hb_tr_frag(sb + (2 * wave + 1) * HB_TILE, kk), b1, sacc, 0, 0, 0);
   }
 }
 
-// LB: the [bottleneck | sigma] layer (Lb, den_render.hip's transposed layer j = 2): dz_b has a ninth
-// tile (staged after the 8 bottleneck tiles) whose stored position 0 is sigma's dz and the rest zero;
-// the chain takes its first fragment as a 17th k-step (W_b^T's sigma column; the rest of that k-step
-// and the 18th are zero padding).  Sigma's weight-gradient row would be a ninth row tile of 8 more
-// accumulator tiles; instead wave w computes the transposed products S7 tile^T x sigma tile for its
-// S7 tiles 2w, 2w + 1 into one shared accumulator: the sigma tile read plainly puts sigma in column 0,
-// read with its halves exchanged in column 16, so tile 2w lands in column 0 and tile 2w + 1 in 16.
+// LB: the [bottleneck | sigma] layer (Lb, den_render.hip's transposed layer j = 2): besides the 8
+// bottleneck tiles, sigma's dz arrives as 32 bf16 per block (staged after them); the chain takes it as
+// a 17th k-step whose B fragment holds sigma at stored position 0 (W_b^T's sigma column; the rest of
+// that k-step and the 18th are zero padding).  Sigma's weight-gradient row would be a ninth row tile
+// of 8 more accumulator tiles; instead wave w computes S7 tile^T x [sigma as a one-feature tile] for
+// its S7 tiles 2w, 2w + 1 into one shared accumulator, tile 2w in column 0 and 2w + 1 in column 16
+// (hb_sigma_dw).
 template <bool LB>
 __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, int64_t b,
                                          const bf16x8 (&wt)[2][LB ? 17 : 16], f32x16 (&dw)[2][8], float (&db)[2],
                                          f32x16& sacc, float& sdb) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int DZ_BYTES = LB ? HB_BLOCK + HB_TILE : HB_BLOCK;
+  constexpr int DZ_BYTES = LB ? HB_BLOCK + HB_SIG : HB_BLOCK;
   const char* dzb = cur;
+  const char* sig = cur + HB_BLOCK;  // LB: sigma's dz, bf16[32]
   const char* sb = cur + DZ_BYTES;
   // chain: both row tiles of this wave share each dz_l fragment (K = 256, 16 k-steps): one LDS read
   // feeds two independent MFMAs, and the reads run HB_PF k-steps ahead of their use (issued
@@ -222,10 +201,12 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     }
   }
   if constexpr (LB) {
-    const bf16x8 bs = hb_frag(dzb + 8 * HB_TILE, 0);
+    // B fragment of the sigma k-step: sample c = lane (lanes 0..31) has sigma at stored position 0
+    const __bf16 z = *(const __bf16*)(sig + 2 * (lane & 31)), zz = (__bf16)0.0f;
+    const bf16x8 bs = {lane < 32 ? z : zz, zz, zz, zz, zz, zz, zz, zz};
     accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[0][16], bs, accs[0], 0, 0, 0);
     accs[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[1][16], bs, accs[1], 0, 0, 0);
-    sdb += lane < 32 ? (float)bs[0] : 0.0f;  // sigma's dz of sample lane (stored position 0)
+    sdb += (float)bs[0];
   }
   // then the activation derivative
 #pragma unroll
@@ -274,7 +255,7 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
   }
   // sigma's weight-gradient row last (placed between the chain and the epilogue or before the dW
   // MFMAs its operands spill registers or it measured slower: r03)
-  if constexpr (LB) hb_sigma_dw(dzb, sb, sacc);
+  if constexpr (LB) hb_sigma_dw(sig, sb, sacc);
 #if DEN_HB_OVL == 2
   // one wave per SIMD issues in order: the epilogue's VALU (derivative, bf16 packing) only overlaps
   // the weight-gradient MFMAs if it is interleaved with them in the instruction stream
@@ -293,13 +274,13 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   // HB_RING LDS slots of [dz_l block | S'_{l-1} block]; HB_DEPTH blocks in flight ahead of the one
   // being computed.  Each wave waits for its own part of block b+1 at the end of block b (vmcnt; the
   // younger prefetches and stores stay in flight), then the workgroup barrier publishes every part.
-  constexpr int DZ_TILES = LB ? 9 : 8;           // dz_in tiles per wave block in HBM
-  constexpr int DZ_PIECES = 2 * DZ_TILES;         // KiB of them staged
-  constexpr int SLOT = DZ_PIECES * 1024 + HB_BLOCK;
+  constexpr int DZ_TILES = LB ? 9 : 8;           // dz_in tiles per wave block in HBM (LB: the 9th holds sigma)
+  constexpr int DZ_STAGED = LB ? HB_BLOCK + HB_SIG : HB_BLOCK;  // bytes of them staged
+  constexpr int SLOT = DZ_STAGED + HB_BLOCK;
   constexpr int KST = LB ? 17 : 16;              // chain k-steps
   constexpr int ROW_BYTES = (LB ? 288 : 256) * 64;  // packed W^T row tile (chunk_bytes_K(bwd_K))
   constexpr int MTA = LB ? 9 : 8;                // partial row tiles
-  constexpr int DMA_OPS = (DZ_PIECES + HB_WAVES - 1) / HB_WAVES + HB_BLOCK / 1024 / HB_WAVES;  // per wave per block
+  constexpr int DMA_OPS = 2 * (HB_BLOCK / 1024 / HB_WAVES) + (LB ? 1 : 0);  // per wave per block
   // vector-memory ops a wave issues after its DMA of block b+1 by the end of block b (issue order:
   // stores(b-2), DMA(b+2), stores(b-1), DMA(b+3), stores(b)); the asm DMAs clobber "memory", so the
   // stores keep their program order around them
@@ -313,9 +294,9 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   const int64_t n_it = b0 < P.n_blocks ? (b0 + P.per_wg < P.n_blocks ? P.per_wg : P.n_blocks - b0) : 0;
   auto blk = [&](int64_t it) { return b0 + it; };
   auto fetch = [&](int64_t b, char* dst) {
-    if constexpr (LB) hb_dma_untracked_n<DZ_PIECES>(P.dz_in + b * DZ_TILES * HB_TILE, dst);
-    else hb_dma_untracked(P.dz_in + b * HB_BLOCK, dst);
-    hb_dma_untracked(P.s_in + b * HB_BLOCK, dst + DZ_PIECES * 1024);
+    hb_dma_untracked(P.dz_in + b * DZ_TILES * HB_TILE, dst);
+    if constexpr (LB) hb_dma_sigma(P.dz_in + b * DZ_TILES * HB_TILE + HB_BLOCK, dst + HB_BLOCK);
+    hb_dma_untracked(P.s_in + b * HB_BLOCK, dst + DZ_STAGED);
   };
 #pragma unroll
   for (int u = 0; u < HB_DEPTH; ++u)

@@ -90,16 +90,16 @@ __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, 
 #define DEN_FWD_G 2  // r02 A/B/A/B: 25.05 / 25.08 ms vs 25.28 / 25.46 ms for one tile per chunk
 #endif
 #ifndef DEN_FWD_RING
-#define DEN_FWD_RING (DEN_FWD_G == 2 ? 3 : 4)
+#define DEN_FWD_RING (DEN_FWD_G == 3 ? 2 : DEN_FWD_G == 2 ? 3 : 4)
 #endif
 #ifndef DEN_FWD_SETPRIO
 #define DEN_FWD_SETPRIO 0
 #endif
 constexpr int FWD_RING = DEN_FWD_RING;
-static_assert(FWD_RING == 3 || FWD_RING == 4, "forward weight ring: 3 or 4 slots");
+static_assert(FWD_RING >= 2 && FWD_RING <= 4, "forward weight ring: 2 to 4 slots");
 // row tiles per forward chunk (one barrier per chunk): G = 2 halves the barriers and DMA batches
 constexpr int FWD_G = DEN_FWD_G;
-static_assert(FWD_G == 1 || FWD_G == 2, "forward chunk: 1 or 2 row tiles");
+static_assert(FWD_G >= 1 && FWD_G <= 3, "forward chunk: 1 to 3 row tiles");
 constexpr int FWD_SLOT = FWD_G * CHUNK_MAX;  // bytes per forward ring slot
 static_assert(FWD_RING * FWD_SLOT <= 128 * 1024, "forward ring exceeds the LDS budget");
 DEN_HD constexpr int fwd_nchunks_l(int mode, int l) { return (fwd_tiles(mode, l) + FWD_G - 1) / FWD_G; }
@@ -1034,7 +1034,11 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
   // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles 0..
   bwd_layer_run<MODE, LAST_J, 1, WIDTH_COND / T::KI, 1>(A, lds, sample, xa, xb, 0, D_ZB);
   // sigma head row(s) of Lb as extra fake tile(s) appended to the DZB fragments
-  {
+  if constexpr (MODE == 1 && LAST_J == 1) {
+    // Lb runs layer-major (hidden_bwd_kernel<true>): sigma's dz leaves as 32 bf16 per wave block
+    // in the first 64 B of dz_b's ninth tile (the rest of that tile is not read on this path)
+    if (grp == 0) *(__bf16*)(act_ptr(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)dzs[0];
+  } else {
     constexpr int EXTRA_T = (DZB_W - WIDTH) / TM;  // sigma tile + zero padding
 #pragma unroll
     for (int e = 0; e < EXTRA_T; ++e) {
