@@ -19,6 +19,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -55,7 +57,45 @@ def parse():
     ap.add_argument("--psnr-only", action="store_true", help="run the converged-PSNR leg alone and print it")
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the configs[2] (pixel bandwidth on) and F32-mode legs of the N = 1 line")
+    ap.add_argument("--cpu-stub", action="store_true",
+                    help="launcher test only: gloo on the CPU, a stub step of the same sharding, no GPU")
     return ap.parse_args()
+
+
+def launch_ranks(a):
+    """``--gpus N`` (N > 1) started outside a torch.distributed launcher: run N ranks, one process
+    per GPU as scripts/run.py:84-100's DDP plugin does, by starting ``torch.distributed.run`` as a
+    CHILD process (this process never touches the GPU and is never replaced by another program).
+    The ranks inherit stdout, so rank 0's JSON line is this command's output; returns their exit
+    code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+class StubStep:
+    """``--cpu-stub``: the launcher / sharding / timing contract without a GPU.  Rank r of `world`
+    holds R / world rays (as TrainStep does: whole events of 4 rays) and each step does a small
+    CPU computation over them plus the step's one gradient all-reduce."""
+
+    def __init__(self, rays, world):
+        from deblur_e_nerf.train import allreduce_mean
+        self.R = rays // world
+        self.S = 1
+        self._reduce = allreduce_mean
+        self.x = torch.linspace(0, 1, self.R * 4).view(self.R, 4)
+        self.gbuf = torch.zeros(1024)
+        self.loss = torch.zeros(4)
+
+    def step(self):
+        self.gbuf.fill_(float(self.x.sum()) / self.R)
+        self._reduce(self.gbuf)
+        self.loss[0] = self.gbuf[0]
+        return self.loss
 
 
 BASELINE_METRIC = "train-step rays/sec at 131072 rays \u00d7 128 samples; PSNR vs ref"
@@ -502,32 +542,19 @@ def cpu_baseline_pixbw(n_rays, n_samples, rd, S, threads):
                 **_cpu_info(threads))
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    from deblur_e_nerf import _native as nat
-    if a.psnr_only:
-        print(json.dumps(psnr_long(a.rd, dev, steps=a.psnr_steps)), flush=True)
-        return
-
-    ts, per_event = build_step(a, dev, rank, world)
+def timed_steps(ts, a, world, dev, sync):
+    """W untimed warm-up steps, then EXACTLY K steps bracketed by a barrier + device sync on both
+    sides; the max over ranks of the elapsed time (seconds)."""
     for _ in range(a.warmup):
         ts.step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         ts.step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -535,6 +562,48 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
+    return elapsed
+
+
+def main():
+    a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}")
+    if a.cpu_stub:
+        if world > 1:
+            dist.init_process_group("gloo")
+        world = dist.get_world_size() if world > 1 else 1
+        dev = torch.device("cpu")
+        ts = StubStep(a.rays, world)
+        elapsed = timed_steps(ts, a, world, dev, lambda: None)
+        if rank == 0:
+            print(json.dumps({"metric": metric_name(a), "value": round(a.rays * a.steps / elapsed, 1),
+                              "unit": "rays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                              "ms_per_step": round(elapsed / a.steps * 1e3, 3), "data": "cpu stub",
+                              "config": {"rays_per_step": a.rays, "rays_per_rank": ts.R,
+                                         "parallelism": f"ray-dp{world}"}}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
+    dev = torch.device("cuda", local)
+    from deblur_e_nerf import _native as nat
+    if a.psnr_only:
+        print(json.dumps(psnr_long(a.rd, dev, steps=a.psnr_steps)), flush=True)
+        return
+
+    ts, per_event = build_step(a, dev, rank, world)
+    rays_per_rank = ts.R
+    elapsed = timed_steps(ts, a, world, dev, torch.cuda.synchronize)
     loss = ts.loss[:3].tolist()
     ms = elapsed / a.steps * 1e3
     rays_per_step = a.rays
@@ -628,7 +697,7 @@ def main():
             "config": {"workload": f"chair synthetic, pixel-bandwidth {'on (it_sample_size=%d)' % a.it_samples if a.pixbw else 'off'}, "
                                    f"{a.rays} rays x {a.samples} samples, "
                                    f"mlp 8x256 rd={a.rd}, event prep+rays+fwd+bwd+allreduce+Adam",
-                       "rays_per_step": a.rays, "samples_per_ray": a.samples,
+                       "rays_per_step": a.rays, "rays_per_rank": rays_per_rank, "samples_per_ray": a.samples,
                        "events_per_step": a.rays // per_event,
                        "parallelism": f"ray-dp{world}"},
             "loss": [round(x, 6) for x in loss],
