@@ -417,14 +417,20 @@ class DeblurENeRF(_Base):
                                                          "interval": self.hparams.lr_scheduler.interval}}
 
     def fit_step(self, batch, batch_index, optimizer):
-        """One optimisation step without a Trainer: the occupancy grid from rank 0 when it changed
-        (DDP's buffer broadcast), training_step, backward, the DDP gradient
-        all-reduce (mean over ranks, one flat buffer), optimizer step on the last micro-batch of
-        an accumulation group (PL's accumulate_grad_batches semantics: gradients summed over the
-        group, each micro-batch loss scaled by 1 / accumulate_grad_batches)."""
+        """One optimisation step without a Trainer: the occupancy grid from rank 0 (DDP's buffer
+        broadcast), training_step, backward, the DDP gradient all-reduce (mean over ranks, one
+        flat buffer), optimizer step on the last micro-batch of an accumulation group (PL's
+        accumulate_grad_batches semantics: gradients summed over the group, each micro-batch loss
+        scaled by 1 / accumulate_grad_batches).
+
+        DDP (broadcast_buffers=True, run.py:86-88) broadcasts rank 0's buffers in a forward only
+        when the previous forward ran with gradient sync on; PL runs micro-batches 0..acc-2 of a
+        group under ``no_sync()``, so the broadcast happens before the FIRST micro-batch of each
+        group only -- before training_step's grid update there (deblur_e_nerf.py:465), so the
+        remaining micro-batches of the group march with each rank's own freshly updated grid."""
         acc = self.trainer.accumulate_grad_batches
-        # DDP broadcasts the buffers from rank 0 before each forward (broadcast_buffers=True)
-        marching.sync_grid(getattr(self.nerf, "occupancy_grid", None))
+        if batch_index % acc == 0:
+            marching.sync_grid(getattr(self.nerf, "occupancy_grid", None))
         loss = self.training_step(batch, batch_index)
         (loss / acc).backward()
         if (batch_index + 1) % acc == 0:

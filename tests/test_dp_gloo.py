@@ -175,3 +175,86 @@ def test_occupancy_grid_sync_broadcasts_rank0_after_updates():
         assert s0 == s1 == (step % 2 == 0)
         assert torch.equal(o0, o1) and torch.equal(b0, b1)
     assert not torch.equal(h0[0][1], h0[2][1])  # the grid did change between updates
+
+
+class _FitStub(torch.nn.Module):
+    """The attributes DeblurENeRF.fit_step reads, around the product's fit_step / sync_grid /
+    allreduce_gradients: a training_step that updates the occupancy grid on the first micro-batch
+    of each accumulation group with per-rank draws (deblur_e_nerf.py:465; den_occ_update's effect)
+    and records the grid each micro-batch marches with."""
+
+    def __init__(self, rank, acc):
+        super().__init__()
+        from types import SimpleNamespace
+        from deblur_e_nerf.external.marching import OccupancyGrid
+        self.w = torch.nn.Parameter(torch.zeros(3))
+        self.trainer = SimpleNamespace(accumulate_grad_batches=acc)
+        self.nerf = SimpleNamespace(occupancy_grid=OccupancyGrid([-1.5] * 3 + [1.5] * 3, resolution=8))
+        self._global_step = 0
+        self.g = torch.Generator().manual_seed(300 + rank)
+        self.seen = []
+
+    def training_step(self, batch, batch_index):
+        grid = self.nerf.occupancy_grid
+        before = grid.occs.clone()
+        if batch_index % self.trainer.accumulate_grad_batches == 0:
+            grid.occs.copy_(torch.rand(grid.num_cells, generator=self.g))
+            grid._binary.copy_((grid.occs > 0.5).reshape(grid._binary.shape))
+            grid._dirty = True
+        self.seen.append((before, grid.occs.clone()))
+        return (self.w * batch).sum()
+
+
+def _fit_worker(rank, world, port, out, acc, n_micro):
+    import sys
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deblur_e_nerf.models.deblur_e_nerf import DeblurENeRF
+    m = _FitStub(rank, acc)
+    opt = torch.optim.SGD(m.parameters(), lr=1.0)
+    params = []
+    for i in range(n_micro):
+        DeblurENeRF.fit_step(m, torch.tensor([1.0, 2.0, 3.0]) * (rank + 1) * (i + 1), i, opt)
+        params.append(m.w.detach().clone())
+    out[rank] = (m.seen, params)
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("acc", [1, 3])
+def test_fit_step_grid_broadcast_per_accumulation_group(acc):
+    """DDP + PL accumulation (run.py:84-100, 07_ziggy_and_fuzz_hdr.yaml accumulate_grad_batches):
+    rank 0's grid is broadcast only before the first micro-batch of a group (the only forward
+    after a synced one), before that micro-batch's rank-local grid update; micro-batches 1..acc-1
+    march with each rank's own updated grid; the averaged gradient is applied once per group and
+    leaves identical parameters on every rank."""
+    n_micro = 2 * acc + 1
+    port = _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_fit_worker, args=(WORLD, port, out, acc, n_micro), nprocs=WORLD, join=True)
+    (seen0, p0), (seen1, p1) = out[0], out[1]
+    for i in range(n_micro):
+        (b0, a0), (b1, a1) = seen0[i], seen1[i]
+        if i % acc == 0:
+            # the pre-update grid is rank 0's on every rank (the broadcast), then each rank updates its own
+            assert torch.equal(b0, b1), i
+            if i > 0:  # rank 0's grid of the previous group's last micro-batch
+                assert torch.equal(b1, seen0[i - 1][1]), i
+            assert not torch.equal(a0, a1), i
+        else:  # no broadcast inside a group: each rank keeps its own freshly updated grid
+            assert torch.equal(b0, a0) and torch.equal(b1, a1), i
+            assert not torch.equal(a0, a1), i
+            assert torch.equal(a1, seen1[i - 1][1]), i
+    for i in range(n_micro):
+        assert torch.equal(p0[i], p1[i]), i
+        if (i + 1) % acc == 0:  # SGD lr 1 on the rank-mean of the group's summed (loss / acc) gradients
+            k = i + 1 - acc
+            g = sum((r + 1) * (j + 1) for r in range(WORLD) for j in range(k, i + 1)) / WORLD / acc
+            prev = p0[k - 1] if k > 0 else torch.zeros(3)
+            assert torch.allclose(p0[i], prev - g * torch.tensor([1.0, 2.0, 3.0])), i
+        elif i > 0:
+            assert torch.equal(p0[i], p0[i - 1]), i
