@@ -475,9 +475,10 @@ def affine_log_intensity_correction(pred_intensity_img, target_intensity_img, ga
     B, C, H, W = target.shape
     gep = torch.ones(B, dtype=torch.float64) if gain_exposure_prod is None else \
         torch.as_tensor(gain_exposure_prod, dtype=torch.float64).reshape(B)
-    log_gep = (gep / gep.mean()).log().view(B, 1, 1, 1)
-    plog = pred.to(torch.float64).log()
-    tlog = target.to(torch.float64).log() - log_gep
+    log_gep = (gep / gep.mean()).log().view(B, 1, 1, 1).to(target.dtype)
+    # logs in the images' dtype, f64 only for the least squares (the reference's order, :729-792)
+    plog = pred.log().to(torch.float64)
+    tlog = (target.log() - log_gep).to(torch.float64)
     per_channel = (not has_bayer_filter) or per_channel_log_it_scale
     if per_channel:
         A = torch.nn.functional.pad(plog.unsqueeze(-1), (0, 1), value=1.0)  # (B, C, H, W, 2)

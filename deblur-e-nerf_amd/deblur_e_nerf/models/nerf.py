@@ -27,6 +27,12 @@ from ..external.marching import ContractionType, OccupancyGrid, contraction_id
 from ..utils import modules
 
 
+def _randint(high, size, device=None):
+    """torch.randint draws of the occupancy update's cone branch (a random camera per cell point,
+    reference nerf.py:178-181); tests substitute the draws a reference run recorded."""
+    return torch.randint(0, high, size, device=device)
+
+
 def shifted_softplus(x, shift=1, beta=1, threshold=20):
     raise NotImplementedError("only the shifted_trunc_exp density activation is fused (nerf.py:22)")
 
@@ -141,7 +147,7 @@ class NeRF(torch.nn.Module):
 
         def occ_eval_fn(x):
             if self.cone_angle > 0.0:
-                camera_ids = torch.randint(0, len(T_wc_position), (x.shape[0],), device=T_wc_position.device)
+                camera_ids = _randint(len(T_wc_position), (x.shape[0],), device=T_wc_position.device)
                 origins = T_wc_position[camera_ids, :]
                 t = (origins - x).norm(dim=-1, keepdim=True)
                 s = torch.clamp(t * self.cone_angle, min=self.render_step_size)

@@ -830,12 +830,56 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra
                 timestamp = _GradTap.apply(timestamp, lambda g, i=slot: dts.__setitem__(i, g.detach().clone()))
             return _f(timestamp, *a, **k)
         m.render_log_intensity = rli
+        # per render_log_intensity call: its log intensities (the TV term's |end - start| decides
+        # which events have a well-defined L1 sign); per NeRF.forward call: d loss / d colour x
+        # (1 - opacity) per ray, the terms the render background's gradient sums
+        lis, bkray = [], []
+
+        def rli_rec(*a, _f=m.render_log_intensity, **k):
+            r = _f(*a, **k)
+            lis.append(r[0].detach().clone())
+            return r
+        m.render_log_intensity = rli_rec
+        orig_nerf_forward = m.nerf.forward
+
+        def nerf_rec(o, dr, _f=orig_nerf_forward):
+            rad, op, dp, mspr = _f(o, dr)
+            slot = len(bkray)
+            bkray.append(None)
+            keep = (1 - op.detach()).clone()
+            rad = _GradTap.apply(rad, lambda g, i=slot, w=keep: bkray.__setitem__(
+                i, (g.detach() * (w[..., None] if g.dim() > w.dim() else w)).clone()))
+            return rad, op, dp, mspr
+        m.nerf.forward = nerf_rec
+        # the occupancy update's torch.randint draws (the cone branch's random camera per point,
+        # nerf.py:178-181), replayed by tests through models/nerf._randint
+        cam_draws = []
+        real_randint = torch.randint
+
+        def randint_rec(*a, **k):
+            r = real_randint(*a, **k)
+            cam_draws.append(r.clone())
+            return r
+        orig_upd = m.nerf.update_occ_grid
+
+        def upd_rec(*a, _f=orig_upd, **k):
+            torch.randint = randint_rec
+            try:
+                return _f(*a, **k)
+            finally:
+                torch.randint = real_randint
+        m.nerf.update_occ_grid = upd_rec
         torch.manual_seed(200)
         try:
             loss = m.training_step(b, 0)
             loss.backward()
         finally:
             dmod.ray_marching = real
+            torch.randint = real_randint
+        if variant in ("full", "f64"):
+            sfx = "" if variant == "full" else "_f64"
+            out.update({f"li_g{i}{sfx}": li.numpy() for i, li in enumerate(lis)})
+            out.update({f"bkray_{i}{sfx}": g.numpy() for i, g in enumerate(bkray) if g is not None})
         if variant != "nopose":
             sfx = "" if variant == "full" else "_" + variant
             # per-event timestamp gradients back in the original event order
@@ -843,14 +887,14 @@ def gen_step(pixbw=False, rd=1, seed=6, N=40, S=8, tag=None, arch="mlp", **extra
                         if g is not None})
         if variant == "full":
             grid = m.nerf.occupancy_grid
+            if cam_draws:
+                out.update({f"occ_randint_{i}": r.numpy() for i, r in enumerate(cam_draws)})
             out.update(occ_u=grid.last_u.numpy(), occs=grid.occs.numpy(), binary=grid.binary.numpy(),
                        loss=loss.detach().numpy(), mspr=np.array(float(m.train_batch_size) if hasattr(
                            m, "train_batch_size") else 0.0),
                        new_batch_size=np.array(m.trainer.datamodule.train_dataset.batch_size),
                        **{f"jitter_{i}": j.numpy() for i, j in enumerate(jit)})
             out.update(_step_grads(m, cfg))
-            for i, (ri, t0, t1) in enumerate(kept):  # the marched samples of each render call
-                out.update({f"kept_ri_{i}": ri.numpy(), f"kept_t0_{i}": t0.numpy(), f"kept_t1_{i}": t1.numpy()})
             if arch != "mlp":
                 rf = m.nerf.radiance_field
                 out.update({f"param:{k}": prm.detach().numpy() for k, prm in rf.named_parameters()
@@ -1066,6 +1110,59 @@ def gen_render_ngp(rd=1, seed=25, R=64, sigma_bias_shift=2.0):
         rad, op, dp, mspr = nerf(o, d)
     out.update(eval_radiance=rad.numpy(), eval_opacity=op.numpy(), eval_depth=dp.numpy(), eval_mspr=np.array(mspr))
     save(f"render_ngp_rd{rd}.npz", **out)
+
+
+def gen_render_ngp_cone(rd=1, seed=27, R=64, C=12, sigma_bias_shift=2.0):
+    """render_ngp_cone_rd1.npz -- the reference NeRF with the ngp field in configs[3]'s composition
+    (07_ziggy_and_fuzz_hdr.yaml:60-75: unbounded-sphere contraction of its aabb, near 0.01 / far 13,
+    cone_angle 0.004, a 32^3 grid): the occupancy-grid update at step 0, whose cone branch
+    (models/nerf.py:176-193) draws a random camera per cell point (torch.randint, recorded beside
+    the cell jitter occ_u) and scales the density by that camera's cone step; then an eval render
+    through cone-stepped marching of the updated grid."""
+    cfg = _step_cfg(arch="ngp", contraction="sphere", aabb=[0.2, -0.4, 0.0, 3.7, 3.7, 1.8], near=0.01, far=13.0,
+                    cone=0.004, res=32)
+    nerf, p = _ref_nerf_ngp(rd, seed, cfg["res"], cfg)
+    rf = nerf.radiance_field
+    a = torch.tensor(cfg["aabb"])
+    centre, half = (a[:3] + a[3:]) / 2, (a[3:] - a[:3]) / 2
+    g = torch.Generator().manual_seed(seed + 1000)
+    v = torch.randn(C, 3, generator=g)
+    cams = (centre + v / v.norm(dim=-1, keepdim=True) * float(half.norm()) * 1.3).float()
+    out = dict(seed=seed, rd=rd, res=cfg["res"], step=cfg["step"], aabb=np.array(cfg["aabb"], np.float32),
+               near=cfg["near"], far=cfg["far"], cone=cfg["cone"], contraction=np.array("sphere"),
+               sigma_bias_shift=sigma_bias_shift, pos_encoding=np.array(json.dumps(NGP_SMALL)),
+               table=p["mlp_base.0.params"].numpy(), cams=cams.numpy(),
+               **{f"param:{k}": v.numpy() for k, v in p.items() if k != "mlp_base.0.params"})
+    draws, real_randint = [], torch.randint
+
+    def randint_rec(*ra, **rk):
+        r = real_randint(*ra, **rk)
+        draws.append(r.clone())
+        return r
+    nerf.train()
+    torch.manual_seed(110)
+    torch.randint = randint_rec
+    try:
+        nerf.update_occ_grid(step=0, T_wc_position=cams)
+    finally:
+        torch.randint = real_randint
+    grid = nerf.occupancy_grid
+    assert len(draws) == 1, len(draws)
+    out.update(occ_u=grid.last_u.numpy(), occ_randint_0=draws[0].numpy(), occs=grid.occs.numpy(),
+               binary=grid.binary.numpy())
+    with torch.no_grad():
+        rf.mlp_base[1].output_layer.bias[0] += sigma_bias_shift
+    idx = torch.randint(0, C, (R,), generator=g)
+    o = cams[idx]
+    tgt = centre + (torch.rand(R, 3, generator=g) * 2 - 1) * half * 0.6
+    d = tgt - o
+    d = (d / d.norm(dim=-1, keepdim=True)).float()
+    nerf.eval()
+    with torch.no_grad():
+        rad, op, dp, mspr = nerf(o, d)
+    out.update(rays_o=o.numpy(), rays_d=d.numpy(), eval_radiance=rad.numpy(), eval_opacity=op.numpy(),
+               eval_depth=dp.numpy(), eval_mspr=np.array(mspr))
+    save(f"render_ngp_cone_rd{rd}.npz", **out)
 
 
 def gen_ngp_all():

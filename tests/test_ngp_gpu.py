@@ -240,8 +240,11 @@ def _ngp_nerf(z, sigma_shift=None):
               mlp_head=dict(hidden_activation="softplus", radiance_activation="softplus", n_neurons=64,
                             n_hidden_layers=2, weight_norm=False))
     occ = ED(resolution=int(z["res"]), occ_thre=0.01, ema_decay=0.95, warmup_steps=256, n=16)
-    nerf = nerf_lib.NeRF([float(v) for v in z["aabb"]], marching.ContractionType.AABB, occ, float(z["near"]),
-                         float(z["far"]), float(z["step"]), "parameter", 0.0, 1e-4, 0.0, 16384, "ngp", arch, 3, rd)
+    ctype = {"aabb": "AABB", "sphere": "UN_BOUNDED_SPHERE", "tanh": "UN_BOUNDED_TANH"}[
+        str(z["contraction"]) if "contraction" in z.files else "aabb"]
+    cone = float(z["cone"]) if "cone" in z.files else 0.0
+    nerf = nerf_lib.NeRF([float(v) for v in z["aabb"]], getattr(marching.ContractionType, ctype), occ, float(z["near"]),
+                         float(z["far"]), float(z["step"]), "parameter", cone, 1e-4, 0.0, 16384, "ngp", arch, 3, rd)
     rf = nerf.radiance_field
     p = {k[len("param:"):]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param:")}
     p["mlp_base.0.params"] = torch.from_numpy(z["table"])
@@ -288,3 +291,57 @@ def test_nerf_ngp_matches_reference(golden_dir, rd, monkeypatch):
         rad, op, dp, mspr = nerf(o, d)
     for a, k in ((rad, "eval_radiance"), (op, "eval_opacity"), (dp, "eval_depth")):
         assert rel_err(a, z[k]) <= 1e-4, k
+
+
+def _check_grid(grid, z, occ_thre=0.01):
+    """occs within 1e-4 relative of the reference's; the binary grid identical except cells whose
+    reference occupancy lies within 1e-4 (relative) of the threshold (nerfacc: occs > min(mean,
+    occ_thre))."""
+    occs = grid.occs.detach().cpu().double()
+    ref = torch.from_numpy(z["occs"]).double()
+    e = float((occs - ref).norm() / ref.norm())
+    thre = min(float(ref.mean()), occ_thre)
+    flips = grid.binary.detach().cpu().reshape(-1) != torch.from_numpy(z["binary"]).reshape(-1)
+    near = (ref - thre).abs() <= 1e-4 * thre
+    print(f"  occs rel err {e:.2e} (max {float(ref.max()):.3e}), binary flips {int(flips.sum())} "
+          f"({int((flips & ~near).sum())} away from the threshold)")
+    assert e <= 1e-4, e
+    assert not bool((flips & ~near).any())
+
+
+def test_nerf_ngp_cone_update_and_render_matches_reference(golden_dir, monkeypatch):
+    """configs[3]'s composition (07_ziggy_and_fuzz_hdr.yaml: unbounded-sphere contraction, near 0.01
+    / far 13, cone_angle 0.004): the occupancy update's cone branch (nerf.py:176-193 -- a random
+    camera per cell point, its cone step times the density) with the reference's recorded cell
+    jitter and camera draws, then the eval render through cone-stepped marching.  F32."""
+    from deblur_e_nerf.external import marching
+    from deblur_e_nerf.models import nerf as nerf_lib
+    from test_nerfacc_gpu import _Draws
+    z = np.load(f"{golden_dir}/render_ngp_cone_rd1.npz")
+    nerf = _ngp_nerf(z)
+    nerf.train()
+    cams = torch.from_numpy(z["cams"]).to(DEV)
+    monkeypatch.setattr(marching, "_uniform", _Draws([z["occ_u"]]))
+    ids = [torch.from_numpy(z["occ_randint_0"])]
+
+    def replay(high, size, device=None):
+        r = ids.pop(0)
+        assert tuple(r.shape) == tuple(size) and int(r.max()) < high
+        return r.to(device)
+    monkeypatch.setattr(nerf_lib, "_randint", replay)
+    nerf.update_occ_grid(step=0, T_wc_position=cams)
+    assert not ids
+    _check_grid(nerf.occupancy_grid, z)
+    with torch.no_grad():
+        nerf.radiance_field.mlp_base[1].output_layer.bias[0] += float(z["sigma_bias_shift"])
+    # the render marches the reference's binary grid (cells at the threshold could flip)
+    nerf.occupancy_grid._binary.copy_(torch.from_numpy(z["binary"]).to(DEV))
+    nerf.eval()
+    o = torch.from_numpy(z["rays_o"]).to(DEV)
+    d = torch.from_numpy(z["rays_d"]).to(DEV)
+    with torch.no_grad():
+        rad, op, dp, mspr = nerf(o, d)
+    assert abs(mspr - float(z["eval_mspr"])) <= 1e-3 * float(z["eval_mspr"]), (mspr, float(z["eval_mspr"]))
+    errs = {k: rel_err(a, z[k]) for a, k in ((rad, "eval_radiance"), (op, "eval_opacity"), (dp, "eval_depth"))}
+    print(f"  cone render: mean samples / ray {mspr:.2f} vs {float(z['eval_mspr']):.2f}; {errs}")
+    assert max(errs.values()) <= 1e-4, errs

@@ -7,7 +7,7 @@ judged against the oracle run in f64: the loss is a difference of log
 intensities of two nearby renders, so its gradient cancels and even the f32
 oracle sits up to a few 1e-4 from the f64 one on some layers.  Per layer the HIP
 gradient must be within max(1e-4, 4 x the f32 oracle's own error) of f64.
-BF16 -- 3e-2 on losses, 6e-2 on gradients (vs f64).
+BF16 -- 2.5e-3 on losses, 3e-2 on gradients (vs f64; ~2x the measured worst case).
 Adam is checked against torch.optim.Adam fed the same gradient (1e-6).
 """
 import pytest
@@ -30,7 +30,9 @@ def _setup(mode, rd, N=64, S=128, seed=5):
 
 
 @pytest.mark.parametrize("rd", [1, 3])
-@pytest.mark.parametrize("mode,tol_l,tol_g", [("f32", 1e-4, 1e-4), ("bf16", 3e-2, 6e-2)])
+# BF16 bounds ~2x the measured worst case (r03, gpurun full.log): losses 1.1e-3 (the TV loss on the
+# 1e-3 floor), gradients 1.4e-2
+@pytest.mark.parametrize("mode,tol_l,tol_g", [("f32", 1e-4, 1e-4), ("bf16", 2.5e-3, 3e-2)])
 def test_train_step_matches_oracle(mode, rd, tol_l, tol_g):
     from oracle.train import flat_grad
     ts, b = _setup(mode, rd)
@@ -161,14 +163,16 @@ def test_missed_rays_stay_finite_over_training():
 
 
 @pytest.mark.parametrize("rd", [1, 3])
-@pytest.mark.parametrize("mode,tol_l,tol_g", [("f32", 1e-4, 1e-4), ("bf16", 3e-2, 6e-2)])
+# BF16: the TV loss measured 2.4e-2 off (a difference of pixel-bandwidth filtered log intensities
+# 1e-3 apart), gradients 1.4e-2
+@pytest.mark.parametrize("mode,tol_l,tol_g", [("f32", 1e-4, 1e-4), ("bf16", 3e-2, 3e-2)])
 def test_pixbw_train_step_matches_oracle(rd, mode, tol_l, tol_g):
     """Pixel-bandwidth-on step (BASELINE configs[2] shape, small): PixbwTrainStep
     (event prep, sample timestamps, rays, renders, pixel-bandwidth filter, losses,
     autograd backward through the HIP kernels) against the oracle's step; F32
     parity mode: losses 1e-4 relative, gradients judged against the f64 oracle
     as in test_train_step_matches_oracle; BF16 (the mode bench.py --pixbw runs):
-    3e-2 on losses, 6e-2 on gradients."""
+    3e-2 on losses, 3e-2 on gradients."""
     from deblur_e_nerf.train import PixbwTrainStep, synthetic_pixbw_events
     from oracle import pixbw as opb
     from oracle.train import pixbw_flat_grad
@@ -250,12 +254,12 @@ def test_full_size_step_properties():
     e_sub = norm_rel(sub.gbuf, g64)
     print(f"full-size loss {full.loss[:3].cpu().tolist()}; sub-batch {loss} vs f64 oracle {(Ld, Lt, tot)}; "
           f"sub-batch gradient vs f64 oracle {e_sub:.2e}")
-    assert abs(loss[2] - tot) <= 3e-2 * abs(tot)
-    assert e_sub <= 6e-2  # the BF16 gradient bound of this file
+    assert abs(loss[2] - tot) <= 1e-4 * abs(tot)  # measured 8e-6
+    assert e_sub <= 3e-2  # the BF16 gradient bound of this file (measured 1.5e-2)
     # linearity at full size: the 2^24-sample gradient (persistent split-K over every CU, one
     # reduction) equals the event-weighted sum of the gradients of its K sub-batches computed
     # separately -- the loss is a mean over events, so g_full = sum_k (n_k / N) g_k (BF16
-    # summation-order noise: 1e-2)
+    # summation-order noise: measured 8.2e-5)
     K = 8
     acc = torch.zeros_like(full.gbuf, dtype=torch.float64)
     g_full = full.gbuf.detach().double().clone()
@@ -269,4 +273,4 @@ def test_full_size_step_properties():
         acc += part.gbuf.double() / K
     e_lin = norm_rel(acc, g_full)
     print(f"full-size gradient vs the mean of {K} sub-batch gradients: {e_lin:.2e}")
-    assert e_lin <= 1e-2
+    assert e_lin <= 2e-4
