@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--it-samples", type=int, default=16)
     ap.add_argument("--cpu-rays", type=int, default=2048,
                     help="rays of the bounded pixel-bandwidth-on CPU-baseline sample (--pixbw)")
-    ap.add_argument("--psnr-steps", type=int, default=2000, help="Adam steps of the converged-PSNR leg (0: skip)")
+    ap.add_argument("--psnr-steps", type=int, default=1000, help="Adam steps of the converged-PSNR leg (0: skip)")
     ap.add_argument("--psnr-only", action="store_true", help="run the converged-PSNR leg alone and print it")
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the configs[2] (pixel bandwidth on) and F32-mode legs of the N = 1 line")
@@ -441,7 +441,7 @@ def _teacher_batch(gen, n_events, dev="cpu", motion=0.3, radius=4.03):
 
 VIEW_DIRS = ((0.62, -0.55, 0.56), (-0.7, 0.3, 0.4), (0.1, 0.8, -0.5), (-0.4, -0.6, -0.3))
 # the converged-PSNR leg: Adam steps, events per batch, samples per ray, view size, lr cuts, seeds
-PSNR_LEG = dict(steps=2000, n_events=1024, n_samples=64, view=64, milestones=(0.5, 0.8), batch_seed=123,
+PSNR_LEG = dict(steps=1000, n_events=512, n_samples=64, view=64, milestones=(0.5, 0.8), batch_seed=123,
                 teacher_seed=77, student_seed=0)
 
 
@@ -503,7 +503,7 @@ def psnr_long(rd, dev, steps=None, modes=("f32", "bf16")):
     """BASELINE's "PSNR vs ref" at convergence (PSNR_LEG): the HIP TrainStep in F32 (the reference's
     arithmetic, pinned to the reference at 1e-4 by tests/) and in BF16 (the benchmark's mode) train
     from ONE init on a teacher scene for `steps` Adam steps, each on a fresh batch of configs[0]'s
-    shape (1024 events = 4096 rays x 64 samples, drawn on a seeded CPU generator) whose measured
+    shape (512 events = 2048 rays x 64 samples, drawn on a seeded CPU generator) whose measured
     log-intensity changes are the teacher's; the learning rate is cut x0.3 at the milestones (the
     reference's multi_step_lr); four held-out views are aligned to the teacher's by the reference's
     affine log-intensity correction (deblur_e_nerf.py:705-833) and scored with its PSNR

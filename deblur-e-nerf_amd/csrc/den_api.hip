@@ -81,9 +81,6 @@ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
                          // 0 = in render_bwd_kernel + a streamed weight gradient (r03: 1.6-2 ms slower)
 #endif
 
-#ifndef DEN_DW_STREAM
-#define DEN_DW_STREAM 1  // BF16: operand-sharing streamed weight gradients (den_dwstream.hip)
-#endif
 
 struct WsLayout {
   size_t act[NACT];
@@ -374,20 +371,35 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   return DEN_OK;
 }
 
+// compute units of the current device (the persistent forward runs one workgroup per CU)
+int device_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 template <int MODE>
 int render_fwd_impl(const den_render_desc* d, const den_render_io* io, hipStream_t s) {
   WsLayout L = ws_layout(d);
   RenderArgs<MODE> A = make_args<MODE>(d, io, L);
   A.w = (const char*)io->w_fwd;
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
+  A.n_items = n / fwd_wg_samples(MODE);
+  // persistent: one workgroup per CU (the 143 KB weight ring + records admit one), each walking
+  // items blockIdx.x, blockIdx.x + grid, ...
+  const unsigned grid = (unsigned)std::min<int64_t>(A.n_items, device_cu_count());
   {
     DEN_TIMED(T_RENDER_FWD, s);
     if (d->train)
-      hipLaunchKernelGGL((render_fwd_kernel<MODE, true>), dim3((unsigned)(n / fwd_wg_samples(MODE))),
-                         dim3(fwd_threads(MODE)), 0, s, A);
+      hipLaunchKernelGGL((render_fwd_kernel<MODE, true>), dim3(grid), dim3(fwd_threads(MODE)), 0, s, A);
     else
-      hipLaunchKernelGGL((render_fwd_kernel<MODE, false>), dim3((unsigned)(n / fwd_wg_samples(MODE))),
-                         dim3(fwd_threads(MODE)), 0, s, A);
+      hipLaunchKernelGGL((render_fwd_kernel<MODE, false>), dim3(grid), dim3(fwd_threads(MODE)), 0, s, A);
   }
   DEN_LAUNCHED();
   return DEN_OK;
@@ -430,21 +442,20 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
     }
   }
   if (!(parts & 2)) return DEN_OK;
-#if DEN_DW_STREAM
   if (hidden) {
     // streamed, operand-sharing weight gradients (den_dwstream.hip)
-    if ((rc = launch_dwstream<8, 16, 2, 2, DEN_DWS_NW1, 3>(d, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK)
+    if ((rc = launch_dwstream<8, 16, 2, 2, DWS_NW1, 3>(d, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK)
       return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s)) != DEN_OK) return rc;
     if (!DEN_LB_HIDDEN) {
-      if ((rc = launch_dwstream<9, 9, 8, 8, DEN_DWS_NW2, 3>(d, L, ws, D_ZB, -1, A_S0 + 7, -1, s)) != DEN_OK) return rc;
+      if ((rc = launch_dwstream<9, 9, 8, 8, DWS_NW2, 3>(d, L, ws, D_ZB, -1, A_S0 + 7, -1, s)) != DEN_OK) return rc;
       if ((rc = launch_dwstream_reduce(d, L, ws, 9, 8, 0, 9, L_B, 256, 0, 1, G, s)) != DEN_OK) return rc;
     }
-    if ((rc = launch_dwstream<4, 4, 8, 9, DEN_DWS_NW3, DEN_DWS_D3, DEN_DWS_U3>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 4, 9, 0, 4, L_G, 256, WIDTH, 1, G, s)) != DEN_OK) return rc;
     if (!(DEN_LB_HIDDEN && DEN_LR_FUSED)) {  // else inside render_bwd_kernel<1, 1>
-      if ((rc = launch_dwstream<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4, DEN_DWS_U4>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK)
+      if ((rc = launch_dwstream<1, 1, 4, 4, DWS_NW4, DWS_D4, DWS_U4>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK)
         return rc;
       if ((rc = launch_dwstream_reduce(d, L, ws, 1, 4, 0, 1, L_R, 128, 0, 1, G, s)) != DEN_OK) return rc;
     }
@@ -455,7 +466,6 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
     }
     return DEN_OK;
   }
-#endif
   if ((rc = launch_dw<MODE, 8, 64, 0>(d, L, ws, 0, D_Z0 + 0, A_PE, -1, 0, G, s)) != DEN_OK) return rc;
   if (hidden) {
     // pe columns of L5 (the S4 columns and the bias come from the hidden launch of layer 5)
@@ -790,7 +800,7 @@ size_t den_event_loss_workspace_bytes(int32_t N) {
 
 int den_event_loss_fwd(int32_t N, int32_t fn, const float* x, const float* target, const uint8_t* valid,
                        const float* c, float* loss, void* ws, void* stream) {
-  if (N <= 0 || fn < 0 || fn > 2 || !x || !c || !loss || !ws) return fail(DEN_EINVAL, "bad arguments");
+  if (N <= 0 || fn < 0 || fn > 3 || !x || !c || !loss || !ws) return fail(DEN_EINVAL, "bad arguments");
   const int nb = (N + LOSS_BLOCK - 1) / LOSS_BLOCK;
   float* part = (float*)ws;
   float* count = part + 2 * nb;
@@ -805,7 +815,7 @@ int den_event_loss_fwd(int32_t N, int32_t fn, const float* x, const float* targe
 int den_event_loss_bwd(int32_t N, int32_t fn, const float* x, const float* target, const uint8_t* valid,
                        const float* c, const float* gout, float* d_x, float* d_target, float* d_c, void* ws,
                        void* stream) {
-  if (N <= 0 || fn < 0 || fn > 2 || !x || !c || !gout || !d_x || !d_c || !ws) return fail(DEN_EINVAL, "bad arguments");
+  if (N <= 0 || fn < 0 || fn > 3 || !x || !c || !gout || !d_x || !d_c || !ws) return fail(DEN_EINVAL, "bad arguments");
   const int nb = (N + LOSS_BLOCK - 1) / LOSS_BLOCK;
   float* part = (float*)ws;
   float* count = part + 2 * nb;
@@ -847,7 +857,7 @@ static EventStepArgs make_event_args(int32_t N, int32_t rd, int32_t fn_d, int32_
 int den_event_step_fwd(int32_t N, int32_t rd, int32_t fn_d, int32_t fn_t, int32_t has_bkgd, float min_int, float w_d,
                        float w_t, const float* radiance, const float* opacity, const int64_t* channel,
                        const float* target, const float* c, void* ws, float* out, void* stream) {
-  if (N <= 0 || (rd != 1 && rd != 3) || fn_d < 0 || fn_d > 2 || fn_t < 0 || fn_t > 2 || !radiance || !target || !c ||
+  if (N <= 0 || (rd != 1 && rd != 3) || fn_d < 0 || fn_d > 3 || fn_t < 0 || fn_t > 3 || !radiance || !target || !c ||
       !ws || !out || (!has_bkgd && !opacity) || (rd > 1 && !channel))
     return fail(DEN_EINVAL, "bad arguments");
   EventStepArgs E = make_event_args(N, rd, fn_d, fn_t, has_bkgd, min_int, w_d, w_t, radiance, opacity, channel,
@@ -1347,7 +1357,7 @@ bool ngp_grid(const den_ngp_desc* d, NgpGrid* G, int64_t* table_floats) {
 // workgroups of the MFMA field kernels: one 32-sample tile per wave, capped (they loop)
 unsigned ngp_mf_grid(int64_t n) {
   const int64_t wg = ((n + 31) / 32 + NM_WAVES - 1) / NM_WAVES;
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(wg, DEN_NGP_MF_GRID));
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(wg, NM_GRID));
 }
 
 struct NgpWs {
@@ -1365,11 +1375,11 @@ NgpWs ngp_ws(int64_t n) {
   off += align256((size_t)ND_ROWS * ngp_ld(n) * 4);
   int64_t splits = std::max<int64_t>(1, std::min<int64_t>(256, (n + 4095) / 4096));
   int64_t per = (n + splits - 1) / splits;
-  per = (per + NGP_DW_CHUNK - 1) / NGP_DW_CHUNK * NGP_DW_CHUNK;
+  per = (per + NDW_CHUNK - 1) / NDW_CHUNK * NDW_CHUNK;
   w.splits = (int)((n + per - 1) / per);
   w.per_split = per;
   w.partial = off;
-  off += align256(std::max((size_t)5 * w.splits * NGP_DW_PM * NGP_DW_PK, (size_t)NDW_TASKS * w.splits * NDW_PART) * 4);
+  off += align256((size_t)NDW_TASKS * w.splits * NDW_PART * 4);
   w.total = off;
   return w;
 }
@@ -1427,14 +1437,10 @@ int den_ngp_fwd(const den_ngp_desc* desc, int64_t n, int32_t points, const float
   A.out_sigma = out_sigma;
   A.ld = ngp_ld(n);
   A.save = train ? (float*)((char*)workspace + ngp_ws(n).save) : nullptr;
-#if DEN_NGP_MFMA
   if (A.hidden_relu)
     hipLaunchKernelGGL(ngp_fwd_mfma_kernel<true>, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, (hipStream_t)stream, A);
   else
     hipLaunchKernelGGL(ngp_fwd_mfma_kernel<false>, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, (hipStream_t)stream, A);
-#else
-  hipLaunchKernelGGL(ngp_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
-#endif
   DEN_LAUNCHED();
   return DEN_OK;
 }
@@ -1468,23 +1474,16 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
   A.d_sigma = d_sigma;
   A.d_table = grad_params;
   A.dz = (float*)(ws + W.dz);
-#if DEN_NGP_MFMA
   if (A.hidden_relu)
     hipLaunchKernelGGL(ngp_bwd_mfma_kernel<true>, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, st, A);
   else
     hipLaunchKernelGGL(ngp_bwd_mfma_kernel<false>, dim3(ngp_mf_grid(n)), dim3(NM_THREADS), 0, st, A);
-#if DEN_NGP_SCATTER_LDS
   DEN_LAUNCHED();
   hipLaunchKernelGGL(ngp_scatter_kernel, dim3((unsigned)((n + NSC_THREADS - 1) / NSC_THREADS)), dim3(NSC_THREADS), 0, st,
                      A);
-#endif
-#else
-  hipLaunchKernelGGL(ngp_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
-#endif
   DEN_LAUNCHED();
   const int rd = desc->radiance_dim;
   const NgpOff& O = A.off;
-#if DEN_NGP_DW_MFMA
   NgpDwMfArgs Q{};
   Q.dz = A.dz;
   Q.save = A.save;
@@ -1509,26 +1508,6 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
   DEN_LAUNCHED();
   hipLaunchKernelGGL(ngp_dw_mfma_reduce_kernel, dim3((NDW_PART + 63) / 64, NDW_TASKS), dim3(256), 0, st, Q);
   DEN_LAUNCHED();
-#else
-  NgpDwArgs P{};
-  P.dz = A.dz;
-  P.save = A.save;
-  P.n = n;
-  P.ld = A.ld;
-  P.per_split = W.per_split;
-  P.splits = W.splits;
-  P.partial = (float*)(ws + W.partial);
-  P.grad = grad_params + tfl;
-  P.L[0] = NgpDwLayer{ND_Z0, NGP_W, NS_FEAT, A.enc, O.w[0], O.b[0]};
-  P.L[1] = NgpDwLayer{ND_O, 1 + NGP_GEO, NS_H0, NGP_W, O.w[1], O.b[1]};
-  P.L[2] = NgpDwLayer{ND_Z2, NGP_W, NS_HIN, NGP_HIN, O.w[2], O.b[2]};
-  P.L[3] = NgpDwLayer{ND_Z3, NGP_W, NS_H1, NGP_W, O.w[3], O.b[3]};
-  P.L[4] = NgpDwLayer{ND_R, rd, NS_H2, NGP_W, O.w[4], O.b[4]};
-  hipLaunchKernelGGL(ngp_dw_kernel, dim3((unsigned)W.splits, 5), dim3(256), 0, st, P);
-  DEN_LAUNCHED();
-  hipLaunchKernelGGL(ngp_dw_reduce_kernel, dim3((NGP_DW_PM * NGP_DW_PK + 255) / 256, 5), dim3(256), 0, st, P);
-  DEN_LAUNCHED();
-#endif
   return DEN_OK;
 }
 
@@ -1540,9 +1519,6 @@ int den_ngp_ray_grad(const den_ngp_desc* desc, int64_t n, int32_t points, int32_
   NgpGrid g;
   int64_t tfl;
   if (!ngp_grid(desc, &g, &tfl)) return fail(DEN_EUNSUPPORTED, "unsupported ngp descriptor");
-#if !(DEN_NGP_MFMA && DEN_NGP_SCATTER_LDS)
-  return fail(DEN_EUNSUPPORTED, "the ngp ray gradient reads the encoding-gradient rows of the MFMA backward");
-#endif
   if (n < 0 || (points != 1 && points != 2) || !params || !workspace || !d_x || !d_d || (n > 0 && !rg_workspace) ||
       (n > 0 && (!x || !d)) || (points == 2 && (n_rays <= 0 || (n > 0 && (!ray_idx || !t0 || !t1)))))
     return fail(DEN_EINVAL, "bad arguments");

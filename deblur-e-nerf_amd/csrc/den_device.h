@@ -78,33 +78,18 @@ __device__ __forceinline__ typename Tr<MODE>::Acc acc_zero() {
 // so every store / load instruction of a wave moves 1 KiB of consecutive bytes.
 // `tile` is the (wave-uniform) base of the tile; each lane adds its own offset.
 
-// BF16 hidden softplus as log2(1 + 2^t) (softplus2_scaled)
-#ifndef DEN_SP_DIRECT
-#define DEN_SP_DIRECT 0
-#endif
 // Activation / dz tiles are written once and read once, by a later kernel, after far more data
-// than the caches hold: BF16 stores and loads of them go non-temporal (DEN_NT_STREAMS).
-#ifndef DEN_NT_STREAMS
-#define DEN_NT_STREAMS 1
-#endif
+// than the caches hold: BF16 stores and loads of them go non-temporal.
 typedef unsigned int den_u32x4 __attribute__((ext_vector_type(4)));
 template <typename V>
 __device__ __forceinline__ void st_stream(V* p, V v) {
-#if DEN_NT_STREAMS
   static_assert(sizeof(V) == 16, "16-byte streams");
   __builtin_nontemporal_store(__builtin_bit_cast(den_u32x4, v), (den_u32x4*)p);
-#else
-  *p = v;
-#endif
 }
 template <typename V>
 __device__ __forceinline__ V ld_stream(const V* p) {
-#if DEN_NT_STREAMS
   static_assert(sizeof(V) == 16, "16-byte streams");
   return __builtin_bit_cast(V, __builtin_nontemporal_load((const den_u32x4*)p));
-#else
-  return *p;
-#endif
 }
 
 // Store a lane's operand fragments of one tile (stored order: regs 0..REGS-1).
@@ -176,16 +161,8 @@ __device__ __forceinline__ float dsoftplus_b100_from_out(float s) {
 // max(t, 0) as v_med3_f32(t, 0, FLT_MAX): fmaxf lowers to maxnum, which makes the compiler
 // canonicalize an MFMA result first (a second v_max_f32 per element in the forward epilogue).
 __device__ __forceinline__ float softplus2_scaled(float t) {
-#ifdef DEN_EXP_CHEAP_ACT  // measurement experiment only (never in libden.so): VALU cost of the epilogue
-  return __builtin_amdgcn_fmed3f(t, 0.0f, 3.4028235e38f);
-#elif DEN_SP_DIRECT  // default; 0: the max + log1p form (r03 A/B: render_fwd 24.9 -> 24.0 ms per step)
-  // log2(1 + 2^t) directly, t clamped below the exp2 overflow (for t > 24 the sum rounds to 2^t and
-  // the log returns t): one VALU op per element fewer than the max + log1p form
-  return __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(t, -3.4028235e38f, 64.0f)));
-#else
   return __builtin_amdgcn_fmed3f(t, 0.0f, 3.4028235e38f) +
          __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(-fabsf(t)));
-#endif
 }
 // its derivative from the output: sigmoid(100 z) = 1 - 2^-s'
 __device__ __forceinline__ float dsoftplus2_scaled_from_out(float s) { return 1.0f - __builtin_amdgcn_exp2f(-s); }

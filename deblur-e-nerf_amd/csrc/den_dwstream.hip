@@ -19,33 +19,15 @@
 // bottleneck_layer, rgb_layer.* (external/mlp.py:99-113, 193-205).
 // Included by den_api.hip after den_hidden.hip (hb_slot, hb_tr_frag, hb_wait_vm_lgkm0, HB_TILE).
 
-// waves per workgroup of the streamed weight-gradient launches {L0 + L5 pe}, Lg, Lr
-#ifndef DEN_DWS_NW1
-#define DEN_DWS_NW1 16  // r02 A/B: streamed dW 13.0-13.35 ms per step (4 waves), 11.2 (8), 10.8 (16, with NW3)
-#endif
-#ifndef DEN_DWS_NW2
-#define DEN_DWS_NW2 8
-#endif
-#ifndef DEN_DWS_NW3
-#define DEN_DWS_NW3 16
-#endif
-#ifndef DEN_DWS_NW4
-#define DEN_DWS_NW4 4
-#endif
-#ifndef DEN_DWS_D4
-#define DEN_DWS_D4 3  // ring steps in flight of the Lr launch (U4 x 10 KiB each)
-#endif
-#ifndef DEN_DWS_U4
-#define DEN_DWS_U4 4  // wave blocks per ring step of the Lr launch (r03 A/B: U 1 -> 4 with U3 2: 7.6 -> 6.6 ms per step)
-#endif
-#ifndef DEN_DWS_D3
-#define DEN_DWS_D3 2  // ring steps in flight of the Lg launch (U3 x 26 KiB each)
-#endif
-#ifndef DEN_DWS_U3
-#define DEN_DWS_U3 2  // wave blocks per ring step of the Lg launch
-#endif
-
 namespace den {
+
+// waves per workgroup of the streamed weight-gradient launches {L0 + L5 pe}, Lb, Lg, Lr, and the
+// ring shapes of the Lg / Lr launches (r02 / r03 A/B, profiles/r0{2,3}_*experiments.txt: 4 -> 16
+// waves took the {L0 + L5 pe} / Lg launches from 13.0 to 10.8 ms per step; U = 4 wave blocks per Lr
+// ring step with 3 steps in flight and U = 2 with 2 for Lg, 7.6 -> 6.6 ms)
+constexpr int DWS_NW1 = 16, DWS_NW2 = 8, DWS_NW3 = 16, DWS_NW4 = 4;
+constexpr int DWS_D3 = 2, DWS_U3 = 2;  // Lg: ring steps in flight, wave blocks per step (26 KiB each)
+constexpr int DWS_D4 = 3, DWS_U4 = 4;  // Lr: the same (10 KiB each)
 
 struct DwStreamArgs {
   const char* a[2];     // dz tensors (wave-block major), row tiles [0, MA) from a[0], [MA, MT) from a[1]
@@ -191,9 +173,9 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
 }
 
 // the launches of a BF16 backward (Lb + sigma: DEN_LB_HIDDEN = 0 only)
-template __global__ void dwstream_kernel<8, 16, 2, 2, DEN_DWS_NW1, 3>(DwStreamArgs);  // L0 + L5 pe
-template __global__ void dwstream_kernel<9, 9, 8, 8, DEN_DWS_NW2, 3>(DwStreamArgs);    // Lb + sigma
-template __global__ void dwstream_kernel<4, 4, 8, 9, DEN_DWS_NW3, DEN_DWS_D3, DEN_DWS_U3>(DwStreamArgs);    // Lg
-template __global__ void dwstream_kernel<1, 1, 4, 4, DEN_DWS_NW4, DEN_DWS_D4, DEN_DWS_U4>(DwStreamArgs);  // Lr
+template __global__ void dwstream_kernel<8, 16, 2, 2, DWS_NW1, 3>(DwStreamArgs);  // L0 + L5 pe
+template __global__ void dwstream_kernel<9, 9, 8, 8, DWS_NW2, 3>(DwStreamArgs);    // Lb + sigma
+template __global__ void dwstream_kernel<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3>(DwStreamArgs);    // Lg
+template __global__ void dwstream_kernel<1, 1, 4, 4, DWS_NW4, DWS_D4, DWS_U4>(DwStreamArgs);  // Lr
 
 }  // namespace den

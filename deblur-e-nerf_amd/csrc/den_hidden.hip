@@ -26,24 +26,13 @@ constexpr int HB_THREADS = 64 * HB_WAVES;
 constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
 constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
 constexpr int HB_SIG = 256;            // LB: LDS bytes for sigma's bf16[32] dz of a block (aligned)
-#ifndef DEN_HB_GRID
-#define DEN_HB_GRID 256  // persistent workgroups (one per CU)
-#endif
-constexpr int HB_GRID_MAX = DEN_HB_GRID;
-#ifndef DEN_HB_NT
-#define DEN_HB_NT 1  // non-temporal dz_l / S'_{l-1} loads and dz_{l-1} stores (streamed once)
-#endif
-#ifndef DEN_HB_DEPTH
-#define DEN_HB_DEPTH 3
-#endif
-#ifndef DEN_HB_OVL
-#define DEN_HB_OVL 0  // epilogue / dW overlap: 0 phases apart, 1 compiler order, 2 pinned interleave
-#endif
-#ifndef DEN_HB_PF
-#define DEN_HB_PF 4  // dz_l fragments read ahead of the chain MFMAs
-#endif
-constexpr int HB_PF = DEN_HB_PF;
-constexpr int HB_DEPTH = DEN_HB_DEPTH;                   // blocks in flight ahead of the computed one
+// Measured (r02/r03): one persistent workgroup per CU; non-temporal dz_l / S'_{l-1}
+// loads and dz_{l-1} stores (streamed once; cached stores were slower); 3 blocks in flight (4 did not
+// help); dz_l fragments read 4 k-steps ahead; the epilogue and the dW MFMAs kept in separate phases
+// (overlapping them, in compiler order or a pinned interleave, was 1-2 ms per step slower).
+constexpr int HB_GRID_MAX = 256;  // persistent workgroups (one per CU)
+constexpr int HB_PF = 4;          // dz_l fragments read ahead of the chain MFMAs
+constexpr int HB_DEPTH = 3;       // blocks in flight ahead of the computed one
 constexpr int HB_RING = HB_DEPTH + 1;                    // LDS slots (32 KiB each, 33 for Lb; <= 4 fit in 160 KiB)
 constexpr int HB_STORE_OPS = 4;                          // dz_{l-1} stores per wave per block
 
@@ -95,13 +84,8 @@ __device__ __forceinline__ void hb_dma_untracked(const char* src, char* dst) {
     const int pc = __builtin_amdgcn_readfirstlane(q * HB_WAVES + wave);
     const char* base = src + pc * 1024;
     const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(dst + pc * 1024));
-#if DEN_HB_NT
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"((pc & 1) ? off1 : off0),
                  "s"(base), "s"(m0) : "memory", "m0");
-#else
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"((pc & 1) ? off1 : off0),
-                 "s"(base), "s"(m0) : "memory", "m0");
-#endif
   }
 }
 
@@ -223,18 +207,11 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     bf16x8 of[2];
     acc_to_frags<1>(acc, of);
     char* d = P.dz_out + (b * 8 + 2 * wave + t) * HB_TILE + lane * 16;  // dz_{l-1}: 8 tiles per block
-#if DEN_HB_NT
     __builtin_nontemporal_store(of[0], (bf16x8*)d);
     __builtin_nontemporal_store(of[1], (bf16x8*)(d + 1024));
-#else
-    *(bf16x8*)d = of[0];
-    *(bf16x8*)(d + 1024) = of[1];
-#endif
-#if DEN_HB_OVL == 0
     // keep the scheduler from hoisting the next phase's LDS reads here (register pressure: W^T lives
     // in 128 VGPRs and dW in all 256 AGPRs for the whole launch)
     __builtin_amdgcn_sched_barrier(0);
-#endif
   }
   // weight / bias gradients over the block's 32 samples (two k-steps of 16)
 #pragma unroll
@@ -256,17 +233,6 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
   // sigma's weight-gradient row last (placed between the chain and the epilogue or before the dW
   // MFMAs its operands spill registers or it measured slower: r03)
   if constexpr (LB) hb_sigma_dw(sig, sb, sacc);
-#if DEN_HB_OVL == 2
-  // one wave per SIMD issues in order: the epilogue's VALU (derivative, bf16 packing) only overlaps
-  // the weight-gradient MFMAs if it is interleaved with them in the instruction stream
-  __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);  // DS reads: epilogue operands + first fragments
-#pragma unroll
-  for (int q = 0; q < 32; ++q) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-    __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // VALU
-    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-  }
-#endif
 }
 
 template <bool LB>

@@ -139,16 +139,31 @@ __global__ __launch_bounds__(1024) void sum_partials_kernel(int n, int nb, const
 }
 
 // ------------------------------------------------------------------ event loss (loss.py:34-96)
-__device__ __forceinline__ float err_fn(int fn, float d) {
-  float ad = fabsf(d);
+// error functions of (input a, target t): 0 l1, 1 mse, 2 huber (delta 1), 3 mape (utils/modules.py:97-122:
+// |a - t| / max(|t|, eps), eps = the f64 machine epsilon)
+constexpr float MAPE_EPS = 2.220446049250313e-16f;
+__device__ __forceinline__ float sgnf(float d) { return d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f); }
+__device__ __forceinline__ float err_fn(int fn, float a, float t) {
+  const float d = a - t, ad = fabsf(d);
   if (fn == 0) return ad;                                   // l1
   if (fn == 1) return d * d;                                // mse
+  if (fn == 3) return ad / fmaxf(fabsf(t), MAPE_EPS);       // mape
   return ad < 1.0f ? 0.5f * d * d : (ad - 0.5f);            // huber, delta = 1
 }
-__device__ __forceinline__ float derr_fn(int fn, float d) {
-  if (fn == 0) return d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+// d err / d a
+__device__ __forceinline__ float derr_fn(int fn, float a, float t) {
+  const float d = a - t;
+  if (fn == 0) return sgnf(d);
   if (fn == 1) return 2.0f * d;
+  if (fn == 3) return sgnf(d) / fmaxf(fabsf(t), MAPE_EPS);
   return d < -1.0f ? -1.0f : (d > 1.0f ? 1.0f : d);
+}
+// d err / d t (torch's autograd: abs' gradient sign(x), clamp's passes where |t| >= eps)
+__device__ __forceinline__ float derr_dt_fn(int fn, float a, float t) {
+  if (fn != 3) return -derr_fn(fn, a, t);
+  const float m = fmaxf(fabsf(t), MAPE_EPS);
+  const float g = -sgnf(a - t) / m;
+  return fabsf(t) >= MAPE_EPS ? g - fabsf(a - t) * sgnf(t) / (m * m) : g;
 }
 
 constexpr int LOSS_BLOCK = 256;
@@ -162,7 +177,7 @@ __global__ void loss_partial_kernel(int N, int fn, const float* x, const float* 
   if (i < N && (!valid || valid[i])) {
     float a = x[i] / c[0];
     float t = target ? target[i] : 0.0f;
-    e = err_fn(fn, a - t);
+    e = err_fn(fn, a, t);
     k = 1.0f;
   }
   se[threadIdx.x] = e;
@@ -217,9 +232,9 @@ __global__ void loss_bwd_kernel(int N, int fn, const float* x, const float* targ
       float a = x[i] / cc;
       float t = target ? target[i] : 0.0f;
       float gerr = gout[0] / count[0];
-      float de = derr_fn(fn, a - t) * gerr;
+      float de = derr_fn(fn, a, t) * gerr;
       gx = de / cc;
-      gt = -de;
+      gt = derr_dt_fn(fn, a, t) * gerr;
       dcv = de * (-x[i] / (cc * cc));
     }
     dx[i] = gx;
@@ -284,12 +299,12 @@ __global__ void event_step_partial_kernel(EventStepArgs E) {
     const float c = E.c[0];
     if (ev_valid(E, 0, i)) {
       float x = ev_logI(E, 1, i) - ev_logI(E, 0, i);
-      v[0] = err_fn(E.fn_d, x / c - E.target[i]);
+      v[0] = err_fn(E.fn_d, x / c, E.target[i]);
       v[1] = 1.0f;
     }
     if (ev_valid(E, 2, i)) {
       float x = ev_logI(E, 3, i) - ev_logI(E, 2, i);
-      v[2] = err_fn(E.fn_t, x / c);
+      v[2] = err_fn(E.fn_t, x / c, 0.0f);
       v[3] = 1.0f;
     }
   }
@@ -337,13 +352,13 @@ __global__ void event_step_bwd_kernel(EventStepArgs E) {
   float dy[4] = {0.f, 0.f, 0.f, 0.f};
   if (ev_valid(E, 0, i)) {
     float x = ev_logI(E, 1, i) - ev_logI(E, 0, i);
-    float g = derr_fn(E.fn_d, x / c - E.target[i]) * (E.w_d / cnt_d) / c;
+    float g = derr_fn(E.fn_d, x / c, E.target[i]) * (E.w_d / cnt_d) / c;
     dy[1] = g;
     dy[0] = -g;
   }
   if (ev_valid(E, 2, i)) {
     float x = ev_logI(E, 3, i) - ev_logI(E, 2, i);
-    float g = derr_fn(E.fn_t, x / c) * (E.w_t / cnt_t) / c;
+    float g = derr_fn(E.fn_t, x / c, 0.0f) * (E.w_t / cnt_t) / c;
     dy[3] = g;
     dy[2] = -g;
   }

@@ -114,110 +114,6 @@ struct NgpArgs {
 };
 
 // ------------------------------------------------------------------ elementwise pieces
-// torch.nn.Softplus(beta, threshold = 20): x if beta x > 20 else log1p(exp(beta x)) / beta
-__device__ __forceinline__ float ngp_sp100(float x) {
-  const float bx = x * 100.0f;
-  return bx > 20.0f ? x : __fdiv_rn(log1pf(expf(bx)), 100.0f);
-}
-// its backward from the input: z = exp(beta x); beta x > 20 ? g : g z / (z + 1)
-__device__ __forceinline__ float ngp_dsp100(float x) {
-  const float bx = x * 100.0f;
-  if (bx > 20.0f) return 1.0f;
-  const float z = expf(bx);
-  return __fdiv_rn(z, z + 1.0f);
-}
-__device__ __forceinline__ float ngp_act(float x, int relu) { return relu ? fmaxf(x, 0.0f) : ngp_sp100(x); }
-__device__ __forceinline__ float ngp_dact(float pre, float out, int relu) {
-  return relu ? (out > 0.0f ? 1.0f : 0.0f) : ngp_dsp100(pre);
-}
-
-// The MLP weights are read through the constant address space: wave-uniform addresses there become
-// scalar loads into SGPR operands (through the generic / global space the compiler cannot prove the
-// stores of the kernel leave them unchanged, emits vector loads and runs out of VGPRs).
-typedef const __attribute__((address_space(4))) float* ngp_cptr;
-__device__ __forceinline__ ngp_cptr ngp_const(const float* p) { return (ngp_cptr)p; }
-
-// y = W x + b, W row-major (OUT, LD), first IN columns (uniform weights: scalar loads)
-template <int OUT, int IN, int LD, typename Ptr>
-__device__ __forceinline__ void ngp_linear(Ptr W, Ptr b, const float* x, float* y) {
-#pragma unroll
-  for (int o = 0; o < OUT; ++o) {
-    float acc = 0.0f;
-#pragma unroll
-    for (int i = 0; i < IN; ++i) acc = fmaf(W[o * LD + i], x[i], acc);
-    y[o] = acc + b[o];
-  }
-}
-// layer 0: the encoding width E = 2 n_levels <= NGP_ENC is a runtime (wave-uniform) row length
-template <typename Ptr>
-__device__ __forceinline__ void ngp_linear_enc(Ptr W, Ptr b, const float* x, float* y, int E, int LD) {
-#pragma unroll
-  for (int o = 0; o < NGP_W; ++o) {
-    float acc = 0.0f;
-#pragma unroll
-    for (int i = 0; i < NGP_ENC; ++i)
-      if (i < E) acc = fmaf(W[o * LD + i], x[i], acc);
-    y[o] = acc + b[o];
-  }
-}
-template <typename Ptr>
-__device__ __forceinline__ void ngp_linear_enc_t(Ptr W, const float* dy, float* dx, int E, int LD) {
-#pragma unroll
-  for (int i = 0; i < NGP_ENC; ++i) dx[i] = 0.0f;
-#pragma unroll
-  for (int o = 0; o < NGP_W; ++o)
-#pragma unroll
-    for (int i = 0; i < NGP_ENC; ++i)
-      if (i < E) dx[i] = fmaf(W[o * LD + i], dy[o], dx[i]);
-}
-
-// dx = W^T dy (OUT rows of W, first IN columns), rows streamed in order
-template <int OUT, int IN, int LD, typename Ptr>
-__device__ __forceinline__ void ngp_linear_t(Ptr W, const float* dy, float* dx) {
-#pragma unroll
-  for (int i = 0; i < IN; ++i) dx[i] = 0.0f;
-#pragma unroll
-  for (int o = 0; o < OUT; ++o)
-#pragma unroll
-    for (int i = 0; i < IN; ++i) dx[i] = fmaf(W[o * LD + i], dy[o], dx[i]);
-}
-
-// Where the MLP weights come from.  Default (DEN_NGP_LDS 0): wave-uniform scalar loads through the
-// constant address space (SGPR operands of v_fmac_f32).  DEN_NGP_LDS 1: an LDS image staged per
-// workgroup, rows padded to multiples of 4 floats (layer 0 to 32 columns, the 31-wide head input to
-// 32) and read as wave-wide broadcasts.  Measured (profiles/ngp_parts.py, 2^19 samples, synthetic.yaml
-// config): field forward 2.91 ms scalar vs 10.6 ms LDS, density-only 1.28 vs 2.60 ms -- the
-// broadcast reads occupy the LDS->VGPR path for every weight of every wave.
-#ifndef DEN_NGP_LDS
-#define DEN_NGP_LDS 0
-#endif
-constexpr int NL_W0 = 0, NL_B0 = NL_W0 + NGP_W * NGP_ENC;
-constexpr int NL_W1 = NL_B0 + NGP_W, NL_B1 = NL_W1 + (1 + NGP_GEO) * NGP_W;
-constexpr int NL_W2 = NL_B1 + 1 + NGP_GEO, NL_B2 = NL_W2 + NGP_W * 32;
-constexpr int NL_W3 = NL_B2 + NGP_W, NL_B3 = NL_W3 + NGP_W * NGP_W;
-constexpr int NL_W4 = NL_B3 + NGP_W, NL_B4 = NL_W4 + 3 * NGP_W;
-constexpr int NL_FLOATS = NL_B4 + 4;
-static_assert(NL_W1 % 4 == 0 && NL_W2 % 4 == 0 && NL_W3 % 4 == 0 && NL_W4 % 4 == 0, "b128-aligned rows");
-
-__device__ __forceinline__ void ngp_stage_layer(const float* __restrict__ g, int out, int in, int ld, float* lds) {
-  for (int q = threadIdx.x; q < out * ld; q += blockDim.x) {
-    const int o = q / ld, i = q - o * ld;
-    lds[q] = i < in ? g[o * in + i] : 0.0f;
-  }
-}
-__device__ __forceinline__ void ngp_stage(const float* __restrict__ mlp, const NgpOff& off, int E, int rd, float* wl) {
-  const int in[5] = {E, NGP_W, NGP_HIN, NGP_W, NGP_W};
-  const int out[5] = {NGP_W, 1 + NGP_GEO, NGP_W, NGP_W, rd};
-  const int ld[5] = {NGP_ENC, NGP_W, 32, NGP_W, NGP_W};
-  const int lw[5] = {NL_W0, NL_W1, NL_W2, NL_W3, NL_W4};
-  const int lb[5] = {NL_B0, NL_B1, NL_B2, NL_B3, NL_B4};
-#pragma unroll
-  for (int l = 0; l < 5; ++l) {
-    ngp_stage_layer(mlp + off.w[l], out[l], in[l], ld[l], wl + lw[l]);
-    for (int q = threadIdx.x; q < out[l]; q += blockDim.x) wl[lb[l] + q] = mlp[off.b[l] + q];
-  }
-  __syncthreads();
-}
 
 // SHEncoder (external/sh_encoder.py:27-80), degree 4, the reference's f32 operation order
 __device__ __forceinline__ void ngp_sh4(const float* dv, float* out) {
@@ -320,19 +216,14 @@ __device__ __forceinline__ void ngp_corners(const NgpGrid& G, int l, const float
 
 // Pre-aggregation of the table-gradient scatter: the samples of a wave are consecutive samples of
 // the packed rays, so at the coarse levels neighbouring lanes sit in the same cell and add to the
-// same 8 entries.  In steps k = 0 .. DEN_NGP_AGG_STEPS - 1, the lane with the k + 1 low bits clear
+// same 8 entries.  In steps k = 0 .. NGP_AGG_STEPS - 1, the lane with the k + 1 low bits clear
 // folds in the 16 values of lane + 2^k when both hold the same base cell (lane ^ 1, ^ 2 by DPP
 // quad_perm, ^ 4, ^ 8, ^ 16 by ds_swizzle bit mode); only lanes that were not folded issue atomics.
 // Equal cells give identical corner indices, so the fold is exact (another summation order of the
 // same terms, like the atomics themselves).  Measured on the configs[3] emulation (ray-ordered
 // samples): 1.19 -> 0.88 s per optimizer step with quads at every level, 0.84 with 16-lane groups; no
 // cost on unordered points (profiles/ngp_bench.py).
-#ifndef DEN_NGP_AGG_RES
-#define DEN_NGP_AGG_RES 0x7FFFFFFF  // levels with resolution <= this fold (all); 0: off
-#endif
-#ifndef DEN_NGP_AGG_STEPS
-#define DEN_NGP_AGG_STEPS 4  // configs[3] emulation: 0.88 (2 steps) / 0.86 (3) / 0.84 (4) / 0.84 (5) s per step
-#endif
+constexpr int NGP_AGG_STEPS = 4;  // configs[3] emulation: 0.88 (2 steps) / 0.86 (3) / 0.84 (4) / 0.84 (5) s per step
 // value of lane ^ 2^K (K < 5: within 32 lanes); an inactive source yields `old`
 template <int K>
 __device__ __forceinline__ int ngp_xlane(int v, int old) {
@@ -361,10 +252,10 @@ __device__ __forceinline__ bool ngp_fold(const uint32_t* cell, float* v, bool ok
   bool alive = ok;
   const uint64_t active = __ballot(ok);
   ngp_fold_step<0>(cell, v, alive, active);
-  if constexpr (DEN_NGP_AGG_STEPS > 1) ngp_fold_step<1>(cell, v, alive, active);
-  if constexpr (DEN_NGP_AGG_STEPS > 2) ngp_fold_step<2>(cell, v, alive, active);
-  if constexpr (DEN_NGP_AGG_STEPS > 3) ngp_fold_step<3>(cell, v, alive, active);
-  if constexpr (DEN_NGP_AGG_STEPS > 4) ngp_fold_step<4>(cell, v, alive, active);
+  if constexpr (NGP_AGG_STEPS > 1) ngp_fold_step<1>(cell, v, alive, active);
+  if constexpr (NGP_AGG_STEPS > 2) ngp_fold_step<2>(cell, v, alive, active);
+  if constexpr (NGP_AGG_STEPS > 3) ngp_fold_step<3>(cell, v, alive, active);
+  if constexpr (NGP_AGG_STEPS > 4) ngp_fold_step<4>(cell, v, alive, active);
   return alive;
 }
 
@@ -418,217 +309,6 @@ __device__ __forceinline__ void ngp_point(const NgpArgs& A, int64_t i, float* xn
   contract_unit(pos, A.aabb, xn, sel, A.contraction);
 }
 
-// ------------------------------------------------------------------ forward
-#if DEN_NGP_LDS
-#define NGP_W_(l) (wl + NL_W##l)
-#define NGP_B_(l) (wl + NL_B##l)
-#define NGP_LD0 NGP_ENC
-#define NGP_LD2 32
-#else
-#define NGP_W_(l) (P + A.off.w[l])
-#define NGP_B_(l) (P + A.off.b[l])
-#define NGP_LD0 A.enc
-#define NGP_LD2 NGP_HIN
-#endif
-
-__global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpArgs A) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-#if DEN_NGP_LDS
-  __shared__ __attribute__((aligned(16))) float wl[NL_FLOATS];
-  ngp_stage(A.mlp, A.off, A.enc, A.rd, wl);
-#else
-  const ngp_cptr P = ngp_const(A.mlp);
-#endif
-  if (i >= A.n) return;
-  float xn[3], sel, dir[3];
-  ngp_point(A, i, xn, &sel, dir);
-  float feat[NGP_ENC];
-  ngp_encode(A.grid, A.table, xn, feat);
-  const int relu = A.hidden_relu;
-  float* S = A.save;
-  const int64_t ld = A.ld;
-  if (S) {
-#pragma unroll
-    for (int f = 0; f < NGP_ENC; ++f)
-      if (f < A.enc) S[(NS_FEAT + f) * ld + i] = feat[f];
-  }
-  float h0[NGP_W];
-  {
-    float h0p[NGP_W];
-    ngp_linear_enc(NGP_W_(0), NGP_B_(0), feat, h0p, A.enc, NGP_LD0);
-#pragma unroll
-    for (int o = 0; o < NGP_W; ++o) h0[o] = ngp_act(h0p[o], relu);
-    if (S) {
-#pragma unroll
-      for (int o = 0; o < NGP_W; ++o) {
-        S[(NS_H0P + o) * ld + i] = h0p[o];
-        S[(NS_H0 + o) * ld + i] = h0[o];
-      }
-    }
-  }
-  float ob[1 + NGP_GEO];
-  ngp_linear<1 + NGP_GEO, NGP_W, NGP_W>(NGP_W_(1), NGP_B_(1), h0, ob);
-  // shifted_trunc_exp(o0) * selector; selected (not multiplied) so an overflow outside the box is 0
-  const float sigma = sel != 0.0f ? expf(ob[0] - 1.0f) : 0.0f;
-  A.out_sigma[i] = sigma;
-  if (S) {
-    S[NS_O0 * ld + i] = ob[0];
-    S[NS_SEL * ld + i] = sel;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) S[(NS_X + a) * ld + i] = xn[a];
-  }
-  if (A.density_only) return;
-  float hin[NGP_HIN];
-  ngp_sh4(dir, hin);
-#pragma unroll
-  for (int g = 0; g < NGP_GEO; ++g) hin[NGP_SH + g] = ob[1 + g];
-  if (S) {
-#pragma unroll
-    for (int f = 0; f < NGP_HIN; ++f) S[(NS_HIN + f) * ld + i] = hin[f];
-  }
-  // each layer's saved rows are stored as soon as it is computed (keeps them out of VGPRs)
-  float h1[NGP_W];
-  {
-    float h1p[NGP_W];
-    ngp_linear<NGP_W, NGP_HIN, NGP_LD2>(NGP_W_(2), NGP_B_(2), hin, h1p);
-#pragma unroll
-    for (int o = 0; o < NGP_W; ++o) h1[o] = ngp_act(h1p[o], relu);
-    if (S) {
-#pragma unroll
-      for (int o = 0; o < NGP_W; ++o) {
-        S[(NS_H1P + o) * ld + i] = h1p[o];
-        S[(NS_H1 + o) * ld + i] = h1[o];
-      }
-    }
-  }
-  float h2[NGP_W];
-  {
-    float h2p[NGP_W];
-    ngp_linear<NGP_W, NGP_W, NGP_W>(NGP_W_(3), NGP_B_(3), h1, h2p);
-#pragma unroll
-    for (int o = 0; o < NGP_W; ++o) h2[o] = ngp_act(h2p[o], relu);
-    if (S) {
-#pragma unroll
-      for (int o = 0; o < NGP_W; ++o) {
-        S[(NS_H2P + o) * ld + i] = h2p[o];
-        S[(NS_H2 + o) * ld + i] = h2[o];
-      }
-    }
-  }
-  float r[3] = {0.f, 0.f, 0.f};
-  if (A.rd == 3) ngp_linear<3, NGP_W, NGP_W>(NGP_W_(4), NGP_B_(4), h2, r);
-  else ngp_linear<1, NGP_W, NGP_W>(NGP_W_(4), NGP_B_(4), h2, r);
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    if (c < A.rd) {
-      const float v = A.rad_sigmoid ? __fdiv_rn(1.0f, 1.0f + expf(-r[c])) : (r[c] > 20.0f ? r[c] : log1pf(expf(r[c])));
-      A.out_rgb[i * A.rd + c] = v;
-    }
-    if (S) S[(NS_R + c) * ld + i] = r[c];
-  }
-}
-
-// ------------------------------------------------------------------ backward (per sample)
-// -> the pre-activation gradient of every layer (rows of A.dz) and the hash-table gradient
-// (tcnn kernel_grid_backward: atomicAdd of weight * dy per corner and feature)
-__global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpArgs A) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-#if DEN_NGP_LDS
-  __shared__ __attribute__((aligned(16))) float wl[NL_FLOATS];
-  ngp_stage(A.mlp, A.off, A.enc, A.rd, wl);
-#else
-  const ngp_cptr P = ngp_const(A.mlp);
-#endif
-  if (i >= A.n) return;
-  const float* S = A.save;
-  const int64_t ld = A.ld;
-  const int relu = A.hidden_relu;
-  float* D = A.dz;
-  // radiance activation
-  float dr[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    if (c >= A.rd) break;
-    const float g = A.d_rgb ? A.d_rgb[i * A.rd + c] : 0.0f;
-    const float rv = S[(NS_R + c) * ld + i];
-    if (A.rad_sigmoid) {
-      const float s = __fdiv_rn(1.0f, 1.0f + expf(-rv));
-      dr[c] = g * (s * (1.0f - s));
-    } else {
-      const float z = expf(rv);
-      dr[c] = rv > 20.0f ? g : g * __fdiv_rn(z, z + 1.0f);
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < 3; ++c) D[(ND_R + c) * ld + i] = dr[c];
-  // head output layer -> h2 -> h1 -> head input
-  float dh[NGP_W], dz[NGP_W];
-  if (A.rd == 3) ngp_linear_t<3, NGP_W, NGP_W>(NGP_W_(4), dr, dh);
-  else ngp_linear_t<1, NGP_W, NGP_W>(NGP_W_(4), dr, dh);
-#pragma unroll
-  for (int o = 0; o < NGP_W; ++o) {
-    dz[o] = dh[o] * ngp_dact(S[(NS_H2P + o) * ld + i], S[(NS_H2 + o) * ld + i], relu);
-    D[(ND_Z3 + o) * ld + i] = dz[o];
-  }
-  ngp_linear_t<NGP_W, NGP_W, NGP_W>(NGP_W_(3), dz, dh);
-#pragma unroll
-  for (int o = 0; o < NGP_W; ++o) {
-    dz[o] = dh[o] * ngp_dact(S[(NS_H1P + o) * ld + i], S[(NS_H1 + o) * ld + i], relu);
-    D[(ND_Z2 + o) * ld + i] = dz[o];
-  }
-  float dhin[NGP_HIN];
-  ngp_linear_t<NGP_W, NGP_HIN, NGP_LD2>(NGP_W_(2), dz, dhin);
-  // base output: density (trunc_exp backward clamps the exponent at 15) and the geo features
-  float dob[1 + NGP_GEO];
-  {
-    const float gs = A.d_sigma ? A.d_sigma[i] : 0.0f;
-    const float sel = S[NS_SEL * ld + i];
-    const float o0 = S[NS_O0 * ld + i];
-    dob[0] = sel != 0.0f ? gs * expf(fminf(o0 - 1.0f, 15.0f)) : 0.0f;
-  }
-#pragma unroll
-  for (int g = 0; g < NGP_GEO; ++g) dob[1 + g] = dhin[NGP_SH + g];
-#pragma unroll
-  for (int o = 0; o < 1 + NGP_GEO; ++o) D[(ND_O + o) * ld + i] = dob[o];
-  ngp_linear_t<1 + NGP_GEO, NGP_W, NGP_W>(NGP_W_(1), dob, dh);
-#pragma unroll
-  for (int o = 0; o < NGP_W; ++o) {
-    dz[o] = dh[o] * ngp_dact(S[(NS_H0P + o) * ld + i], S[(NS_H0 + o) * ld + i], relu);
-    D[(ND_Z0 + o) * ld + i] = dz[o];
-  }
-  float dfeat[NGP_ENC];
-  ngp_linear_enc_t(NGP_W_(0), dz, dfeat, A.enc, NGP_LD0);
-  // hash-table scatter
-  float xn[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) xn[a] = S[(NS_X + a) * ld + i];
-  for (int l = 0; l < A.grid.n_levels; ++l) {
-    NgpCorner C;
-    uint32_t cell[3];
-    ngp_corners(A.grid, l, xn, C, cell);
-    const float g0 = dfeat[2 * l], g1 = dfeat[2 * l + 1];
-    float v[16];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      v[2 * c] = C.w[c] * g0;
-      v[2 * c + 1] = C.w[c] * g1;
-    }
-    bool emit = true;
-#if DEN_NGP_AGG_RES > 0
-    // (a lane past n returned above: its partner reads it as a missing cell, see ngp_fold_step)
-    if (A.grid.res[l] <= (uint32_t)DEN_NGP_AGG_RES) emit = ngp_fold(cell, v);
-#endif
-    if (emit) {
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        float* t = A.d_table + 2 * (int64_t)C.idx[c];
-        unsafeAtomicAdd(t, v[2 * c]);
-        unsafeAtomicAdd(t + 1, v[2 * c + 1]);
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------ standalone encoding (tcnn.Encoding)
 struct NgpEncArgs {
   int64_t n;
@@ -666,105 +346,6 @@ __global__ __launch_bounds__(256) void ngp_encode_bwd_kernel(NgpEncArgs E) {
       unsafeAtomicAdd(t + 1, C.w[c] * g1);
     }
   }
-}
-
-// ------------------------------------------------------------------ weight gradients
-// dW[o][k] = sum_s dZ[o][s] X[k][s], db[o] = sum_s dZ[o][s] for the five layers, split-K over
-// samples: workgroup (split, layer) stages 64-sample chunks of its dZ and X rows sample-major in
-// LDS ([s][row], 4-row groups contiguous for ds_read_b128; a ones row gives the bias) and each lane
-// accumulates 4 x 4 output blocks.  Partials [layer][split][64][65] reduced in a fixed order.
-constexpr int NGP_DW_CHUNK = 64, NGP_DW_LD = 68, NGP_DW_PM = 64, NGP_DW_PK = 65;
-
-struct NgpDwLayer {
-  int a_row, m;   // dZ rows
-  int b_row, k;   // X rows (saved activations)
-  int64_t w_off;  // weight / bias offsets in the flat gradient
-  int64_t b_off;
-};
-struct NgpDwArgs {
-  const float* dz;
-  const float* save;
-  int64_t n;
-  int64_t ld;  // row stride
-  int64_t per_split;
-  int splits;
-  NgpDwLayer L[5];
-  float* partial;  // [5][splits][64][65]
-  float* grad;
-};
-
-__global__ __launch_bounds__(256) void ngp_dw_kernel(NgpDwArgs P) {
-  __shared__ __attribute__((aligned(16))) float sa[NGP_DW_CHUNK * NGP_DW_LD];
-  __shared__ __attribute__((aligned(16))) float sb[NGP_DW_CHUNK * NGP_DW_LD];
-  const NgpDwLayer L = P.L[blockIdx.y];
-  const int tid = threadIdx.x;
-  const int MG = (L.m + 3) / 4, KG = (L.k + 1 + 3) / 4;  // + the ones column
-  const int T = MG * KG;
-  float acc[2][16];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[u][e] = 0.0f;
-  const int64_t s0 = (int64_t)blockIdx.x * P.per_split;
-  const int64_t s1 = s0 + P.per_split < P.n ? s0 + P.per_split : P.n;
-  for (int64_t c0 = s0; c0 < s1; c0 += NGP_DW_CHUNK) {
-    __syncthreads();
-    // stage: lane (s = tid & 63) of row group (tid >> 6) -- coalesced over samples
-    for (int r = tid >> 6; r < NGP_DW_LD; r += 4) {
-      const int s = tid & 63;
-      const int64_t si = c0 + s;
-      const bool ok = si < s1;
-      float va = 0.0f, vb = 0.0f;
-      if (r < L.m && ok) va = P.dz[(int64_t)(L.a_row + r) * P.ld + si];
-      if (r < L.k && ok) vb = P.save[(int64_t)(L.b_row + r) * P.ld + si];
-      else if (r == L.k && ok) vb = 1.0f;
-      sa[s * NGP_DW_LD + r] = va;
-      sb[s * NGP_DW_LD + r] = vb;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int t = tid + u * 256;
-      if (t < T) {
-        const int og = t / KG, kg = t % KG;
-        for (int s = 0; s < NGP_DW_CHUNK; ++s) {
-          const f32x4 a = *(const f32x4*)(sa + s * NGP_DW_LD + 4 * og);
-          const f32x4 b = *(const f32x4*)(sb + s * NGP_DW_LD + 4 * kg);
-#pragma unroll
-          for (int p = 0; p < 4; ++p)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[u][4 * p + q] = fmaf(a[p], b[q], acc[u][4 * p + q]);
-        }
-      }
-    }
-  }
-  float* out = P.partial + ((int64_t)blockIdx.y * P.splits + blockIdx.x) * NGP_DW_PM * NGP_DW_PK;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int t = tid + u * 256;
-    if (t < T) {
-      const int og = t / KG, kg = t % KG;
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int o = 4 * og + p, k = 4 * kg + q;
-          if (o < L.m && k <= L.k) out[o * NGP_DW_PK + k] = acc[u][4 * p + q];
-        }
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void ngp_dw_reduce_kernel(NgpDwArgs P) {
-  const NgpDwLayer L = P.L[blockIdx.y];
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= L.m * (L.k + 1)) return;
-  const int o = e / (L.k + 1), k = e % (L.k + 1);
-  const float* src = P.partial + (int64_t)blockIdx.y * P.splits * NGP_DW_PM * NGP_DW_PK + o * NGP_DW_PK + k;
-  float s = 0.0f;
-  for (int sp = 0; sp < P.splits; ++sp) s += src[(int64_t)sp * NGP_DW_PM * NGP_DW_PK];
-  if (k < L.k) P.grad[L.w_off + (int64_t)o * L.k + k] = s;
-  else P.grad[L.b_off + o] = s;
 }
 
 }  // namespace den

@@ -1,9 +1,8 @@
 // den_ngp_mfma.hip -- the `ngp` field's MLPs on the matrix cores: v_mfma_f32_32x32x2_f32 (f32
-// operands, f32 accumulation, exact f32 products), forward and backward.  Same inputs, saved rows
-// and outputs as ngp_fwd_kernel / ngp_bwd_kernel (den_ngp.hip), which stay as the DEN_NGP_MFMA 0
-// build.
+// operands, f32 accumulation, exact f32 products), forward and backward.
 //
-// Why: the per-lane formulation runs the 9.3 K MACs per sample as v_fmac_f32 with scalar weight
+// Why: a per-lane formulation (measured in r02 and removed: 13.1 vs 3.5 ms fwd + bwd per 2^19
+// samples) runs the 9.3 K MACs per sample as v_fmac_f32 with scalar weight
 // operands -- one FMA per lane per instruction behind a stream of scalar loads -- and measured
 // ~4 TF/s on the head MLP.  Here a wave owns 32 samples; features are the M (row) dimension, the 32
 // samples the N (column) dimension, and the weights the A operand:
@@ -23,41 +22,18 @@
 
 namespace den {
 
-#ifndef DEN_NGP_MFMA
-#define DEN_NGP_MFMA 1
-#endif
-#ifndef DEN_NGP_SAVE_PRE
-#define DEN_NGP_SAVE_PRE 0  // 1: store the hidden pre-activations too (the VALU kernels' derivative)
-#endif
-#ifndef DEN_NGP_EXP_NO_ATOMIC
-#define DEN_NGP_EXP_NO_ATOMIC 0  // experiment builds (wrong results): cost of the scatter / the gathers
-#endif
-#ifndef DEN_NGP_EXP_LOCAL_GATHER
-#define DEN_NGP_EXP_LOCAL_GATHER 0
-#endif
-#ifndef DEN_NGP_SCATTER_LDS
-#define DEN_NGP_SCATTER_LDS 1  // table gradient through ngp_scatter_kernel (0: in the backward kernel)
-#endif
-#ifndef DEN_NGP_MF_WAVES
-#define DEN_NGP_MF_WAVES 8  // waves (32-sample tiles in flight) per workgroup
-#endif
-#ifndef DEN_NGP_MF_OCC
-#define DEN_NGP_MF_OCC 4  // waves per SIMD the field kernels are compiled for (128 VGPRs; 2 / 3 measured slower)
-#endif
-#ifndef DEN_NGP_MF_GRID
-#define DEN_NGP_MF_GRID 512  // workgroups at most: 2 resident per CU, each loops over tiles (1024 / 2048 / 4096 measured slower)
-#endif
-constexpr int NM_WAVES = DEN_NGP_MF_WAVES, NM_THREADS = 64 * NM_WAVES;
+// Measured (r02): 8-wave workgroups (32-sample tiles in flight), compiled for 4 waves per
+// SIMD (128 VGPRs; 2 / 3 were slower), at most 512 workgroups looping over tiles (2 resident per CU;
+// 1024 / 2048 / 4096 were slower); the table gradient aggregated by ngp_scatter_kernel.
+constexpr int NM_WAVES = 8, NM_THREADS = 64 * NM_WAVES;
+constexpr int NM_OCC = 4;      // waves per SIMD the field kernels are compiled for
+constexpr int NM_GRID = 512;   // workgroups at most
 
-// Activations of the MFMA kernels.  DEN_NGP_FAST_ACT 1: softplus(beta = 100) with torch's threshold as
+// Activations of the MFMA kernels: softplus(beta = 100) with torch's threshold as
 // max(bx, 0) + log1p(exp(-|bx|)) from the hardware exp2 / log2 with log1p(t) = log(1 + t) t / ((1 + t) - 1)
 // (Goldberg) and a multiply by 0.01; its derivative from the output y as -expm1(-100 y) with
 // expm1(z) = (e^z - 1) z / log(e^z) (Kahan).  A few ulps from the libm forms (which cost ~50 VALU
-// instructions per element with the IEEE division); 0: torch's operation order (ngp_sp100 /
-// ngp_dsp100_out).
-#ifndef DEN_NGP_FAST_ACT
-#define DEN_NGP_FAST_ACT 1
-#endif
+// instructions per element with the IEEE division).
 __device__ __forceinline__ float ngp_sp100_fast(float x) {
   const float bx = x * 100.0f;
   const float t = __expf(-fabsf(bx));
@@ -75,7 +51,7 @@ __device__ __forceinline__ float ngp_dsp100_out_fast(float y) {
 template <bool RELU>
 __device__ __forceinline__ float ngp_act_t(float x) {
   if constexpr (RELU) return fmaxf(x, 0.0f);
-  else return DEN_NGP_FAST_ACT ? ngp_sp100_fast(x) : ngp_sp100(x);
+  else return ngp_sp100_fast(x);
 }
 
 // accumulator register r of half h holds row ngp_row(r, h) of its 32-row tile
@@ -213,7 +189,7 @@ __device__ __forceinline__ NgpLevel ngp_level_h(const NgpGrid& G, int q, int l1,
 
 // ------------------------------------------------------------------ forward
 template <bool RELU>
-__global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kernel(NgpArgs A) {
+__global__ __launch_bounds__(NM_THREADS, NM_OCC) void ngp_fwd_mfma_kernel(NgpArgs A) {
   __shared__ __attribute__((aligned(16))) float img[FI_FLOATS];
   const int E = A.enc, L = A.grid.n_levels, L0 = (L + 1) / 2;
   for (int q = threadIdx.x; q < FI_FLOATS; q += NM_THREADS) img[q] = ngp_fi(A.mlp, A.off, E, L0, A.rd, q);
@@ -247,7 +223,7 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kerne
         float2 v[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c)
-          v[c] = *(const float2*)(A.table + 2 * (int64_t)(DEN_NGP_EXP_LOCAL_GATHER ? (C.idx[c] & 4095) : C.idx[c]));
+          v[c] = *(const float2*)(A.table + 2 * (int64_t)C.idx[c]);
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
           f0 = fmaf(C.w[c], v[c].x, f0);
@@ -275,7 +251,6 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kerne
           hb[16 * t + r] = a;
           if (S && ok) {
             const int row = 32 * t + ngp_row(r, 0);
-            if (DEN_NGP_SAVE_PRE) Sh[(NS_H0P + row) * nn] = pre;
             Sh[(NS_H0 + row) * nn] = a;
           }
         }
@@ -324,7 +299,6 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kerne
           hb[16 * t + r] = a;
           if (S && ok) {
             const int row = 32 * t + ngp_row(r, 0);
-            if (DEN_NGP_SAVE_PRE) Sh[(NS_H1P + row) * nn] = pre;
             Sh[(NS_H1 + row) * nn] = a;
           }
         }
@@ -340,7 +314,6 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kerne
           hb[16 * t + r] = a;
           if (S && ok) {
             const int row = 32 * t + ngp_row(r, 0);
-            if (DEN_NGP_SAVE_PRE) Sh[(NS_H2P + row) * nn] = pre;
             Sh[(NS_H2 + row) * nn] = a;
           }
         }
@@ -360,81 +333,19 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_fwd_mfma_kerne
   }
 }
 
-// ------------------------------------------------------------------ backward
-// Table-gradient scatter, transposed over quads of lanes.  Float atomics execute at the memory side,
-// one 64-B request per distinct 64-B segment an instruction touches (MI355X_MICROARCH.md 'Global
-// float atomics': ~20 G requests/s chip-wide), so one lane per sample adding to 8 random corners is
-// 16 requests per sample-level.  Here the 4 lanes of a quad issue, per instruction, the 4 dwords of
-// one x-neighbour corner pair (2k, 2k + 1) of ONE sample (lane q: corner 2k + (q >> 1), feature
-// q & 1): the two features of an entry are always one request, and the pair is one 16-B aligned run
-// whenever the two entries are adjacent (dense levels away from the wrap; hashed levels with an even
-// x cell) -- 4..8 requests per sample-level instead of 16.  The values, indices and emit flags are
-// exchanged with quad_perm DPP moves (lane q receives from lane q ^ r).
-#ifndef DEN_NGP_SCATTER_QUAD
-#define DEN_NGP_SCATTER_QUAD 1
-#endif
-template <int R>
-__device__ __forceinline__ int ngp_qxor(int v) {
-  if constexpr (R == 0) return v;
-  else return __builtin_amdgcn_update_dpp(v, v, R == 1 ? 0xB1 : R == 2 ? 0x4E : 0x1B, 0xF, 0xF, false);
-}
-template <typename T>
-__device__ __forceinline__ T ngp_sel4(T x0, T x1, T x2, T x3, int i) {
-  return i == 0 ? x0 : i == 1 ? x1 : i == 2 ? x2 : x3;
-}
-__device__ __forceinline__ void ngp_scatter_quad(float* d_table, const uint32_t* idx, const float* v, bool emit) {
-  const int q = threadIdx.x & 3;
-  // rv[r][k] = v_{q^r}[4k + q]; ri[r][k] = idx_{q^r}[2k + (q >> 1)]; re[r] = emit_{q^r}
-  float rv[4][4];
-  uint32_t ri[4][4];
-  int re[4];
-#define NGP_QX(R)                                                                                         \
-  {                                                                                                       \
-    const int dst = q ^ R;                                                                                \
-    _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                                       \
-      const float sv = ngp_sel4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3], dst);                 \
-      const uint32_t si = (dst >> 1) ? idx[2 * k + 1] : idx[2 * k];                                       \
-      rv[R][k] = __builtin_bit_cast(float, ngp_qxor<R>(__builtin_bit_cast(int, sv)));                     \
-      ri[R][k] = (uint32_t)ngp_qxor<R>((int)si);                                                          \
-    }                                                                                                     \
-    re[R] = ngp_qxor<R>(emit ? 1 : 0);                                                                    \
-  }
-  NGP_QX(0)
-  NGP_QX(1)
-  NGP_QX(2)
-  NGP_QX(3)
-#undef NGP_QX
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int r = q ^ s;  // sample s of the quad arrived through rotation q ^ s
-    if (ngp_sel4(re[0], re[1], re[2], re[3], r)) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t e = ngp_sel4(ri[0][k], ri[1][k], ri[2][k], ri[3][k], r);
-        const float val = ngp_sel4(rv[0][k], rv[1][k], rv[2][k], rv[3][k], r);
-        unsafeAtomicAdd(d_table + 2 * (int64_t)e + (q & 1), val);
-      }
-    }
-  }
-}
-
-// this lane's activation derivative of saved layer rows (pre-activation rows P, outputs Q)
-// DEN_NGP_SAVE_PRE 0: the softplus derivative from the saved OUTPUT y alone: exp(100 x) / (exp(100 x)
-// + 1) = 1 - exp(-100 y) = -expm1(-100 y), and 100 y > 20 exactly where 100 x > 20 (torch's
-// threshold; at the boundary both round to 1).  Saves and re-reads 192 rows (768 B) per sample less.
-__device__ __forceinline__ float ngp_dsp100_out(float y) {
-  const float by = y * 100.0f;
-  return by > 20.0f ? 1.0f : -expm1f(-by);
-}
+// this lane's activation derivative of saved layer rows (outputs at rows Q; the pre-activation rows
+// P of the save layout stay unwritten): the softplus derivative from the saved OUTPUT y alone,
+// exp(100 x) / (exp(100 x) + 1) = 1 - exp(-100 y) = -expm1(-100 y), and 100 y > 20 exactly where
+// 100 x > 20 (torch's threshold; at the boundary both round to 1) -- 192 rows (768 B) per sample
+// less to save and re-read than the pre-activations.
 template <bool RELU>
 __device__ __forceinline__ float ngp_dact_row(const float* S, int P, int Q, int row, int64_t n) {
   if constexpr (RELU) return S[(Q + row) * n] > 0.0f ? 1.0f : 0.0f;
-  if (DEN_NGP_SAVE_PRE) return ngp_dsp100(S[(P + row) * n]);
-  return DEN_NGP_FAST_ACT ? ngp_dsp100_out_fast(S[(Q + row) * n]) : ngp_dsp100_out(S[(Q + row) * n]);
+  return ngp_dsp100_out_fast(S[(Q + row) * n]);
 }
 
 template <bool RELU>
-__global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_bwd_mfma_kernel(NgpArgs A) {
+__global__ __launch_bounds__(NM_THREADS, NM_OCC) void ngp_bwd_mfma_kernel(NgpArgs A) {
   __shared__ __attribute__((aligned(16))) float img[BI_FLOATS];
   const int E = A.enc, L = A.grid.n_levels, rd = A.rd;
   for (int q = threadIdx.x; q < BI_FLOATS; q += NM_THREADS) img[q] = ngp_bi(A.mlp, A.off, E, rd, q);
@@ -528,56 +439,12 @@ __global__ __launch_bounds__(NM_THREADS, DEN_NGP_MF_OCC) void ngp_bwd_mfma_kerne
     }
     f32x16 df[1] = {ngp_zero16()};
     ngp_mm<1, 32>(img + BI_A0, dz, df, lane);
-#if DEN_NGP_SCATTER_LDS
     // the encoding gradient goes to ND_F rows; ngp_scatter_kernel aggregates and adds it
     if (ok) {
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         if (ngp_row(r, h) < E) Dh[(ND_F + ngp_row(r, 0)) * nn] = df[0][r];
     }
-    continue;
-#endif
-    // hash-table scatter: half h holds feature rows 2 l, 2 l + 1 of levels l = 4 a + 2 h + b
-    // (registers 4 a + 2 b, + 1)
-    float xn[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) xn[a] = S0[(NS_X + a) * nn];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int l = 4 * a + 2 * h + b;
-        if (l >= L) continue;
-        const NgpLevel V = ngp_level_h(A.grid, 4 * a + b, 4 * a + 2 + b, h);
-        NgpCorner C;
-        uint32_t cell[3];
-        ngp_corners(V, A.grid.hashed, xn, C, cell);
-        const float g0 = df[0][4 * a + 2 * b], g1 = df[0][4 * a + 2 * b + 1];
-        float v[16];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          v[2 * c] = C.w[c] * g0;
-          v[2 * c + 1] = C.w[c] * g1;
-        }
-        bool emit = ok;
-#if DEN_NGP_AGG_RES > 0
-        if (V.res <= (uint32_t)DEN_NGP_AGG_RES) emit = ngp_fold(cell, v, ok);
-#endif
-#if DEN_NGP_EXP_NO_ATOMIC  // experiment build only: the backward without its table scatter
-        (void)emit;
-#elif DEN_NGP_SCATTER_QUAD
-        ngp_scatter_quad(A.d_table, C.idx, v, emit);
-#else
-        if (emit) {
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            float* t = A.d_table + 2 * (int64_t)C.idx[c];
-            unsafeAtomicAdd(t, v[2 * c]);
-            unsafeAtomicAdd(t + 1, v[2 * c + 1]);
-          }
-        }
-#endif
-      }
   }
 }
 
@@ -672,10 +539,8 @@ __global__ __launch_bounds__(NSC_THREADS) void ngp_scatter_kernel(NgpArgs A) {
 // without LDS.  The bias is the row sum of the A operand, accumulated (in f64) from the same registers.
 // Workgroup = (split, task), 4 waves over interleaved 32-sample chunks, reduced through LDS into
 // partials [task][split][2][32][32] + [64]; a second kernel sums the splits in a fixed order.
-#ifndef DEN_NGP_DW_MFMA
-#define DEN_NGP_DW_MFMA 1
-#endif
 constexpr int NDW_TASKS = 6, NDW_PART = 2 * 32 * 32 + 64;
+constexpr int NDW_CHUNK = 64;  // the samples of a split: a multiple of this (the padded save stride)
 
 struct NgpDwTask {
   int a_row, a_rows, mt;  // dZ rows (first, valid count), row tiles (1 or 2; column tiles = 3 - mt)

@@ -54,14 +54,15 @@ struct RenderArgs {
   const float* d_depth;
   float* bkgd_partial;    // [4][n_rays]
   float* lr_partial;      // [workgroup][LR_PART]: the fused Lr weight gradient (render_bwd_kernel, LAST_J = 1)
+  int64_t n_items;        // forward: 256-sample (BF16) / 128-sample (F32) blocks, walked by a persistent grid
 };
 
 // ------------------------------------------------------------------ helpers
 
 // Base of tile `tile` of activation tensor `a` for the wave that owns `sample` (wave-block major
 // layout, den_geom.h); the per-lane offset is added by store_tile_* / load_tile_vals.
-template <int MODE>
-__device__ __forceinline__ char* act_ptr(const RenderArgs<MODE>& A, int a, int64_t sample, int tile) {
+template <int MODE, typename AT>
+__device__ __forceinline__ char* act_ptr(const AT& A, int a, int64_t sample, int tile) {
   constexpr int TM = Tr<MODE>::TM, ES = es_of(MODE);
   const int64_t wb = __builtin_amdgcn_readfirstlane((int)(sample / TM));  // uniform across the wave
   return A.act[a] + (wb * (act_width(MODE, a) / TM) + tile) * (int64_t)(TM * TM * ES);
@@ -77,29 +78,26 @@ __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, 
   __syncthreads();
 }
 
-// ---- forward weight ring: FWD_RING slots, chunks t+1 .. t+FWD_RING-1 in flight while chunk t is
-// computed.  The LDS-DMA is issued through inline asm, so the compiler does not track it (tracked,
-// it makes the first LDS read of every chunk wait vmcnt(0) -- i.e. for the deeper prefetch and for
-// the activation stores too).  Each step instead waits for chunk t+1 only, by count: vmcnt is
-// in-order, so "chunk t+1 landed" = at most <vector-memory ops issued after its DMA> outstanding
-// (FwdVm keeps that count).  The activation stores of a step then have FWD_RING - 2 further chunk
-// intervals to drain before a wait covers them: with the whole chip writing 5 KB per sample, an HBM
-// store outlives one interval, and a 3-slot ring made every barrier wait for the previous step's
-// stores.
-#ifndef DEN_FWD_G
-#define DEN_FWD_G 2  // r02 A/B/A/B: 25.05 / 25.08 ms vs 25.28 / 25.46 ms for one tile per chunk
-#endif
-#ifndef DEN_FWD_RING
-#define DEN_FWD_RING (DEN_FWD_G == 3 ? 2 : DEN_FWD_G == 2 ? 3 : 4)
-#endif
-#ifndef DEN_FWD_SETPRIO
-#define DEN_FWD_SETPRIO 0
-#endif
-constexpr int FWD_RING = DEN_FWD_RING;
-static_assert(FWD_RING >= 2 && FWD_RING <= 4, "forward weight ring: 2 to 4 slots");
-// row tiles per forward chunk (one barrier per chunk): G = 2 halves the barriers and DMA batches
-constexpr int FWD_G = DEN_FWD_G;
-static_assert(FWD_G >= 1 && FWD_G <= 3, "forward chunk: 1 to 3 row tiles");
+// ---- forward weight ring: FWD_RING slots of FWD_G row tiles each; chunks t+1 .. t+FWD_RING-1 are in
+// flight while chunk t is computed.  The LDS-DMA is issued through inline asm, so the compiler does
+// not track it (tracked, it makes the first LDS read of every chunk wait vmcnt(0) -- i.e. for the
+// deeper prefetch and for the activation stores too).  Each step instead waits for chunk t+1 only,
+// by count: vmcnt is in-order, so "chunk t+1 landed" = at most <vector-memory ops issued after its
+// DMA> outstanding (FwdVm keeps that count).  The activation stores of a step then have FWD_RING - 2
+// further chunk intervals to drain before a wait covers them.
+//
+// The kernel is persistent: one workgroup per CU walks 256-sample blocks ("items", whole rays),
+// and the weight stream runs on across items -- the weights are the same for every item, so the
+// chunks of the next item's first layer are loaded during the current item's last layers and the
+// next item starts on a full ring, with no launch or refill bubble.  The ring slot of a chunk is
+// therefore a run-time value (the item's chunk count is not a multiple of FWD_RING).
+// Measured (r02/r03 A/B): two row tiles per chunk on a 3-slot ring (one barrier per
+// 32 MFMAs), 8 waves of 32 samples (two 32-sample blocks per wave with 4 waves was slower), the
+// compiler's instruction order (pinned interleaves were slower), weight fragments read 4 k-steps
+// ahead.
+constexpr int FWD_G = 2;     // row tiles per forward chunk (one barrier per chunk)
+constexpr int FWD_RING = 3;  // ring slots
+constexpr int FWD_PF = 4;    // weight fragments read ahead (BF16)
 constexpr int FWD_SLOT = FWD_G * CHUNK_MAX;  // bytes per forward ring slot
 static_assert(FWD_RING * FWD_SLOT <= 128 * 1024, "forward ring exceeds the LDS budget");
 DEN_HD constexpr int fwd_nchunks_l(int mode, int l) { return (fwd_tiles(mode, l) + FWD_G - 1) / FWD_G; }
@@ -108,38 +106,16 @@ DEN_HD constexpr int fwd_gchunk_index(int mode, int l) {
   for (int i = 0; i < l; ++i) c += fwd_nchunks_l(mode, i);
   return c;
 }
+DEN_HD constexpr int fwd_item_chunks(int mode) { return fwd_gchunk_index(mode, NL); }
 
-// Forward workgroup: 8 column blocks of TM samples (BF16: 256 samples) share one weight stream --
-// every workgroup streams the whole packed MLP (1.2 MB) through LDS, so samples per workgroup set
-// the L2 -> LDS weight traffic (78 GB per 2^24-sample step at 256 per workgroup).  NB column
-// blocks per wave, 8 / NB waves: NB = 2 (BF16 only; 4 waves, one per SIMD with 512 registers) feeds
-// each LDS weight fragment to two MFMAs, but measured slower than 8 waves x 1 block (the compiler
-// then serialises LDS reads and MFMAs within the single wave and moves accumulators through AGPRs;
-// profiles/fwd_prof.py cycle split).
-#ifndef DEN_FWD_NB
-#define DEN_FWD_NB 1  // r02 A/B: NB = 2 (4 waves x 64 samples) 27.7 ms vs 24.9 ms for NB = 1
-#endif
-static_assert(DEN_FWD_NB == 1 || DEN_FWD_NB == 2, "BF16 forward: 1 or 2 column blocks per wave");
-#ifndef DEN_FWD_WAVES_BF16
-#define DEN_FWD_WAVES_BF16 (8 / DEN_FWD_NB)
-#endif
-DEN_HD constexpr int fwd_nb(int mode) { return mode == 1 ? DEN_FWD_NB : 1; }
-DEN_HD constexpr int fwd_waves(int mode) { return mode == 1 ? DEN_FWD_WAVES_BF16 : 8; }
+// Forward workgroup: 8 waves x TM samples (BF16: 256 samples) share one weight stream -- every item
+// streams the whole packed MLP (1.2 MB) through LDS, so samples per item set the L2 -> LDS weight
+// traffic (78 GB per 2^24-sample step at 256 per item).
+DEN_HD constexpr int fwd_nb(int mode) { return 1; }
+DEN_HD constexpr int fwd_waves(int mode) { return 8; }
 DEN_HD constexpr int fwd_threads(int mode) { return 64 * fwd_waves(mode); }
 DEN_HD constexpr int fwd_wg_samples(int mode) { return fwd_waves(mode) * fwd_nb(mode) * tm_of(mode); }
-// waves per SIMD the register budget is sized for: 1 with two blocks per wave (512 registers),
-// else 2 (256 registers; 4-wave workgroups then run two per CU)
-DEN_HD constexpr int fwd_min_waves(int mode) { return fwd_nb(mode) == 2 ? 1 : 2; }
-
-// per-wave count of DMA instructions dma_chunk_untracked<NTH> issues for `bytes` (wave-uniform)
-template <int NTH>
-__device__ __forceinline__ int dma_ops(int bytes) {
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int n = 0;
-#pragma unroll
-  for (int q = 0; q < (FWD_SLOT + NTH * 16 - 1) / (NTH * 16); ++q) n += (q * NTH * 16 + wave * 1024 < bytes) ? 1 : 0;
-  return n;
-}
+DEN_HD constexpr int fwd_min_waves(int mode) { return 2; }  // 256 registers per wave
 
 template <int NTH>
 __device__ __forceinline__ void dma_chunk_untracked(const char* g, char* lds_slot, int bytes) {
@@ -185,47 +161,50 @@ __device__ __forceinline__ void wait_vm_lgkm0_rt(int n) {
   }
 }
 
-// Vector-memory ops this wave issued (DMA pieces + global stores), and the count right after the
-// DMA of each chunk in the ring.  A store must be counted here or not at all: an uncounted op only
-// makes a wait stricter, an over-count would let the barrier pass before a chunk landed.
+// Vector-memory ops this wave issued in the current item (DMA pieces + global stores), and the
+// count right after each of the last FWD_RING - 1 chunk DMAs (hist[0] oldest).  Every value is a
+// compile-time constant of the unrolled item body.  A store must be counted here or not at all: an
+// uncounted op only makes a wait stricter, an over-count would let the barrier pass before a chunk
+// landed.  At an item's start everything issued before it has landed (the item prologue waits),
+// so the counts restart at 0.
 struct FwdVm {
   int issued;
-  int mark[FWD_RING];
+  int hist[FWD_RING - 1];
 #ifdef DEN_FWD_PROF
-  // experiment builds only: cycles in body / vmcnt wait / barrier, kernel start, prologue end,
-  // layers end, kernel end, (unused)
+  // experiment builds only: cycles in body / vmcnt wait / barrier, kernel start, item prologues,
+  // item tails, kernel end, (unused)
   uint64_t prof[8];
 #endif
 };
 #ifdef DEN_FWD_PROF
-#ifndef DEN_FWD_PROF_BASE
-#define DEN_FWD_PROF_BASE 0  // first workgroup recorded (512 of them): past the cold start, e.g. 32768
-#endif
 __device__ uint64_t den_fwd_prof[512 * 8 * 8];
 #endif
 
-// One forward step: issue chunk t+FWD_RING-1 into the slot chunk t-1 used (free since the last
-// barrier), run `body` on chunk t (it issues n_st stores), wait for chunk t+1, barrier.
+// One forward step on chunk t (in ring slot `slot`, run-time 0..FWD_RING-1): issue chunk
+// t+FWD_RING-1 into the slot chunk t-1 used (free since the last barrier), run `body` on chunk t
+// (it issues n_st stores), wait for chunk t+1, barrier.
 template <int NTH, typename Body>
-__device__ __forceinline__ void fwd_step(char* lds, const char* wbase, int t, int64_t off_n, int bytes_n, int n_st,
-                                         FwdVm& vm, Body&& body) {
+__device__ __forceinline__ void fwd_step(char* lds, const char* wbase, int slot, int64_t off_n, int bytes_n,
+                                         int n_st, FwdVm& vm, Body&& body) {
   constexpr int R = FWD_RING;
 #ifdef DEN_FWD_PROF
   const uint64_t p0 = __builtin_amdgcn_s_memtime();
 #endif
-  if (bytes_n > 0) {
-    dma_chunk_untracked<NTH>(wbase + off_n, lds + ((t + R - 1) % R) * FWD_SLOT, bytes_n);
-    // the DMA ops EVERY wave issues (some issue one more): an under-count, so the count stays a
-    // compile-time constant and each wait an immediate
-    vm.issued += bytes_n / (NTH * 16);
-  }
-  vm.mark[(t + R - 1) % R] = vm.issued;
-  body(lds + (t % R) * FWD_SLOT);
+  const int dst = slot == 0 ? R - 1 : slot - 1;  // (slot + R - 1) % R
+  dma_chunk_untracked<NTH>(wbase + off_n, lds + dst * FWD_SLOT, bytes_n);
+  // the DMA ops EVERY wave issues (some issue one more): an under-count, so the count stays a
+  // compile-time constant and each wait an immediate
+  vm.issued += bytes_n / (NTH * 16);
+#pragma unroll
+  for (int k = 0; k + 1 < R - 1; ++k) vm.hist[k] = vm.hist[k + 1];
+  vm.hist[R - 2] = vm.issued;
+  body(lds + slot * FWD_SLOT);
 #ifdef DEN_FWD_PROF
   const uint64_t p1 = __builtin_amdgcn_s_memtime();
 #endif
   vm.issued += n_st;
-  wait_vm_lgkm0_rt(vm.issued - vm.mark[(t + 1) % R]);
+  // chunk t+1's DMA was issued R-2 steps ago: hist[0]
+  wait_vm_lgkm0_rt(vm.issued - vm.hist[0]);
 #ifdef DEN_FWD_PROF
   const uint64_t p2 = __builtin_amdgcn_s_memtime();
 #endif
@@ -240,19 +219,28 @@ __device__ __forceinline__ void fwd_step(char* lds, const char* wbase, int t, in
 #endif
 }
 
-// geometry of the forward chunk k after chunk c of layer l (bytes 0 past the last one): FWD_G
-// consecutive row tiles of one layer (fewer at a layer's end), contiguous in the packed layout
+// geometry of the forward chunk k after chunk c of layer l: FWD_G consecutive row tiles of one
+// layer (fewer at a layer's end), contiguous in the packed layout; past the last layer the stream
+// wraps to layer 0 (the next item's first chunks)
 template <int MODE>
 __device__ __forceinline__ void fwd_ahead(int l, int c, int k, int64_t* off, int* bytes) {
 #pragma unroll
   for (int s = 0; s < k; ++s) {
-    if (++c >= fwd_nchunks_l(MODE, l)) { ++l; c = 0; }
+    if (++c >= fwd_nchunks_l(MODE, l)) {
+      c = 0;
+      if (++l == NL) l = 0;
+    }
   }
-  if (l >= NL) { *off = 0; *bytes = 0; return; }
   const int tile = chunk_bytes_K(fwd_K(MODE, l));
   const int left = fwd_tiles(MODE, l) - c * FWD_G;
   *bytes = (left < FWD_G ? left : FWD_G) * tile;
   *off = fwd_layer_offset(MODE, l) + (int64_t)c * FWD_G * tile;
+}
+
+// ring slot of the item's chunk `gc` (compile-time) given the slot of its chunk 0 (run-time)
+__device__ __forceinline__ int fwd_slot(int slot0, int gc) {
+  const int s = slot0 + gc % FWD_RING;
+  return s >= FWD_RING ? s - FWD_RING : s;
 }
 
 template <int MODE, int LAST_J>
@@ -265,9 +253,6 @@ __device__ __forceinline__ void bwd_next(int j, int i, int64_t* off, int* bytes)
 }
 
 // ------------------------------------------------------------------ forward layer
-// A wave carries NB = fwd_nb(MODE) column blocks of TM samples: every weight fragment read from
-// LDS feeds NB independent MFMAs (BF16: two 32-sample blocks, so a workgroup of 4 waves -- one per
-// SIMD, up to 512 registers each -- shares one weight stream over 256 samples).
 // Fragment arrays are block-major: block b's k-th fragment of an input of stride S is x[b * S + k].
 // Runs all row tiles of forward layer L with input fragments x1[0..KS1) ++ x2[0..KS2).
 // EPI: 0 = hidden softplus(100) -> xo (+store act outA), 1 = bottleneck/sigma, 2 = rgb.
@@ -303,17 +288,16 @@ __device__ __forceinline__ void fwd_epilogue(Acc* acc, int i, Frag* xo, FwdOut* 
 
 // HBM store of forward tile i (train mode), issued in the chunk interval after the one that
 // computed it, so that the barrier closing an interval does not wait for it.
-template <int MODE, bool TRAIN, int EPI, int NB, typename Frag>
-__device__ __forceinline__ void fwd_store(const RenderArgs<MODE>& A, const int64_t* sample, int i, const Frag* xo,
-                                          int outA) {
+template <int MODE, bool TRAIN, int EPI, int NB, typename Frag, typename AT>
+__device__ __forceinline__ void fwd_store(const AT& A, const int64_t* sample, int i, const Frag* xo, int outA) {
   constexpr int TM = Tr<MODE>::TM, FPT = Tr<MODE>::FPT, KS = WIDTH / Tr<MODE>::KI;
   if constexpr (!TRAIN) return;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     if constexpr (EPI == 0) {
-      store_tile_frags<MODE>(act_ptr(A, outA, sample[b], i), xo + b * KS + i * FPT);
+      store_tile_frags<MODE>(act_ptr<MODE>(A, outA, sample[b], i), xo + b * KS + i * FPT);
     } else if constexpr (EPI == 1) {
-      if (i < WIDTH / TM) store_tile_frags<MODE>(act_ptr(A, A_BT, sample[b], i), xo + b * KS + i * FPT);
+      if (i < WIDTH / TM) store_tile_frags<MODE>(act_ptr<MODE>(A, A_BT, sample[b], i), xo + b * KS + i * FPT);
     }
   }
 }
@@ -329,9 +313,9 @@ __device__ __forceinline__ constexpr int fwd_store_ops(int i) {
 }
 
 // The last row tile's epilogue of layer L and the stores of its last two tiles.
-template <int MODE, bool TRAIN, int L, int EPI, int NB, typename Frag, typename Acc>
-__device__ __forceinline__ void fwd_layer_tail(const RenderArgs<MODE>& A, const int64_t* sample, Acc* last, Frag* xo,
-                                               int outA, FwdOut* out) {
+template <int MODE, bool TRAIN, int L, int EPI, int NB, typename Frag, typename Acc, typename AT>
+__device__ __forceinline__ void fwd_layer_tail(const AT& A, const int64_t* sample, Acc* last, Frag* xo, int outA,
+                                               FwdOut* out) {
   constexpr int NT = fwd_tiles(MODE, L);
   fwd_epilogue<MODE, L, EPI, NB>(last, NT - 1, xo, out);
   if constexpr (NT >= 2) fwd_store<MODE, TRAIN, EPI, NB>(A, sample, NT - 2, xo, outA);
@@ -346,15 +330,6 @@ __device__ __forceinline__ constexpr int fwd_tail_store_ops() {
 // acc[b] += W_chunk x[b * S + 0 .. KS), b < NB: one LDS read of each weight fragment per NB MFMAs.
 // BF16: the weight fragments are read FWD_PF k-steps ahead into a register ring (left alone, the
 // compiler issues each read right before its MFMAs and waits out the LDS latency every k-step).
-#ifndef DEN_FWD_PF
-#define DEN_FWD_PF 4
-#endif
-#ifndef DEN_FWD_LDS_OPAQUE
-#define DEN_FWD_LDS_OPAQUE 1  // r03 A/B: render_fwd 24.60 / 24.87 -> 24.38 / 24.39 ms per step
-#endif
-#ifndef DEN_FWD_SCHED
-#define DEN_FWD_SCHED 0  // r02 A/B: pinned schedule 25.8 ms vs 24.9 ms for the compiler's order (NB = 1)
-#endif
 template <int MODE, int K0, int K1, int NB, int S>
 __device__ __forceinline__ void mfma_chunk_nb(const char* lds_chunk, const typename Tr<MODE>::Frag* x,
                                               typename Tr<MODE>::Acc* acc) {
@@ -363,19 +338,14 @@ __device__ __forceinline__ void mfma_chunk_nb(const char* lds_chunk, const typen
   if constexpr (KS <= 0) {
     return;
   } else if constexpr (MODE == 1) {
-    constexpr int PF = DEN_FWD_PF < KS ? DEN_FWD_PF : KS;
-#if DEN_FWD_LDS_OPAQUE
-    // the chunk's LDS address as a run-time VGPR: unrolled, the slot is a compile-time constant and
-    // the compiler folds it into every read's address -- past 64 KiB that no longer fits the 16-bit
-    // offset field, and each read of the third ring slot then costs a v_or (and a temporary)
+    constexpr int PF = FWD_PF < KS ? FWD_PF : KS;
+    // the chunk's LDS address as a run-time VGPR: unrolled, a compile-time slot would be folded into
+    // every read's 16-bit offset field, which the third ring slot overflows (r03 A/B: -0.4 ms)
     typedef __attribute__((address_space(3))) const bf16x8 lds_frag_t;
     uint32_t lb = (uint32_t)(uintptr_t)(lds_ptr_t)lds_chunk + (uint32_t)lane * 16u;
     asm volatile("" : "+v"(lb));
     const lds_frag_t* lq = (const lds_frag_t*)(uintptr_t)lb;
     auto rd = [&](int k) -> bf16x8 { return lq[k * 64]; };
-#else
-    auto rd = [&](int k) -> bf16x8 { return *(const bf16x8*)(lds_chunk + k * 1024 + lane * 16); };
-#endif
     bf16x8 a[PF];
 #pragma unroll
     for (int p = 0; p < PF; ++p) a[p] = rd(K0 + p);
@@ -399,35 +369,6 @@ __device__ __forceinline__ void mfma_chunk_nb(const char* lds_chunk, const typen
   }
 }
 
-// BF16 chunk schedule pins (DEN_FWD_SCHED): the bias and the first FWD_PF weight fragments up
-// front, then per k-step its NB MFMAs, the LDS read of fragment k + FWD_PF and V VALU instructions
-// of the previous tile's epilogue (softplus + bf16 packing).
-template <int KS1, int KS2, int NB, bool EPI_VALU>
-__device__ __forceinline__ void fwd_interleave() {
-#if DEN_FWD_SCHED
-  // DEN_FWD_SCHED 2: LDS reads and MFMAs only (the VALU epilogue left to the scheduler)
-  constexpr int V = DEN_FWD_SCHED == 2 ? 0 : EPI_VALU ? (NB * 90 + KS1 + KS2 - 1) / (KS1 + KS2) : 1;
-  constexpr int PF1 = DEN_FWD_PF < KS1 ? DEN_FWD_PF : KS1;
-  constexpr int PF2 = DEN_FWD_PF < KS2 ? DEN_FWD_PF : KS2;
-  __builtin_amdgcn_sched_group_barrier(0x100, 4 + PF1, 0);  // DS read: bias (4) + first fragments
-#pragma unroll
-  for (int k = 0; k < KS1; ++k) {
-    __builtin_amdgcn_sched_group_barrier(0x008, NB, 0);     // MFMA
-    if (k + PF1 < KS1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    if (V > 0) __builtin_amdgcn_sched_group_barrier(0x002, V, 0);  // VALU
-  }
-  if constexpr (KS2 > 0) {
-    __builtin_amdgcn_sched_group_barrier(0x100, PF2, 0);
-#pragma unroll
-    for (int k = 0; k < KS2; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x008, NB, 0);
-      if (k + PF2 < KS2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      if (V > 0) __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
-    }
-  }
-#endif
-}
-
 // Layer transitions: the epilogue of a layer's last row tile (and its last two tile stores) does not
 // run on its own between two layers -- every wave would then be in VALU at once, the MFMAs idle.
 // With DEFER the layer leaves its last accumulators in `tail`; the next layer runs them (`pend`,
@@ -438,15 +379,14 @@ struct NoPend {
 };
 
 template <int MODE, bool TRAIN, int L, int KS1, int S1, int KS2, int S2, int EPI, int NB, bool DEFER, int PEND_ST,
-          typename Frag, typename Acc, typename Pend>
-__device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, const int64_t* sample,
+          typename Frag, typename Acc, typename Pend, typename AT>
+__device__ __forceinline__ void fwd_layer(const AT& A, char* lds, int slot0, int grp, const int64_t* sample,
                                           const Frag* x1, const Frag* x2, Frag* xo, int outA, FwdOut* out,
                                           FwdVm& vm, Pend&& pend, Acc* tail) {
   using T = Tr<MODE>;
   constexpr int TM = T::TM, FPT = T::FPT;
   constexpr int NT = fwd_tiles(MODE, L);
   constexpr int CB = fwd_chunk_index(MODE, L);
-  const int lane = threadIdx.x & 63, grp = lane / TM;
   constexpr int NC = fwd_nchunks_l(MODE, L);
   constexpr int GB = fwd_gchunk_index(MODE, L);
   constexpr int TILE_BYTES = chunk_bytes_K(fwd_K(MODE, L));
@@ -480,10 +420,6 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
           if (i >= 2) fwd_store<MODE, TRAIN, EPI, NB>(A, sample, i - 2, xo, outA);
 #pragma unroll
           for (int b = 0; b < NB; ++b) prev[b] = acc[b];
-          if constexpr (MODE == 1) {
-            if (i > 0) fwd_interleave<KS1, KS2, NB, EPI == 0>();  // i is unrolled: one branch survives
-            else fwd_interleave<KS1, KS2, NB, false>();
-          }
         }
       }
     };
@@ -496,7 +432,7 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
       const int i = c * FWD_G + j;
       if (i < NT && i >= 2) n_st += fwd_store_ops<MODE, TRAIN, EPI, NB>(i - 2);
     }
-    fwd_step<fwd_threads(MODE)>(lds, A.w, GB + c, noff, nbytes, n_st, vm, body);
+    fwd_step<fwd_threads(MODE)>(lds, A.w, fwd_slot(slot0, GB + c), noff, nbytes, n_st, vm, body);
   }
   if constexpr (DEFER) {
 #pragma unroll
@@ -509,7 +445,7 @@ __device__ __forceinline__ void fwd_layer(const RenderArgs<MODE>& A, char* lds, 
 
 // ------------------------------------------------------------------ forward kernel
 template <int MODE, bool TRAIN>
-__global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render_fwd_kernel(RenderArgs<MODE> A) {
+__global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render_fwd_kernel(RenderArgs<MODE> A0) {
   using T = Tr<MODE>;
   using Frag = typename T::Frag;
   using Acc = typename T::Acc;
@@ -519,258 +455,281 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
   constexpr int WGS = fwd_wg_samples(MODE);
   constexpr int NTH = fwd_threads(MODE);
   constexpr int NBIAS = (int)bias_floats(MODE);
+  constexpr int NCH = fwd_item_chunks(MODE);
   __shared__ __attribute__((aligned(16))) char lds[FWD_RING * FWD_SLOT + NBIAS * 4 + WGS * 16];
   float* bias_lds = (float*)(lds + FWD_RING * FWD_SLOT);
   float* rec_lds = bias_lds + NBIAS;
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane % TM, grp = lane / TM;
-  int64_t sample[NB];
-#pragma unroll
-  for (int b = 0; b < NB; ++b) sample[b] = (int64_t)blockIdx.x * WGS + (wave * NB + b) * TM + c;
-#if DEN_FWD_SETPRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half: static priority
+  const int wave = threadIdx.x >> 6;
+#ifdef DEN_FWD_PROF
+  uint64_t prof[8] = {0, 0, 0, __builtin_amdgcn_s_memtime(), 0, 0, 0, 0};
 #endif
 
-  // prologue: whole bias table -> LDS, chunks 0 .. FWD_RING-2 -> their ring slots
-  for (int q = threadIdx.x; q < NBIAS; q += NTH) bias_lds[q] = A.bias[q];
+  // once per workgroup: the bias table -> LDS, the first item's chunks 0 .. FWD_RING-2 -> slots
+  // 0 .. FWD_RING-2 (later items find theirs loaded by the previous item's last steps)
+  for (int q = threadIdx.x; q < NBIAS; q += NTH) bias_lds[q] = A0.bias[q];
 #pragma unroll
   for (int ch = 0; ch < FWD_RING - 1; ++ch) {
     int64_t off_c;
     int bytes_c;
     fwd_ahead<MODE>(0, 0, ch, &off_c, &bytes_c);
-    dma_chunk_untracked<NTH>(A.w + off_c, lds + ch * FWD_SLOT, bytes_c);
+    dma_chunk_untracked<NTH>(A0.w + off_c, lds + ch * FWD_SLOT, bytes_c);
   }
-  FwdVm vm;
-  vm.issued = 0;
+  int slot0 = 0;  // ring slot of the current item's chunk 0
+
+  for (int64_t item = blockIdx.x; item < A0.n_items; item += gridDim.x) {
+    // the arguments re-read from the kernarg segment in every item: through a pointer the compiler
+    // cannot prove loop-invariant, so it does not hoist ~30 argument words out of the loop and keep
+    // them live (in SGPRs, then spilled into VGPRs) across the whole item
+    typedef __attribute__((address_space(4))) const RenderArgs<MODE> KArgs;
+    KArgs* Ap = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // A0 is the kernel's only argument
+    asm volatile("" : "+s"(Ap));
+    KArgs& A = *Ap;
+    // lane-derived values recomputed per item from an opaque copy of the thread index: hoisted out
+    // of the loop, the per-lane LDS addresses of every bias read and encoding row stay live across
+    // the item and spill
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, c = lane % TM, grp = lane / TM;
+    float aabb[6];
 #pragma unroll
-  for (int ch = 0; ch < FWD_RING; ++ch) vm.mark[ch] = 0;
+    for (int q = 0; q < 6; ++q) aabb[q] = A.aabb[q];
+#ifdef DEN_FWD_PROF
+    const uint64_t q0 = __builtin_amdgcn_s_memtime();
+#endif
+    int64_t sample[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) sample[b] = item * WGS + (wave * NB + b) * TM + c;
+    FwdVm vm;
+    vm.issued = 0;
+#pragma unroll
+    for (int k = 0; k < FWD_RING - 1; ++k) vm.hist[k] = 0;
 #ifdef DEN_FWD_PROF
 #pragma unroll
-  for (int q = 0; q < 8; ++q) vm.prof[q] = 0;
-  vm.prof[3] = __builtin_amdgcn_s_memtime();
+    for (int q = 0; q < 8; ++q) vm.prof[q] = 0;
 #endif
 
-  // sample positions -> positional encoding as PE_PAD/TM fake accumulator tiles -> fragments
-  constexpr int PE_T = PE_PAD / TM, PE_S = PE_T * FPT;
-  float dir[NB][3], sel[NB];
-  Frag pe[NB * PE_S];
+    // sample positions -> positional encoding as PE_PAD/TM fake accumulator tiles -> fragments
+    constexpr int PE_T = PE_PAD / TM, PE_S = PE_T * FPT;
+    float dir[NB][3], sel[NB];
+    Frag pe[NB * PE_S];
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    float o[3], xc[3];
-    if (A.points == 1) {
+    for (int b = 0; b < NB; ++b) {
+      float o[3], xc[3];
+      if (A.points == 1) {
 #pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        o[a] = A.rays_o[sample[b] * 3 + a];
-        dir[b][a] = A.rays_d[sample[b] * 3 + a];
+        for (int a = 0; a < 3; ++a) {
+          o[a] = A.rays_o[sample[b] * 3 + a];
+          dir[b][a] = A.rays_d[sample[b] * 3 + a];
+        }
+        contract_point(o, aabb, xc, &sel[b], A.contraction);
+      } else if (A.points == 2) {
+        // packed ray-marching samples: position o + d (t0 + t1)/2 of the sample's ray (utils.py:83-87)
+        const int64_t r = A.ray_idx[sample[b]];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          o[a] = A.rays_o[r * 3 + a];
+          dir[b][a] = A.rays_d[r * 3 + a];
+        }
+        contract(o, dir[b], A.t_start[sample[b]], A.t_end[sample[b]], aabb, xc, &sel[b], A.contraction);
+      } else {
+        const int64_t ray = sample[b] / A.n_samples;
+        const int k = (int)(sample[b] - ray * A.n_samples);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          o[a] = A.rays_o[ray * 3 + a];
+          dir[b][a] = A.rays_d[ray * 3 + a];
+        }
+        const float u = A.jitter[ray];
+        RayGeom g = ray_geom(o, dir[b], aabb, A.near_p, A.far_p);
+        float t0, t1;
+        sample_interval(g, k, u, A.n_samples, &t0, &t1);
+        contract(o, dir[b], t0, t1, aabb, xc, &sel[b]);
       }
-      contract_point(o, A.aabb, xc, &sel[b], A.contraction);
-    } else if (A.points == 2) {
-      // packed ray-marching samples: position o + d (t0 + t1)/2 of the sample's ray (utils.py:83-87)
-      const int64_t r = A.ray_idx[sample[b]];
 #pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        o[a] = A.rays_o[r * 3 + a];
-        dir[b][a] = A.rays_d[r * 3 + a];
-      }
-      contract(o, dir[b], A.t_start[sample[b]], A.t_end[sample[b]], A.aabb, xc, &sel[b], A.contraction);
-    } else {
-      const int64_t ray = sample[b] / A.n_samples;
-      const int k = (int)(sample[b] - ray * A.n_samples);
+      for (int p = 0; p < PE_T; ++p) {
+        Acc a;
 #pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        o[a] = A.rays_o[ray * 3 + a];
-        dir[b][a] = A.rays_d[ray * 3 + a];
+        for (int r = 0; r < REGS; ++r) a[r] = enc_feature<EXACT>(xc, p * TM + acc_row(MODE, grp, r), 10);
+        if (TRAIN) store_tile_vals<MODE>(act_ptr<MODE>(A, A_PE, sample[b], p), a);
+        acc_to_frags<MODE>(a, pe + b * PE_S + p * FPT);
       }
-      const float u = A.jitter[ray];
-      RayGeom g = ray_geom(o, dir[b], A.aabb, A.near_p, A.far_p);
-      float t0, t1;
-      sample_interval(g, k, u, A.n_samples, &t0, &t1);
-      contract(o, dir[b], t0, t1, A.aabb, xc, &sel[b]);
     }
-#pragma unroll
-    for (int p = 0; p < PE_T; ++p) {
-      Acc a;
-#pragma unroll
-      for (int r = 0; r < REGS; ++r) a[r] = enc_feature<EXACT>(xc, p * TM + acc_row(MODE, grp, r), 10);
-      if (TRAIN) store_tile_vals<MODE>(act_ptr(A, A_PE, sample[b], p), a);
-      acc_to_frags<MODE>(a, pe + b * PE_S + p * FPT);
-    }
-  }
-#ifndef DEN_FWD_PE_INFLIGHT
-#define DEN_FWD_PE_INFLIGHT 1
-#endif
-  // the untracked prologue DMAs landed; the pe stores (the youngest vector-memory ops, issued after
-  // the DMAs and the ray loads) may stay in flight -- vmcnt is in-order, so waiting for all but them
-  // covers the DMAs (older ops left in flight only make the later counted waits stricter)
-  constexpr int PE_ST = (TRAIN && DEN_FWD_PE_INFLIGHT) ? NB * PE_T * (MODE == 1 ? 2 : 1) : 0;
-  static_assert(PE_ST < 64, "vmcnt is 6 bits");
-  wait_vm_lgkm0<PE_ST>();
-  __syncthreads();
+    // the item's first chunks landed (their DMAs: the prologue, or the previous item's last steps);
+    // the pe stores (the youngest vector-memory ops) may stay in flight -- vmcnt is in-order, so
+    // waiting for all but them covers the DMAs (older ops left in flight only make the later counted
+    // waits stricter)
+    constexpr int PE_ST = TRAIN ? NB * PE_T * (MODE == 1 ? 2 : 1) : 0;
+    static_assert(PE_ST < 64, "vmcnt is 6 bits");
+    wait_vm_lgkm0<PE_ST>();
+    __syncthreads();
 #ifdef DEN_FWD_PROF
-  vm.prof[4] = __builtin_amdgcn_s_memtime();
+    prof[4] += __builtin_amdgcn_s_memtime() - q0;
 #endif
 
-  constexpr int KS = WIDTH / T::KI;  // k-steps of a 256-wide input
-  Frag xa[NB * KS], xb[NB * KS];
-  FwdOut out[NB];
-  Acc tl[NB];  // last row tile of the previous layer, finished inside the next one (fwd_layer DEFER)
-  // the previous layer's tail, run by the next layer inside its first tile (xo: where it writes)
+    constexpr int KS = WIDTH / T::KI;  // k-steps of a 256-wide input
+    Frag xa[NB * KS], xb[NB * KS];
+    FwdOut out[NB];
+    Acc tl[NB];  // last row tile of the previous layer, finished inside the next one (fwd_layer DEFER)
+    // the previous layer's tail, run by the next layer inside its first tile (xo: where it writes)
 #define DEN_PEND(LP, EPIP, XO, OUTA) \
   [&]() { fwd_layer_tail<MODE, TRAIN, LP, EPIP, NB>(A, sample, tl, XO, OUTA, out); }
 #define DEN_PST(LP, EPIP) fwd_tail_store_ops<MODE, TRAIN, LP, EPIP, NB>()
-  fwd_layer<MODE, TRAIN, 0, PE_S, PE_S, 0, 0, 0, NB, true, -1>(A, lds, sample, pe, pe, xa, A_S0 + 0, out, vm, NoPend{}, tl);
-  fwd_layer<MODE, TRAIN, 1, KS, KS, 0, 0, 0, NB, true, DEN_PST(0, 0)>(A, lds, sample, xa, xa, xb, A_S0 + 1, out, vm,
-                                                                      DEN_PEND(0, 0, xa, A_S0 + 0), tl);
-  fwd_layer<MODE, TRAIN, 2, KS, KS, 0, 0, 0, NB, true, DEN_PST(1, 0)>(A, lds, sample, xb, xb, xa, A_S0 + 2, out, vm,
-                                                                      DEN_PEND(1, 0, xb, A_S0 + 1), tl);
-  fwd_layer<MODE, TRAIN, 3, KS, KS, 0, 0, 0, NB, true, DEN_PST(2, 0)>(A, lds, sample, xa, xa, xb, A_S0 + 3, out, vm,
-                                                                      DEN_PEND(2, 0, xa, A_S0 + 2), tl);
-  fwd_layer<MODE, TRAIN, 4, KS, KS, 0, 0, 0, NB, true, DEN_PST(3, 0)>(A, lds, sample, xb, xb, xa, A_S0 + 4, out, vm,
-                                                                      DEN_PEND(3, 0, xb, A_S0 + 3), tl);
-  fwd_layer<MODE, TRAIN, 5, KS, KS, PE_S, PE_S, 0, NB, true, DEN_PST(4, 0)>(A, lds, sample, xa, pe, xb, A_S0 + 5, out,
-                                                                            vm, DEN_PEND(4, 0, xa, A_S0 + 4), tl);
-  fwd_layer<MODE, TRAIN, 6, KS, KS, 0, 0, 0, NB, true, DEN_PST(5, 0)>(A, lds, sample, xb, xb, xa, A_S0 + 6, out, vm,
-                                                                      DEN_PEND(5, 0, xb, A_S0 + 5), tl);
-  fwd_layer<MODE, TRAIN, 7, KS, KS, 0, 0, 0, NB, true, DEN_PST(6, 0)>(A, lds, sample, xa, xa, xb, A_S0 + 7, out, vm,
-                                                                      DEN_PEND(6, 0, xa, A_S0 + 6), tl);
-  // xa <- bottleneck; its tail (the sigma row tile) runs inside L_G
-  fwd_layer<MODE, TRAIN, L_B, KS, KS, 0, 0, 1, NB, true, DEN_PST(7, 0)>(A, lds, sample, xb, xb, xa, 0, out, vm,
-                                                                        DEN_PEND(7, 0, xb, A_S0 + 7), tl);
+    fwd_layer<MODE, TRAIN, 0, PE_S, PE_S, 0, 0, 0, NB, true, -1>(A, lds, slot0, grp, sample, pe, pe, xa, A_S0 + 0, out,
+                                                                 vm, NoPend{}, tl);
+    fwd_layer<MODE, TRAIN, 1, KS, KS, 0, 0, 0, NB, true, DEN_PST(0, 0)>(A, lds, slot0, grp, sample, xa, xa, xb, A_S0 + 1,
+                                                                        out, vm, DEN_PEND(0, 0, xa, A_S0 + 0), tl);
+    fwd_layer<MODE, TRAIN, 2, KS, KS, 0, 0, 0, NB, true, DEN_PST(1, 0)>(A, lds, slot0, grp, sample, xb, xb, xa, A_S0 + 2,
+                                                                        out, vm, DEN_PEND(1, 0, xb, A_S0 + 1), tl);
+    fwd_layer<MODE, TRAIN, 3, KS, KS, 0, 0, 0, NB, true, DEN_PST(2, 0)>(A, lds, slot0, grp, sample, xa, xa, xb, A_S0 + 3,
+                                                                        out, vm, DEN_PEND(2, 0, xa, A_S0 + 2), tl);
+    fwd_layer<MODE, TRAIN, 4, KS, KS, 0, 0, 0, NB, true, DEN_PST(3, 0)>(A, lds, slot0, grp, sample, xb, xb, xa, A_S0 + 4,
+                                                                        out, vm, DEN_PEND(3, 0, xb, A_S0 + 3), tl);
+    fwd_layer<MODE, TRAIN, 5, KS, KS, PE_S, PE_S, 0, NB, true, DEN_PST(4, 0)>(
+        A, lds, slot0, grp, sample, xa, pe, xb, A_S0 + 5, out, vm, DEN_PEND(4, 0, xa, A_S0 + 4), tl);
+    fwd_layer<MODE, TRAIN, 6, KS, KS, 0, 0, 0, NB, true, DEN_PST(5, 0)>(A, lds, slot0, grp, sample, xb, xb, xa, A_S0 + 6,
+                                                                        out, vm, DEN_PEND(5, 0, xb, A_S0 + 5), tl);
+    fwd_layer<MODE, TRAIN, 7, KS, KS, 0, 0, 0, NB, true, DEN_PST(6, 0)>(A, lds, slot0, grp, sample, xa, xa, xb, A_S0 + 7,
+                                                                        out, vm, DEN_PEND(6, 0, xa, A_S0 + 6), tl);
+    // xa <- bottleneck; its tail (the sigma row tile) runs inside L_G
+    fwd_layer<MODE, TRAIN, L_B, KS, KS, 0, 0, 1, NB, true, DEN_PST(7, 0)>(A, lds, slot0, grp, sample, xb, xb, xa, 0, out,
+                                                                          vm, DEN_PEND(7, 0, xb, A_S0 + 7), tl);
 
-  // view-direction encoding (mlp.py:353-355): condition * pi, degree 4
-  constexpr int VE_T = VE_PAD / TM, VE_S = VE_T * FPT;
-  Frag ve[NB * VE_S];
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-#pragma clang fp contract(off)
-    float dv[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) dv[a] = dir[b][a] * 3.1415927f;
-#pragma unroll
-    for (int p = 0; p < VE_T; ++p) {
-      Acc a;
-#pragma unroll
-      for (int r = 0; r < REGS; ++r) a[r] = enc_feature<EXACT>(dv, p * TM + acc_row(MODE, grp, r), 4);
-      if (TRAIN) {
-        store_tile_vals<MODE>(act_ptr(A, A_VE, sample[b], p), a);
-        vm.issued += MODE == 1 ? 2 : 1;
-      }
-      acc_to_frags<MODE>(a, ve + b * VE_S + p * FPT);
-    }
-  }
-  fwd_layer<MODE, TRAIN, L_G, KS, KS, VE_S, VE_S, 0, NB, true, DEN_PST(L_B, 1)>(A, lds, sample, xa, ve, xb, A_G, out,
-                                                                                vm, DEN_PEND(L_B, 1, xa, 0), tl);
-  fwd_layer<MODE, TRAIN, L_R, WIDTH_COND / T::KI, KS, 0, 0, 2, NB, false, DEN_PST(L_G, 0)>(
-      A, lds, sample, xb, xb, xa, 0, out, vm, DEN_PEND(L_G, 0, xb, A_G), tl);
-#undef DEN_PEND
-#undef DEN_PST
-
-#ifdef DEN_FWD_PROF
-  vm.prof[5] = __builtin_amdgcn_s_memtime();
-  auto prof_store = [&]() {
-    const int pb = (int)blockIdx.x - DEN_FWD_PROF_BASE;
-    if (pb >= 0 && pb < 512 && lane == 0) {
-      vm.prof[6] = __builtin_amdgcn_s_memtime();
-#pragma unroll
-      for (int q = 0; q < 8; ++q) den_fwd_prof[(pb * 8 + wave) * 8 + q] = vm.prof[q];
-    }
-  };
-#endif
-  // per-sample sigma / rgb (lane group 0 holds rows 0..)
-  if (grp == 0) {
+    // view-direction encoding (mlp.py:353-355): condition * pi, degree 4
+    constexpr int VE_T = VE_PAD / TM, VE_S = VE_T * FPT;
+    Frag ve[NB * VE_S];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const int wl = (wave * NB + b) * TM + c;  // WG-local sample
-      // select, not multiply: a sample outside the box (only zero-length samples of missed rays;
-      // nerfacc never produces one) must get sigma = 0 even where exp overflows (inf * 0 = NaN)
-      float sigma = sel[b] != 0.0f ? expf(out[b].sigma_raw - 1.0f) : 0.0f;
-      float r0 = softplus_b1(out[b].rgb_raw[0]);
-      float r1 = A.rd > 1 ? softplus_b1(out[b].rgb_raw[1]) : 0.0f;
-      float r2 = A.rd > 2 ? softplus_b1(out[b].rgb_raw[2]) : 0.0f;
-      f32x4 v = {sigma, r0, r1, r2};
-      *(f32x4*)(rec_lds + wl * 4) = v;
-      if (TRAIN) *(f32x4*)(A.rec + sample[b] * 4) = v;
-      if (A.points) {
-        A.out_opacity[sample[b]] = sigma;
+#pragma clang fp contract(off)
+      float dv[3];
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch)
-          if (ch < A.rd) A.out_rgb[sample[b] * A.rd + ch] = v[1 + ch];
+      for (int a = 0; a < 3; ++a) dv[a] = dir[b][a] * 3.1415927f;
+#pragma unroll
+      for (int p = 0; p < VE_T; ++p) {
+        Acc a;
+#pragma unroll
+        for (int r = 0; r < REGS; ++r) a[r] = enc_feature<EXACT>(dv, p * TM + acc_row(MODE, grp, r), 4);
+        if (TRAIN) {
+          store_tile_vals<MODE>(act_ptr<MODE>(A, A_VE, sample[b], p), a);
+          vm.issued += MODE == 1 ? 2 : 1;
+        }
+        acc_to_frags<MODE>(a, ve + b * VE_S + p * FPT);
       }
     }
-  }
+    fwd_layer<MODE, TRAIN, L_G, KS, KS, VE_S, VE_S, 0, NB, true, DEN_PST(L_B, 1)>(
+        A, lds, slot0, grp, sample, xa, ve, xb, A_G, out, vm, DEN_PEND(L_B, 1, xa, 0), tl);
+    fwd_layer<MODE, TRAIN, L_R, WIDTH_COND / T::KI, KS, 0, 0, 2, NB, false, DEN_PST(L_G, 0)>(
+        A, lds, slot0, grp, sample, xb, xb, xa, 0, out, vm, DEN_PEND(L_G, 0, xb, A_G), tl);
+#undef DEN_PEND
+#undef DEN_PST
 #ifdef DEN_FWD_PROF
-  if (A.points) prof_store();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) prof[q] += vm.prof[q];
+    const uint64_t q1 = __builtin_amdgcn_s_memtime();
 #endif
-  if (A.points) return;
-  __syncthreads();
+    slot0 = fwd_slot(slot0, NCH);  // the next item's chunk 0 follows this item's last chunk
 
-  // compositing: one wave per ray (nerfacc render_weight_from_density +
-  // accumulate_along_rays, vol_rendering.py:89-126)
-  const int rays_per_wg = WGS / A.n_samples;
-  if (wave < rays_per_wg) {
-    const int64_t r = (int64_t)blockIdx.x * rays_per_wg + wave;
-    float ro[3], rdv[3];
+    // per-sample sigma / rgb (lane group 0 holds rows 0..)
+    if (grp == 0) {
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      ro[a] = A.rays_o[r * 3 + a];
-      rdv[a] = A.rays_d[r * 3 + a];
-    }
-    RayGeom rg = ray_geom(ro, rdv, A.aabb, A.near_p, A.far_p);
-    const float ru = A.jitter[r];
-    const int spl = A.n_samples / 64;  // samples per lane (1, 2 or 4)
-    float tau[4], tmid[4], locx[4];
-    float run = 0.0f;
-    
+      for (int b = 0; b < NB; ++b) {
+        const int wl = (wave * NB + b) * TM + c;  // WG-local sample
+        // select, not multiply: a sample outside the box (only zero-length samples of missed rays;
+        // nerfacc never produces one) must get sigma = 0 even where exp overflows (inf * 0 = NaN)
+        float sigma = sel[b] != 0.0f ? expf(out[b].sigma_raw - 1.0f) : 0.0f;
+        float r0 = softplus_b1(out[b].rgb_raw[0]);
+        float r1 = A.rd > 1 ? softplus_b1(out[b].rgb_raw[1]) : 0.0f;
+        float r2 = A.rd > 2 ? softplus_b1(out[b].rgb_raw[2]) : 0.0f;
+        f32x4 v = {sigma, r0, r1, r2};
+        *(f32x4*)(rec_lds + wl * 4) = v;
+        if (TRAIN) *(f32x4*)(A.rec + sample[b] * 4) = v;
+        if (A.points) {
+          A.out_opacity[sample[b]] = sigma;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (q >= spl) break;
-      int kk = lane * spl + q;
-      float a0, a1;
-      sample_interval(rg, kk, ru, A.n_samples, &a0, &a1);
-      float sg = rec_lds[(wave * A.n_samples + kk) * 4];
-      // zero-length samples (missed rays) contribute nothing, also where sigma overflowed
-      tau[q] = (a1 > a0) ? sg * (a1 - a0) : 0.0f;
-      tmid[q] = (a0 + a1) / 2.0f;
-      locx[q] = run;
-      run += tau[q];
-    }
-    // exclusive optical depth as a sum of the preceding terms only (nerfacc's sequential
-    // exclusive cumsum): never incl - tau, which is inf - inf once a sigma overflows
-    float base = wave_excl_scan(run);
-    float cs[3] = {0.f, 0.f, 0.f}, op = 0.f, dp = 0.f;
-    
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (q >= spl) break;
-      int kk = lane * spl + q;
-      float excl = base + locx[q];
-      float w = expf(-excl) * (1.0f - expf(-tau[q]));
-      const float* rc = rec_lds + (wave * A.n_samples + kk) * 4;
-      cs[0] += w * rc[1];
-      cs[1] += w * rc[2];
-      cs[2] += w * rc[3];
-      op += w;
-      dp += w * tmid[q];
-    }
-    op = wave_sum(op);
-    dp = wave_sum(dp);
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) cs[ch] = wave_sum(cs[ch]);
-    if (lane == 0) {
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch) {
-        if (ch >= A.rd) break;
-        float v = cs[ch];
-        if (A.has_bkgd) v = v + A.bkgd[ch] * (1.0f - op);
-        A.out_rgb[r * A.rd + ch] = v;
+          for (int ch = 0; ch < 3; ++ch)
+            if (ch < A.rd) A.out_rgb[sample[b] * A.rd + ch] = v[1 + ch];
+        }
       }
-      A.out_opacity[r] = op;
-      A.out_depth[r] = dp;
     }
-  }
+    if (!A.points) {
+      __syncthreads();
+      // compositing: one wave per ray (nerfacc render_weight_from_density +
+      // accumulate_along_rays, vol_rendering.py:89-126); the other waves go on to the next item,
+      // whose rec_lds writes come 40 barriers later
+      const int rays_per_wg = WGS / A.n_samples;
+      if (wave < rays_per_wg) {
+        const int64_t r = item * rays_per_wg + wave;
+        float ro[3], rdv[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          ro[a] = A.rays_o[r * 3 + a];
+          rdv[a] = A.rays_d[r * 3 + a];
+        }
+        RayGeom rg = ray_geom(ro, rdv, aabb, A.near_p, A.far_p);
+        const float ru = A.jitter[r];
+        const int spl = A.n_samples / 64;  // samples per lane (1, 2 or 4)
+        float tau[4], tmid[4], locx[4];
+        float run = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q >= spl) break;
+          int kk = lane * spl + q;
+          float a0, a1;
+          sample_interval(rg, kk, ru, A.n_samples, &a0, &a1);
+          float sg = rec_lds[(wave * A.n_samples + kk) * 4];
+          // zero-length samples (missed rays) contribute nothing, also where sigma overflowed
+          tau[q] = (a1 > a0) ? sg * (a1 - a0) : 0.0f;
+          tmid[q] = (a0 + a1) / 2.0f;
+          locx[q] = run;
+          run += tau[q];
+        }
+        // exclusive optical depth as a sum of the preceding terms only (nerfacc's sequential
+        // exclusive cumsum): never incl - tau, which is inf - inf once a sigma overflows
+        float base = wave_excl_scan(run);
+        float cs[3] = {0.f, 0.f, 0.f}, op = 0.f, dp = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q >= spl) break;
+          int kk = lane * spl + q;
+          float excl = base + locx[q];
+          float w = expf(-excl) * (1.0f - expf(-tau[q]));
+          const float* rc = rec_lds + (wave * A.n_samples + kk) * 4;
+          cs[0] += w * rc[1];
+          cs[1] += w * rc[2];
+          cs[2] += w * rc[3];
+          op += w;
+          dp += w * tmid[q];
+        }
+        op = wave_sum(op);
+        dp = wave_sum(dp);
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) cs[ch] = wave_sum(cs[ch]);
+        if (lane == 0) {
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) {
+            if (ch >= A.rd) break;
+            float v = cs[ch];
+            if (A.has_bkgd) v = v + A.bkgd[ch] * (1.0f - op);
+            A.out_rgb[r * A.rd + ch] = v;
+          }
+          A.out_opacity[r] = op;
+          A.out_depth[r] = dp;
+        }
+      }
+    }
 #ifdef DEN_FWD_PROF
-  prof_store();
+    prof[5] += __builtin_amdgcn_s_memtime() - q1;
+#endif
+  }
+  // the last item's steps prefetched chunks of an item that does not exist: let those DMAs land
+  // before the workgroup (and its LDS) goes away
+  wait_vm_lgkm0<0>();
+#ifdef DEN_FWD_PROF
+  prof[6] = __builtin_amdgcn_s_memtime();
+  if (blockIdx.x < 512 && lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) den_fwd_prof[(blockIdx.x * 8 + wave) * 8 + q] = prof[q];
+  }
 #endif
 }
 
@@ -805,13 +764,13 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
     acc_to_frags<MODE>(acc, xo + i * FPT);
   };
   // dz stores deferred to the start of the next chunk interval (see fwd_store)
-  auto store = [&](int i) { store_tile_frags<MODE>(act_ptr(A, DZ, sample, i), xo + i * FPT); };
+  auto store = [&](int i) { store_tile_frags<MODE>(act_ptr<MODE>(A, DZ, sample, i), xo + i * FPT); };
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     int64_t noff;
     int nbytes;
     bwd_next<MODE, LAST_J>(J, i, &noff, &nbytes);
-    if constexpr (DER == 0) s_cur = load_tile_vals<MODE>(act_ptr(A, SA, sample, i));
+    if constexpr (DER == 0) s_cur = load_tile_vals<MODE>(act_ptr<MODE>(A, SA, sample, i));
     chunk_step(lds, A.w, cb + i, noff, nbytes, [&](const char* chunk) {
       if (i >= 2) store(i - 2);
       Acc acc = acc_zero<MODE>();
@@ -984,8 +943,8 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
     dzs[0] = g4[0];
   }
   if constexpr (!FUSE_LR) {
-    store_tile_vals<MODE>(act_ptr(A, D_ZR, sample, 0), dzr);
-    if constexpr (DZR_W / TM > 1) store_tile_vals<MODE>(act_ptr(A, D_ZR, sample, 1), acc_zero<MODE>());
+    store_tile_vals<MODE>(act_ptr<MODE>(A, D_ZR, sample, 0), dzr);
+    if constexpr (DZR_W / TM > 1) store_tile_vals<MODE>(act_ptr<MODE>(A, D_ZR, sample, 1), acc_zero<MODE>());
   }
   f32x16 lacc;  // FUSE_LR: the shared dW_r accumulator
 #pragma unroll
@@ -1037,13 +996,13 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
   if constexpr (MODE == 1 && LAST_J == 1) {
     // Lb runs layer-major (hidden_bwd_kernel<true>): sigma's dz leaves as 32 bf16 per wave block
     // in the first 64 B of dz_b's ninth tile (the rest of that tile is not read on this path)
-    if (grp == 0) *(__bf16*)(act_ptr(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)dzs[0];
+    if (grp == 0) *(__bf16*)(act_ptr<MODE>(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)dzs[0];
   } else {
     constexpr int EXTRA_T = (DZB_W - WIDTH) / TM;  // sigma tile + zero padding
 #pragma unroll
     for (int e = 0; e < EXTRA_T; ++e) {
       Acc t = e == 0 ? dzs : acc_zero<MODE>();
-      store_tile_vals<MODE>(act_ptr(A, D_ZB, sample, WIDTH / TM + e), t);
+      store_tile_vals<MODE>(act_ptr<MODE>(A, D_ZB, sample, WIDTH / TM + e), t);
       if (WIDTH + e * TM < fwd_M(MODE, L_B)) acc_to_frags<MODE>(t, xb + KS + e * FPT);
     }
   }

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("DEN_LIB", os.path.join(os.path.dirname(_HERE), "libde
 MODE_F32 = 0
 MODE_BF16 = 1
 _MODES = {"f32": MODE_F32, "fp32": MODE_F32, "float32": MODE_F32, "bf16": MODE_BF16, "bfloat16": MODE_BF16}
-ERROR_FNS = {"l1": 0, "mse": 1, "huber": 2}
+ERROR_FNS = {"l1": 0, "mse": 1, "huber": 2, "mape": 3}
 
 
 class DenError(RuntimeError):

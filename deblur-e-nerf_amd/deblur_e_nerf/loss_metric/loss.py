@@ -21,7 +21,7 @@ from ..utils.easydict import EasyDict
 
 class Loss(torch.nn.Module):
     LOSS_NAMES = ["log_intensity_diff", "log_intensity_tv"]
-    ERROR_FNS = ("l1", "mse", "huber")
+    ERROR_FNS = ("l1", "mse", "huber", "mape")
 
     def __init__(self, loss_weight, loss_error_fn, loss_normalize):
         super().__init__()

@@ -268,7 +268,7 @@ int den_pixbw_decay_ts_bwd(int32_t N, const double* output_ts, const double* res
  *   err_i = f(x_i / c - t_i),  L = mean_{i valid} err_i
  * x = rendered log-intensity difference (f32), c = normalising constant (the
  * mean contrast threshold, or 1), t = normalised target (NULL => 0, the TV
- * term).  error_fn: 0 = l1, 1 = mse, 2 = huber(delta = 1).  valid: u8 mask or
+ * term).  error_fn: 0 = l1, 1 = mse, 2 = huber(delta = 1), 3 = mape.  valid: u8 mask or
  * NULL (all valid).  No valid event => L = NaN (torch's empty mean).
  * workspace: den_event_loss_workspace_bytes(N), shared by fwd and bwd (bwd
  * reads the valid count left by fwd). */

@@ -13,6 +13,8 @@ ERROR_FNS = {
     "l1": lambda a, b: torch.nn.functional.l1_loss(a, b, reduction="none"),
     "mse": lambda a, b: torch.nn.functional.mse_loss(a, b, reduction="none"),
     "huber": lambda a, b: torch.nn.functional.huber_loss(a, b, reduction="none", delta=1.0),
+    # utils/modules.py:97-122 MAPELoss: |a - b| / max(|b|, f64 eps)
+    "mape": lambda a, b: torch.nn.functional.l1_loss(a, b, reduction="none") / b.abs().clamp(min=2.220446049250313e-16),
 }
 
 

@@ -32,8 +32,12 @@ def test_loss_constructor_mirrors_reference():
     L = Loss(ED(log_intensity_diff=1.0, log_intensity_tv=1e-3), ED(log_intensity_diff="huber", log_intensity_tv="l1"),
              ED(log_intensity_diff=True, log_intensity_tv=True))
     assert L.error_fn.log_intensity_diff == "huber"
-    with pytest.raises(NotImplementedError):
-        Loss(ED(log_intensity_diff=1.0, log_intensity_tv=1e-3), ED(log_intensity_diff="mape", log_intensity_tv="l1"),
+    # every error function of the reference (loss.py:25-30), mape included
+    for fn in ("l1", "mse", "huber", "mape"):
+        assert Loss(ED(log_intensity_diff=1.0, log_intensity_tv=1e-3), ED(log_intensity_diff=fn, log_intensity_tv="l1"),
+                    ED(log_intensity_diff=True, log_intensity_tv=True)).error_fn.log_intensity_diff == fn
+    with pytest.raises((NotImplementedError, KeyError, ValueError)):
+        Loss(ED(log_intensity_diff=1.0, log_intensity_tv=1e-3), ED(log_intensity_diff="smape", log_intensity_tv="l1"),
              ED(log_intensity_diff=True, log_intensity_tv=True))
 
 

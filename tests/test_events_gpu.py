@@ -125,3 +125,38 @@ def test_event_prep_rejects_bad_input():
     with pytest.raises(nat.DenError):
         nat.pixel_rays(torch.eye(3, device=DEV), torch.zeros(5, 2, device=DEV), torch.zeros(4, 6, 3, device=DEV),
                        torch.zeros(4, 6, 3, 3, device=DEV))
+
+
+@pytest.mark.parametrize("t", ["huber_l1", "l1_huber", "mse_mse", "mape_l1"])
+def test_loss_kernels_match_reference(golden_dir, t):
+    """loss_metric.Loss.compute on the device (den_event_target + den_event_loss_fwd/bwd) against the
+    reference's Loss (loss.npz, make_golden.gen_loss: loss.py:34-96 with utils/modules.py's MAPELoss):
+    both loss terms and the gradients into the rendered differences and the mean contrast
+    threshold (the normaliser and the target's 1 / C)."""
+    from deblur_e_nerf.loss_metric.loss import Loss
+    from deblur_e_nerf.utils.easydict import EasyDict as ED
+    z = _golden(golden_dir, "loss.npz")
+    fd, ft = t.split("_")
+    L = Loss(ED(log_intensity_diff=1.0, log_intensity_tv=1e-3), ED(log_intensity_diff=fd, log_intensity_tv=ft),
+             ED(log_intensity_diff=True, log_intensity_tv=True))
+    d_lid = torch.from_numpy(z[f"{t}:d_lid"]).to(DEV).requires_grad_(True)
+    s_lid = torch.from_numpy(z[f"{t}:s_lid"]).to(DEV).requires_grad_(True)
+    mct = torch.tensor(0.225, device=DEV, requires_grad=True)
+    end_ts = torch.from_numpy(z[f"{t}:end_ts"]).to(DEV)
+    start_ts = torch.from_numpy(z[f"{t}:start_ts"]).to(DEV)
+    be = ED(log_intensity_diff=torch.from_numpy(z[f"{t}:lid"]).to(DEV), end_ts=end_ts, start_ts=start_ts)
+    bd = ED(log_intensity_diff=d_lid, ts_diff=(end_ts - start_ts) * 1.0,
+            is_valid=torch.from_numpy(z[f"{t}:d_valid"]).to(DEV))
+    bs = ED(log_intensity_diff=s_lid, is_valid=torch.from_numpy(z[f"{t}:s_valid"]).to(DEV))
+    res = L.compute(be, bd, bs, mct)
+    (res.log_intensity_diff * 1.0 + res.log_intensity_tv * 1e-3).backward()
+    torch.cuda.synchronize()
+    rel = lambda a, b: float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))  # noqa: E731
+    e = {"L_diff": rel(float(res.log_intensity_diff), z[f"{t}:L_diff"]),
+         "L_tv": rel(float(res.log_intensity_tv), z[f"{t}:L_tv"]),
+         "g_d_lid": rel(d_lid.grad.cpu().numpy(), z[f"{t}:g_d_lid"]),
+         "g_s_lid": rel(s_lid.grad.cpu().numpy(), z[f"{t}:g_s_lid"]),
+         "g_mct": rel(float(mct.grad), z[f"{t}:g_mct"])}
+    print(f"[{t}] {e}")
+    assert max(e["L_diff"], e["L_tv"], e["g_d_lid"], e["g_s_lid"]) <= 1e-5, e
+    assert e["g_mct"] <= 1e-4, e  # a sum of cancelling terms (the normaliser vs the target's 1 / C)

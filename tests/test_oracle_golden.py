@@ -159,7 +159,7 @@ def test_pixel_bandwidth_matches_reference(golden_dir, fname):
 
 
 # --------------------------------------------------------------------------- loss / event model
-@pytest.mark.parametrize("t", ["huber_l1", "l1_huber", "mse_mse"])
+@pytest.mark.parametrize("t", ["huber_l1", "l1_huber", "mse_mse", "mape_l1"])
 def test_loss_matches_reference(golden_dir, t):
     z = _load(golden_dir, "loss.npz")
     fd, ft = t.split("_")

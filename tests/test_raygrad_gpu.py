@@ -104,13 +104,16 @@ def test_fixed_sampler_ray_gradients(mode, tol):
     assert e_o <= tol and e_d <= tol
 
 
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
 @pytest.mark.parametrize("contraction", ["aabb", "sphere"])
-def test_packed_sample_ray_gradients(contraction):
+def test_packed_sample_ray_gradients(contraction, mode):
     """points = 2 (the packed ray-marching samples of NeRF.forward): per-ray sums over sorted,
-    ragged runs of samples (rays with none among them), padding past the real samples."""
+    ragged runs of samples (rays with none among them), padding past the real samples.  BF16 (the
+    path NeRF.forward takes when tau_r is learnable): the layer-major hidden backward's dz buffers
+    (aliased over S0 / S5) feed the per-ray reduce -- 2e-2 against the f64 autograd."""
     nat = _nat()
     rd, R, n = 1, 40, 1000
-    p, flat, packed = _field_setup("f32", rd, 8)
+    p, flat, packed = _field_setup(mode, rd, 8)
     g = torch.Generator().manual_seed(9)
     o = torch.randn(R, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, -3.0])
     d = torch.nn.functional.normalize(torch.randn(R, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, 1.0]), dim=-1)
@@ -120,7 +123,7 @@ def test_packed_sample_ray_gradients(contraction):
     t1 = t0 + 0.01
     g_rgb, g_sig = torch.randn(n, rd, generator=g), torch.randn(n, generator=g)
     od, dd = o.to(DEV).requires_grad_(True), d.to(DEV).requires_grad_(True)
-    rgb, sig = nat.field_packed(od, dd, ri.to(DEV), t0.to(DEV), t1.to(DEV), flat, _cfg("f32", rd, contraction),
+    rgb, sig = nat.field_packed(od, dd, ri.to(DEV), t0.to(DEV), t1.to(DEV), flat, _cfg(mode, rd, contraction),
                                 packed)
     ((rgb * g_rgb.to(DEV)).sum() + (sig * g_sig.to(DEV)).sum()).backward()
     ref = {}
@@ -132,9 +135,9 @@ def test_packed_sample_ray_gradients(contraction):
         ((rgb_r * g_rgb.to(dt)).sum() + (sig_r[:, 0] * g_sig.to(dt)).sum()).backward()
         ref[dt] = (orr.grad, drr.grad)
     (o32, d32), (o64, d64) = ref[torch.float32], ref[torch.float64]
-    to_, td = _floor(o32, o64), _floor(d32, d64)
+    to_, td = (_floor(o32, o64), _floor(d32, d64)) if mode == "f32" else (2e-2, 2e-2)
     e_o, e_d = norm_rel(od.grad, o64), norm_rel(dd.grad, d64)
-    print(f"[packed {contraction}] d rays_o {e_o:.2e} (bound {to_:.2e}), d rays_d {e_d:.2e} (bound {td:.2e})")
+    print(f"[packed {contraction} {mode}] d rays_o {e_o:.2e} (bound {to_:.2e}), d rays_d {e_d:.2e} (bound {td:.2e})")
     assert e_o <= to_ and e_d <= td
     assert float(od.grad[7].abs().max()) == 0.0
 
