@@ -163,6 +163,8 @@ int check_desc(const den_render_desc* d) {
   if (d->contraction < 0 || d->contraction > 2) return fail(DEN_EINVAL, "contraction must be 0 (AABB), 1 (tanh) or 2 (sphere)");
   if (d->points == 0 && d->contraction != 0)
     return fail(DEN_EUNSUPPORTED, "the fixed-count sampler (points = 0) marches the AABB: contraction must be 0");
+  if (d->density_activation < 0 || d->density_activation > 2)
+    return fail(DEN_EINVAL, "density_activation must be 0 (shifted_trunc_exp), 1 (softplus) or 2 (shifted_softplus)");
   return DEN_OK;
 }
 
@@ -195,6 +197,7 @@ RenderArgs<MODE> make_args(const den_render_desc* d, const den_render_io* io, co
   A.out_rgb = io->out_rgb;
   A.out_opacity = io->out_opacity;
   A.out_depth = io->out_depth;
+  A.density_act = d->density_activation;
   return A;
 }
 
@@ -1325,7 +1328,8 @@ bool ngp_grid(const den_ngp_desc* d, NgpGrid* G, int64_t* table_floats) {
       d->log2_hashmap_size < 1 || d->log2_hashmap_size > 30 || d->base_resolution < 1 || !(d->per_level_scale >= 1.0f) ||
       (d->grid_type != 0 && d->grid_type != 1) || (d->radiance_dim != 1 && d->radiance_dim != 3) ||
       d->hidden_activation < 0 || d->hidden_activation > 1 || d->radiance_activation < 0 ||
-      d->radiance_activation > 1 || d->contraction < 0 || d->contraction > 2)
+      d->radiance_activation > 1 || d->contraction < 0 || d->contraction > 2 || d->density_activation < 0 ||
+      d->density_activation > 2)
     return false;
   NgpGrid g{};
   g.n_levels = d->n_levels;
@@ -1420,6 +1424,7 @@ int den_ngp_fwd(const den_ngp_desc* desc, int64_t n, int32_t points, const float
   A.points = points;
   A.contraction = desc->contraction;
   A.hidden_relu = desc->hidden_activation;
+  A.density_act = desc->density_activation;
   A.rad_sigmoid = desc->radiance_activation;
   A.density_only = density_only ? 1 : 0;
   for (int i = 0; i < 6; ++i) A.aabb[i] = desc->aabb[i];
@@ -1463,6 +1468,7 @@ int den_ngp_bwd(const den_ngp_desc* desc, int64_t n, const float* params, void* 
   A.n = n;
   A.rd = desc->radiance_dim;
   A.hidden_relu = desc->hidden_activation;
+  A.density_act = desc->density_activation;
   A.rad_sigmoid = desc->radiance_activation;
   A.mlp = params + tfl;
   A.off = ngp_offsets(2 * g.n_levels, desc->radiance_dim);

@@ -180,6 +180,27 @@ __device__ __forceinline__ float hidden_dact(float s) {
 
 __device__ __forceinline__ float softplus_b1(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
 
+// density activations (models/nerf.py:20-29): 0 shifted_trunc_exp exp(x - 1) whose backward clamps
+// the exponent at 15 (external/ngp.py:45-61), 1 softplus(beta 1, threshold 20), 2 shifted_softplus
+// softplus(x - 1)
+__device__ __forceinline__ float density_act(float raw, int act) {
+  if (act == 0) return expf(raw - 1.0f);
+  return softplus_b1(act == 2 ? raw - 1.0f : raw);
+}
+// d sigma / d raw from the output sigma: the clamped exponential, or sigmoid(u) = 1 - exp(-softplus(u))
+// (1 past the threshold, where softplus(u) = u > 20)
+__device__ __forceinline__ float density_dact_from_out(float sigma, int act) {
+  return act == 0 ? fminf(sigma, 3269017.5f /* expf(15) */) : -expm1f(-sigma);
+}
+// the same from the raw value
+__device__ __forceinline__ float density_dact_from_raw(float raw, int act) {
+  if (act == 0) return expf(fminf(raw - 1.0f, 15.0f));
+  const float u = act == 2 ? raw - 1.0f : raw;
+  if (u > 20.0f) return 1.0f;
+  const float z = expf(u);
+  return __fdiv_rn(z, z + 1.0f);
+}
+
 // ------------------------------------------------------------------ exact f32 sampler math
 // Mirrors oracle/nerf.py op-for-op (no FMA contraction), so that positions and
 // hence encodings are bit-identical to the PyTorch CPU restatement.

@@ -90,6 +90,7 @@ struct NgpArgs {
   int contraction;   // CONTRACT_*
   int hidden_relu;   // hidden activation: 0 softplus(beta = 100), 1 relu
   int rad_sigmoid;   // radiance activation: 0 softplus(beta = 1), 1 sigmoid
+  int density_act;   // density activation (den_device.h density_act)
   int density_only;  // sigma_fn of the marching pre-pass: skip the head
   float aabb[6];
   const float* x;    // points 1: positions; points 2: ray origins (R,3)

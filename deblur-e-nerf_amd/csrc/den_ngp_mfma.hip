@@ -260,7 +260,7 @@ __global__ __launch_bounds__(NM_THREADS, NM_OCC) void ngp_fwd_mfma_kernel(NgpArg
     ngp_mm<1, 32>(img + FI_A1, hb, ob, lane);
     if (h == 0 && ok) {
       const float o0 = ob[0][0];
-      A.out_sigma[i] = sel != 0.0f ? expf(o0 - 1.0f) : 0.0f;
+      A.out_sigma[i] = sel != 0.0f ? density_act(o0, A.density_act) : 0.0f;
       if (S) {
         S0[NS_O0 * nn] = o0;
         S0[NS_SEL * nn] = sel;
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(NM_THREADS, NM_OCC) void ngp_bwd_mfma_kernel(NgpArg
       const float gs = A.d_sigma && ok ? A.d_sigma[ic] : 0.0f;
       const float sel = S0[NS_SEL * nn];
       const float o0 = S0[NS_O0 * nn];
-      const float d0 = sel != 0.0f ? gs * expf(fminf(o0 - 1.0f, 15.0f)) : 0.0f;
+      const float d0 = sel != 0.0f ? gs * density_dact_from_raw(o0, A.density_act) : 0.0f;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         dob[q] = q == 0 && h == 0 ? d0 : dg[0][q];

@@ -55,6 +55,7 @@ struct RenderArgs {
   float* bkgd_partial;    // [4][n_rays]
   float* lr_partial;      // [workgroup][LR_PART]: the fused Lr weight gradient (render_bwd_kernel, LAST_J = 1)
   int64_t n_items;        // forward: 256-sample (BF16) / 128-sample (F32) blocks, walked by a persistent grid
+  int density_act;        // den_render_desc.density_activation
 };
 
 // ------------------------------------------------------------------ helpers
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
         const int wl = (wave * NB + b) * TM + c;  // WG-local sample
         // select, not multiply: a sample outside the box (only zero-length samples of missed rays;
         // nerfacc never produces one) must get sigma = 0 even where exp overflows (inf * 0 = NaN)
-        float sigma = sel[b] != 0.0f ? expf(out[b].sigma_raw - 1.0f) : 0.0f;
+        float sigma = sel[b] != 0.0f ? density_act(out[b].sigma_raw, A.density_act) : 0.0f;
         float r0 = softplus_b1(out[b].rgb_raw[0]);
         float r1 = A.rd > 1 ? softplus_b1(out[b].rgb_raw[1]) : 0.0f;
         float r2 = A.rd > 2 ? softplus_b1(out[b].rgb_raw[2]) : 0.0f;
@@ -826,7 +827,7 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch)
         if (ch < A.rd) g3[ch] = A.d_rgb[sample * A.rd + ch];
-      f32x4 o4 = {dsig * fminf(rv[0], 3269017.5f), g3[0] * (-expm1f(-rv[1])), g3[1] * (-expm1f(-rv[2])),
+      f32x4 o4 = {dsig * density_dact_from_out(rv[0], A.density_act), g3[0] * (-expm1f(-rv[1])), g3[1] * (-expm1f(-rv[2])),
                   g3[2] * (-expm1f(-rv[3]))};
       *(f32x4*)(rec_lds + (wave * TM + c) * 4) = o4;
     }
@@ -916,9 +917,9 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
       float Tnext = expf(-incl);
       float dtau = Tnext * gv[q] - suffix;
       float dsig = dtau * dlt[q];
-      // raw-output gradients: trunc_exp backward clamps at 15 (ngp.py:57-61);
-      // softplus(beta=1) derivative sigmoid(x) = 1 - exp(-softplus(x))
-      float dsig_raw = dsig * fminf(sg4[q], 3269017.5f /* expf(15) */);
+      // raw-output gradients from the outputs: the density activation's (trunc_exp's backward clamps at
+      // 15, ngp.py:57-61); softplus(beta=1) derivative sigmoid(x) = 1 - exp(-softplus(x))
+      float dsig_raw = dsig * density_dact_from_out(sg4[q], A.density_act);
       float v0 = w[q] * dC[0] * (-expm1f(-rc4[q][0]));
       float v1 = w[q] * dC[1] * (-expm1f(-rc4[q][1]));
       float v2 = w[q] * dC[2] * (-expm1f(-rc4[q][2]));

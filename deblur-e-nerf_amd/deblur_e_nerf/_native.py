@@ -27,7 +27,8 @@ class RenderDesc(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("radiance_dim", ctypes.c_int32), ("n_rays", ctypes.c_int32),
                 ("n_samples", ctypes.c_int32), ("aabb", ctypes.c_float * 6), ("near_plane", ctypes.c_float),
                 ("far_plane", ctypes.c_float), ("train", ctypes.c_int32), ("has_bkgd", ctypes.c_int32),
-                ("points", ctypes.c_int32), ("contraction", ctypes.c_int32), ("bwd_path", ctypes.c_int32)]
+                ("points", ctypes.c_int32), ("contraction", ctypes.c_int32), ("bwd_path", ctypes.c_int32),
+                ("density_activation", ctypes.c_int32)]
 
 
 class RenderIO(ctypes.Structure):
@@ -42,7 +43,7 @@ class NgpDesc(ctypes.Structure):
                 ("base_resolution", ctypes.c_int32), ("per_level_scale", ctypes.c_float),
                 ("grid_type", ctypes.c_int32), ("hidden_activation", ctypes.c_int32),
                 ("radiance_activation", ctypes.c_int32), ("contraction", ctypes.c_int32),
-                ("aabb", ctypes.c_float * 6)]
+                ("aabb", ctypes.c_float * 6), ("density_activation", ctypes.c_int32)]
 
 
 class RenderGrad(ctypes.Structure):
@@ -247,6 +248,7 @@ def _desc(cfg, n_rays, n_samples, train, has_bkgd, points=0):
     d.points = int(points)
     d.contraction = int(cfg.get("contraction", 0))
     d.bwd_path = int(cfg.get("bwd_path", 0))
+    d.density_activation = int(cfg.get("density", 0))
     return d
 
 
@@ -373,7 +375,22 @@ def field_packed(rays_o, rays_d, ray_indices, t_starts, t_ends, flat, cfg, packe
 
 
 # ----------------------------------------------------------------------------- ngp radiance field
-def ngp_desc(rd, pos_encoding, hidden_activation, radiance_activation, contraction, aabb):
+# models/nerf.py:20-29 density activations -> den_render_desc / den_ngp_desc.density_activation
+DENSITY_ACTIVATIONS = {"shifted_trunc_exp": 0, "softplus": 1, "shifted_softplus": 2}
+
+
+def density_id(fn):
+    """den density_activation id of a density activation callable (models/nerf.py:20-29):
+    shifted_trunc_exp, torch.nn.Softplus(beta=1) with threshold 20, or shifted_softplus."""
+    name = getattr(fn, "__name__", "")
+    if name in ("shifted_trunc_exp", "shifted_softplus"):
+        return DENSITY_ACTIVATIONS[name]
+    if isinstance(fn, torch.nn.Softplus) and fn.beta == 1 and fn.threshold == 20:
+        return DENSITY_ACTIVATIONS["softplus"]
+    raise DenError(f"density activation {fn!r} unsupported (shifted_trunc_exp, Softplus(beta=1), shifted_softplus)")
+
+
+def ngp_desc(rd, pos_encoding, hidden_activation, radiance_activation, contraction, aabb, density=0):
     """den_ngp_desc of an NGPradianceField configuration (external/ngp.py:112-145 with the
     configs/train/*.yaml nerf.ngp entries); unsupported settings raise DenError."""
     pe = dict(pos_encoding)
@@ -392,6 +409,7 @@ def ngp_desc(rd, pos_encoding, hidden_activation, radiance_activation, contracti
     d.contraction = int(contraction)
     for i, v in enumerate(aabb):
         d.aabb[i] = float(v)
+    d.density_activation = int(density)
     if lib().den_ngp_table_params(ctypes.byref(d)) < 0:
         raise DenError(f"unsupported ngp descriptor: {pe}")
     return d

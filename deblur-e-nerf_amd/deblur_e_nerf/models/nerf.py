@@ -34,7 +34,10 @@ def _randint(high, size, device=None):
 
 
 def shifted_softplus(x, shift=1, beta=1, threshold=20):
-    raise NotImplementedError("only the shifted_trunc_exp density activation is fused (nerf.py:22)")
+    """nerf.py:20-24 (mip-NeRF's density activation): softplus(x - shift).  The fields recognise it by
+    name and evaluate it inside their kernels (den density_activation 2: shift 1, beta 1,
+    threshold 20); called directly it is the reference's torch expression."""
+    return torch.nn.functional.softplus(x - shift, beta, threshold)
 
 
 class NeRF(torch.nn.Module):

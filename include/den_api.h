@@ -115,6 +115,9 @@ typedef struct den_render_desc {
                               layers 0..6, so one train forward feeds ONE den_render_bwd);
                               1 the F32 mode's sample-major chain + split-K GEMMs on the same bf16
                               operands (an A/B reference path).  F32 mode ignores it. */
+  int32_t density_activation; /* models/nerf.py:20-29: 0 shifted_trunc_exp (exp(x - 1), gradient
+                              clamped at exp(15), external/ngp.py:45-61), 1 softplus(beta 1,
+                              threshold 20), 2 shifted_softplus (softplus(x - 1)) */
 } den_render_desc;
 
 /* Device buffers of one render call. */
@@ -461,6 +464,7 @@ typedef struct den_ngp_desc {
   int32_t radiance_activation;   /* 0 softplus(beta=1), 1 sigmoid (models/nerf.py:26-29) */
   int32_t contraction;           /* 0 AABB, 1 UN_BOUNDED_TANH, 2 UN_BOUNDED_SPHERE */
   float aabb[6];
+  int32_t density_activation;    /* as den_render_desc.density_activation */
 } den_ngp_desc;
 
 /* Grid-table floats (tcnn sizing: per level min(next_multiple(res^3, 8), 2^log2_hashmap_size)

@@ -117,7 +117,19 @@ def _lin(p, name, h):
     return torch.nn.functional.linear(h, p[name + ".weight"], p[name + ".bias"])
 
 
-def radiance_field(p, x, d, aabb=AABB_CHAIR, depth=8, skip=4, contraction="aabb"):
+def density_activation(raw, kind="shifted_trunc_exp"):
+    """models/nerf.py:20-29: shifted_trunc_exp (external/ngp.py:45-65), softplus(beta 1), or
+    shifted_softplus (softplus(x - 1))."""
+    if kind == "shifted_trunc_exp":
+        return _TruncExp.apply(raw - 1)
+    if kind == "softplus":
+        return torch.nn.functional.softplus(raw, beta=1, threshold=20)
+    if kind == "shifted_softplus":
+        return torch.nn.functional.softplus(raw - 1, beta=1, threshold=20)
+    raise ValueError(kind)
+
+
+def radiance_field(p, x, d, aabb=AABB_CHAIR, depth=8, skip=4, contraction="aabb", density="shifted_trunc_exp"):
     """VanillaNeRFRadianceField.forward(x, d) -> (rgb (n, rd), sigma (n, 1))."""
     xc, sel = contract_aabb(x, aabb) if contraction == "aabb" else contract_unbounded(x, aabb, contraction)
     pe = encode(xc, 10)
@@ -132,7 +144,7 @@ def radiance_field(p, x, d, aabb=AABB_CHAIR, depth=8, skip=4, contraction="aabb"
     g = softplus100(_lin(p, "mlp.rgb_layer.hidden_layers.0", torch.cat([bott, ve], dim=-1)))
     rgb_raw = _lin(p, "mlp.rgb_layer.output_layer", g)
     rgb = torch.nn.functional.softplus(rgb_raw, beta=1, threshold=20)
-    sigma = _TruncExp.apply(sigma_raw - 1) * sel[..., None]
+    sigma = density_activation(sigma_raw, density) * sel[..., None]
     return rgb, sigma
 
 

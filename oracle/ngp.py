@@ -98,7 +98,12 @@ def field(p, x, d, rd, aabb, ctype=0, pos=POS_ENCODING, base=MLP_BASE, head=MLP_
         h = act(torch.nn.functional.linear(h, p[f"mlp_base.1.hidden_layers.{i}.weight"],
                                            p[f"mlp_base.1.hidden_layers.{i}.bias"]))
     o = torch.nn.functional.linear(h, p["mlp_base.1.output_layer.weight"], p["mlp_base.1.output_layer.bias"])
-    density = _trunc_exp(o[:, :1] - 1) * sel[:, None]
+    kind = base.get("density_activation", "shifted_trunc_exp")
+    if kind == "shifted_trunc_exp":
+        density = _trunc_exp(o[:, :1] - 1) * sel[:, None]
+    else:  # models/nerf.py:20-29: softplus(beta 1), shifted_softplus = softplus(x - 1)
+        density = torch.nn.functional.softplus(o[:, :1] - (1 if kind == "shifted_softplus" else 0), beta=1,
+                                               threshold=20) * sel[:, None]
     hh = torch.cat([tcnn.sh_encode_deg4(d.reshape(-1, 3)), o[:, 1:]], dim=-1)
     act = _act(head["hidden_activation"])
     for i in range(head["n_hidden_layers"]):

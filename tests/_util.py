@@ -68,7 +68,8 @@ def ngp_fixture(z):
     for k in z.files:
         if k.startswith("param:"):
             p[k[len("param:"):]] = torch.from_numpy(z[k])
-    base = dict(ongp.MLP_BASE, hidden_activation=str(z["hidden"]))
+    base = dict(ongp.MLP_BASE, hidden_activation=str(z["hidden"]),
+                density_activation=str(z["density"]) if "density" in z.files else "shifted_trunc_exp")
     head = dict(ongp.MLP_HEAD, hidden_activation=str(z["hidden"]), radiance_activation=str(z["radiance"]))
     return p, pos, base, head, rd, NGP_CTYPE[str(z["contraction"])]
 

@@ -93,12 +93,13 @@ def save(name, **arrays):
 
 
 # ----------------------------------------------------------------------------
-def gen_mlp(rd, seed, contraction="aabb"):
+def gen_mlp(rd, seed, contraction="aabb", density="shifted_trunc_exp"):
     """VanillaNeRFRadianceField forward/backward; contraction "aabb" (mlp_rd{rd}.npz) or the
     unbounded "sphere" / "tanh" input-space contractions (mlp_rd{rd}_{contraction}.npz: mlp.py:321-335,
     ngp.py:68-106), whose positions reach 4x the box so the contracted shells are exercised."""
     mlp = _refload.load("external.mlp")
     ngp = _refload.load("external.ngp")
+    nerfm = _refload.load("models.nerf")
     ContractionType = sys.modules["nerfacc"].ContractionType
     ctype = {"aabb": ContractionType.AABB, "sphere": ContractionType.UN_BOUNDED_SPHERE,
              "tanh": ContractionType.UN_BOUNDED_TANH}[contraction]
@@ -108,7 +109,7 @@ def gen_mlp(rd, seed, contraction="aabb"):
         skip_layer=4, net_depth_condition=1, net_width_condition=128, num_dim=3,
         contraction_type=ctype, radiance_dim=rd,
         hidden_activation=torch.nn.Softplus(beta=100),
-        density_activation=ngp.shifted_trunc_exp,
+        density_activation=nerfm.NeRF.DENSITY_ACTIVATION_NAME_TO_FN[density],
         radiance_activation=torch.nn.Softplus(beta=1),
         pos_encoder_max_deg=10, view_encoder_max_deg=4, weight_norm=False)
     g = torch.Generator().manual_seed(1000 + seed)
@@ -139,8 +140,10 @@ def gen_mlp(rd, seed, contraction="aabb"):
     field.float()
     wsum = {f"wsum:{k}": np.array(p.detach().double().sum().item()) for k, p in field.named_parameters()}
     name = f"mlp_rd{rd}.npz" if contraction == "aabb" else f"mlp_rd{rd}_{contraction}.npz"
-    save(name, seed=seed, contraction=np.array(contraction), x=x.numpy(), d=d.numpy(), g_rgb=g_rgb.numpy(),
-         g_sigma=g_sig.numpy(), param_names=np.array(names), **out, **wsum)
+    if density != "shifted_trunc_exp":
+        name = name.replace(".npz", f"_{density}.npz")
+    save(name, seed=seed, contraction=np.array(contraction), density=np.array(density), x=x.numpy(), d=d.numpy(),
+         g_rgb=g_rgb.numpy(), g_sigma=g_sig.numpy(), param_names=np.array(names), **out, **wsum)
 
 
 # ----------------------------------------------------------------------------
@@ -961,6 +964,13 @@ def gen_step_nopixbw():
     gen_step(False, 1)
 
 
+def gen_mlp_density():
+    """The other density activations of models/nerf.py:20-29 (mip-NeRF's shifted_softplus,
+    softplus), through the reference's VanillaNeRFRadianceField."""
+    gen_mlp(1, seed=4, density="shifted_softplus")
+    gen_mlp(3, seed=5, density="softplus")
+
+
 def gen_mlp_unbounded():
     gen_mlp(3, seed=2, contraction="sphere")
     gen_mlp(1, seed=3, contraction="tanh")
@@ -976,7 +986,8 @@ NGP_ARCH = dict(pos_encoding=dict(NGP_SMALL), dir_encoding=dict(degree=4),
                               n_hidden_layers=2, weight_norm=False))
 
 
-def gen_ngp(rd=1, seed=21, cfg="small", contraction="aabb", hidden="softplus", radiance="softplus", n=512):
+def gen_ngp(rd=1, seed=21, cfg="small", contraction="aabb", hidden="softplus", radiance="softplus", n=512,
+            density="shifted_trunc_exp"):
     """ngp_*.npz -- the reference's NGPradianceField (external/ngp.py:109-280: contraction, the
     mlp_base / mlp_head MLPs of external/mlp.py, SHEncoder, shifted_trunc_exp, the configured
     activations of models/nerf.py:17-29) forward + backward, with oracle/tcnn.py standing in for
@@ -996,7 +1007,9 @@ def gen_ngp(rd=1, seed=21, cfg="small", contraction="aabb", hidden="softplus", r
     pos = dict(NGP_SMALL) if cfg == "small" else dict(ongp.POS_ENCODING)
     act = {"softplus": torch.nn.Softplus(beta=100), "relu": torch.nn.ReLU()}
     ract = {"softplus": torch.nn.Softplus(beta=1), "sigmoid": torch.nn.Sigmoid()}
-    base = dict(ongp.MLP_BASE, hidden_activation=act[hidden], density_activation=ngp.shifted_trunc_exp)
+    nerfm = _refload.load("models.nerf")
+    base = dict(ongp.MLP_BASE, hidden_activation=act[hidden],
+                density_activation=nerfm.NeRF.DENSITY_ACTIVATION_NAME_TO_FN[density])
     head = dict(ongp.MLP_HEAD, hidden_activation=act[hidden], radiance_activation=ract[radiance], output_dim=rd)
     aabb = [-1.5, -1.5, -1.5, 1.5, 1.5, 1.5]
     field = ngp.NGPradianceField(aabb=aabb, num_dim=3, use_viewdirs=True, contraction_type=ctype,
@@ -1031,8 +1044,9 @@ def gen_ngp(rd=1, seed=21, cfg="small", contraction="aabb", hidden="softplus", r
     extra = dict(table=p["mlp_base.0.params"].numpy()) if cfg == "small" else {}
     mlp_w = {f"param:{k}": v.numpy() for k, v in p.items() if k != "mlp_base.0.params"}
     tag = f"ngp_rd{rd}_{cfg}" + ("" if contraction == "aabb" else f"_{contraction}") + \
-        ("" if hidden == "softplus" and radiance == "softplus" else f"_{hidden}_{radiance}")
-    save(tag + ".npz", seed=seed, rd=rd, cfg=np.array(cfg), contraction=np.array(contraction),
+        ("" if hidden == "softplus" and radiance == "softplus" else f"_{hidden}_{radiance}") + \
+        ("" if density == "shifted_trunc_exp" else f"_{density}")
+    save(tag + ".npz", seed=seed, rd=rd, cfg=np.array(cfg), contraction=np.array(contraction), density=np.array(density),
          hidden=np.array(hidden), radiance=np.array(radiance), pos_encoding=np.array(json.dumps(pos)),
          table_sum=np.array(p["mlp_base.0.params"].double().sum().item()), aabb=np.array(aabb, np.float32),
          x=x.numpy(), d=d.numpy(), g_rgb=g_rgb.numpy(), g_sigma=g_sig.numpy(), param_names=np.array(names),
@@ -1174,6 +1188,11 @@ def gen_ngp_all():
     gen_render_ngp(1, 25)
     gen_render_ngp(3, 26)
     gen_step(False, 1, seed=7, tag="step_ngp_nopixbw_rd1.npz", arch="ngp")
+
+
+def gen_ngp_density():
+    gen_ngp(1, 28, "small", density="shifted_softplus")
+    gen_ngp(3, 29, "small", "sphere", density="softplus")
 
 
 def gen_step_ngp():

@@ -18,7 +18,8 @@ from oracle import tcnn as otcnn
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-FIXTURES = ["ngp_rd1_small", "ngp_rd3_small_sphere_relu_sigmoid", "ngp_rd3_small_tanh", "ngp_rd3_default"]
+FIXTURES = ["ngp_rd1_small", "ngp_rd3_small_sphere_relu_sigmoid", "ngp_rd3_small_tanh", "ngp_rd3_default",
+            "ngp_rd1_small_shifted_softplus", "ngp_rd3_small_sphere_softplus"]
 CT_NAMES = {0: "AABB", 1: "UN_BOUNDED_TANH", 2: "UN_BOUNDED_SPHERE"}
 
 
@@ -26,7 +27,11 @@ def _field(p, pos, base, head, rd, ctype, aabb):
     from deblur_e_nerf.external import marching, ngp
     act = {"softplus": torch.nn.Softplus(beta=100), "relu": torch.nn.ReLU()}
     ract = {"softplus": torch.nn.Softplus(beta=1), "sigmoid": torch.nn.Sigmoid()}
-    bcfg = dict(base, hidden_activation=act[base["hidden_activation"]], density_activation=ngp.shifted_trunc_exp)
+    from deblur_e_nerf.models import nerf
+    dens = {"shifted_trunc_exp": ngp.shifted_trunc_exp, "softplus": torch.nn.Softplus(beta=1),
+            "shifted_softplus": nerf.shifted_softplus}
+    bcfg = dict(base, hidden_activation=act[base["hidden_activation"]],
+                density_activation=dens[base.get("density_activation", "shifted_trunc_exp")])
     hcfg = dict(head, hidden_activation=act[head["hidden_activation"]],
                 radiance_activation=ract[head["radiance_activation"]], output_dim=rd)
     f = ngp.NGPradianceField(aabb=[float(v) for v in aabb], num_dim=3, use_viewdirs=True,

@@ -23,10 +23,12 @@ def rel_err(a, b):
 
 
 # --------------------------------------------------------------------------- radiance field
-@pytest.mark.parametrize("fixture,rd", [("mlp_rd1", 1), ("mlp_rd3", 3), ("mlp_rd3_sphere", 3), ("mlp_rd1_tanh", 1)])
+@pytest.mark.parametrize("fixture,rd", [("mlp_rd1", 1), ("mlp_rd3", 3), ("mlp_rd3_sphere", 3), ("mlp_rd1_tanh", 1),
+                                        ("mlp_rd1_shifted_softplus", 1), ("mlp_rd3_softplus", 3)])
 def test_radiance_field_matches_reference(golden_dir, fixture, rd):
     z = _load(golden_dir, fixture + ".npz")
     contraction = str(z["contraction"]) if "contraction" in z.files else "aabb"
+    density = str(z["density"]) if "density" in z.files else "shifted_trunc_exp"
     p = onerf.build_params(rd, int(z["seed"]))
     # same weights as the reference's construction under the same seed
     for name in z["param_names"]:
@@ -35,7 +37,7 @@ def test_radiance_field_matches_reference(golden_dir, fixture, rd):
         p[k].requires_grad_(True)
     x = torch.from_numpy(z["x"])
     d = torch.from_numpy(z["d"])
-    rgb, sig = onerf.radiance_field(p, x, d, contraction=contraction)
+    rgb, sig = onerf.radiance_field(p, x, d, contraction=contraction, density=density)
     # bitwise-level agreement with the reference's fp32 forward (same torch ops on CPU)
     assert rel_err(rgb.detach(), z["rgb_f32"]) < 1e-6
     assert rel_err(sig.detach(), z["sigma_f32"]) < 1e-6
@@ -220,7 +222,8 @@ def test_pixel_rays_match_reference(golden_dir):
 
 
 # --------------------------------------------------------------------------- ngp radiance field
-NGP_FIXTURES = ["ngp_rd1_small", "ngp_rd3_small_sphere_relu_sigmoid", "ngp_rd3_small_tanh", "ngp_rd3_default"]
+NGP_FIXTURES = ["ngp_rd1_small", "ngp_rd3_small_sphere_relu_sigmoid", "ngp_rd3_small_tanh", "ngp_rd3_default",
+                "ngp_rd1_small_shifted_softplus", "ngp_rd3_small_sphere_softplus"]
 
 
 @pytest.mark.parametrize("fixture", NGP_FIXTURES)

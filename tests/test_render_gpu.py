@@ -33,21 +33,25 @@ def _cfg(mode, rd, near=1.43, far=6.63):
 CONTRACTION_ID = {"aabb": 0, "tanh": 1, "sphere": 2}  # den_render_desc.contraction
 
 
-@pytest.mark.parametrize("fixture,rd", [("mlp_rd3", 3), ("mlp_rd1", 1), ("mlp_rd3_sphere", 3), ("mlp_rd1_tanh", 1)])
+@pytest.mark.parametrize("fixture,rd", [("mlp_rd3", 3), ("mlp_rd1", 1), ("mlp_rd3_sphere", 3), ("mlp_rd1_tanh", 1),
+                                        ("mlp_rd1_shifted_softplus", 1), ("mlp_rd3_softplus", 3)])
 @pytest.mark.parametrize("mode,tol_out,tol_grad", [("f32", 1e-4, 1e-4), ("bf16", 2e-3, 3e-2)])
 def test_field_matches_reference_golden(golden_dir, fixture, rd, mode, tol_out, tol_grad):
     """VanillaNeRFRadianceField.forward/backward against the reference run (make_golden.gen_mlp),
-    with the AABB contraction and the unbounded sphere / tanh contractions of configs[3]/[4]."""
+    with the AABB contraction and the unbounded sphere / tanh contractions of configs[3]/[4], and
+    the other density activations of models/nerf.py:20-29 (shifted_softplus, softplus)."""
     nat = _nat()
     z = np.load(os.path.join(golden_dir, fixture + ".npz"))
     contraction = str(z["contraction"]) if "contraction" in z.files else "aabb"
+    density = nat.DENSITY_ACTIVATIONS[str(z["density"])] if "density" in z.files else 0
     p = onerf.build_params(rd, int(z["seed"]))
     flat = flat_from_params(p, rd).to(DEV).requires_grad_(True)
     packed = nat.PackedWeights(mode, rd, DEV)
     packed.pack(flat.detach())
     x = torch.from_numpy(z["x"]).to(DEV)
     d = torch.from_numpy(z["d"]).to(DEV)
-    rgb, sig = nat.field(x, d, flat, dict(_cfg(mode, rd), contraction=CONTRACTION_ID[contraction]), packed)
+    rgb, sig = nat.field(x, d, flat, dict(_cfg(mode, rd), contraction=CONTRACTION_ID[contraction], density=density),
+                         packed)
     e_rgb = rel_err(rgb, z["rgb_f32"])
     e_sig = rel_err(sig, z["sigma_f32"][:, 0])
     print(f"[{mode} {fixture}] field rgb err {e_rgb:.2e} sigma err {e_sig:.2e}")
