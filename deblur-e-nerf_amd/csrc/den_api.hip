@@ -23,6 +23,7 @@
 #include "den_pixbw.hip"
 #include "den_render.hip"
 #include "den_raygrad.hip"
+#include "den_sh.hip"
 
 using namespace den;
 
@@ -1593,6 +1594,25 @@ int den_hashgrid_bwd(const den_ngp_desc* desc, int64_t n, const float* x, const 
   NgpEncArgs E{n, g, x, nullptr, nullptr, d_out, d_table};
   hipLaunchKernelGGL(ngp_encode_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      E);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_sh_encode_fwd(int64_t n, int32_t degree, const float* coords, float* out, void* stream) {
+  if (degree < 1 || degree > SH_MAX_DEG) return fail(DEN_EINVAL, "SH degree must be in 1..8");
+  if (n < 0 || (n > 0 && (!coords || !out))) return fail(DEN_EINVAL, "bad arguments");
+  if (n == 0) return DEN_OK;
+  sh_dispatch(degree, false, n, coords, nullptr, out, (hipStream_t)stream);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_sh_encode_bwd(int64_t n, int32_t degree, const float* coords, const float* d_out, float* d_coords,
+                      void* stream) {
+  if (degree < 1 || degree > SH_MAX_DEG) return fail(DEN_EINVAL, "SH degree must be in 1..8");
+  if (n < 0 || (n > 0 && (!coords || !d_out || !d_coords))) return fail(DEN_EINVAL, "bad arguments");
+  if (n == 0) return DEN_OK;
+  sh_dispatch(degree, true, n, coords, d_out, d_coords, (hipStream_t)stream);
   DEN_LAUNCHED();
   return DEN_OK;
 }

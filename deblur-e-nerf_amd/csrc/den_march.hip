@@ -536,8 +536,13 @@ __global__ void composite_bwd_kernel(CompArgs C) {
     carry += wave_sum(tau);
   }
   const float opacity = wave_sum(op);
-  // pass 2: back to front, suffix_i = sum_{k > i} w_k g_k accumulated directly
+  // pass 2: back to front, suffix_i = sum_{k > i} w_k g_k accumulated directly.  Alpha mode
+  // instead needs S_i = sum_{k > i} alpha_k g_k prod_{i<j<k} (1 - alpha_j) (dL/dalpha_i =
+  // T_i (g_i - S_i), exact also at alpha_i = 1 where the later weights vanish but their
+  // derivatives do not): the back-to-front affine recurrence U_i = alpha_i g_i + (1 - alpha_i)
+  // U_{i+1}, S_i = U_{i+1}, as a wave suffix scan of the maps u -> b + c u.
   float later = 0.0f;  // sum of w g over the blocks after this one
+  float u_carry = 0.0f;  // alpha mode: U at the first sample of the blocks after this one
   const int64_t nb = (s1 - s0 + 63) / 64;
   for (int64_t q = nb - 1; q >= 0; --q) {
     const int64_t s = s0 + q * 64 + lane;
@@ -549,13 +554,28 @@ __global__ void composite_bwd_kernel(CompArgs C) {
     const float incl = wave_incl_suffix(wg);     // sum over lanes >= this one
     const float nxt = __shfl_down(incl, 1, 64);  // sum over lanes > this one (adds only)
     const float suffix = later + (lane < 63 ? nxt : 0.0f);
+    const float g = in ? g_of(s, tmid) : 0.0f;
+    float s_alpha = 0.0f;
+    if (C.alpha) {  // wave-uniform branch
+      const float a = in ? fminf(C.sigma[s], 1.0f) : 0.0f;
+      float b = a * g, c = 1.0f - a;  // identity map on lanes past the ray
+      for (int d = 1; d < 64; d <<= 1) {
+        const float bd = __shfl_down(b, d, 64), cd = __shfl_down(c, d, 64);
+        if (lane + d < 64) {
+          b = b + c * bd;
+          c = c * cd;
+        }
+      }
+      const float u = b + c * u_carry;
+      const float u_next = __shfl_down(u, 1, 64);
+      s_alpha = lane < 63 ? u_next : u_carry;
+      u_carry = __shfl(u, 0, 64);
+    }
     if (in) {
-      const float g = g_of(s, tmid);
       const float w = expf(-excl) * comp_alpha(C, s, tau);
       if (C.alpha) {
-        // dL/dalpha_i = T_i g_i - suffix_i / (1 - alpha_i); at alpha = 1 every later weight is 0
-        const float a = fminf(C.sigma[s], 1.0f);
-        C.d_sigma[s] = expf(-excl) * g - (a < 1.0f ? __fdiv_rn(suffix, 1.0f - a) : 0.0f);
+        // the clamp min(alpha, 1) passes the gradient up to alpha = 1 inclusive (torch.clamp)
+        C.d_sigma[s] = C.sigma[s] > 1.0f ? 0.0f : expf(-excl) * (g - s_alpha);
       } else {
         const float Tnext = expf(-(excl + tau));
         const float dtau = Tnext * g - suffix;

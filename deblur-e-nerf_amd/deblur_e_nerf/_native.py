@@ -125,6 +125,8 @@ _SIGS = {
     "den_ngp_bwd": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64] + [ctypes.c_void_p] * 6),
     "den_hashgrid_fwd": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64] + [ctypes.c_void_p] * 4),
     "den_hashgrid_bwd": (ctypes.c_int, [ctypes.POINTER(NgpDesc), ctypes.c_int64] + [ctypes.c_void_p] * 4),
+    "den_sh_encode_fwd": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 3),
+    "den_sh_encode_bwd": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 4),
     "den_render_ray_grad_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(RenderDesc)]),
     "den_render_ray_grad": (ctypes.c_int, [ctypes.POINTER(RenderDesc), ctypes.POINTER(RenderIO), ctypes.c_void_p,
                                            ctypes.c_int32, ctypes.c_int64] + [ctypes.c_void_p] * 4),
@@ -518,6 +520,35 @@ class HashGridFunction(torch.autograd.Function):
 
 def hashgrid(table, desc, x):
     return HashGridFunction.apply(table, desc, x.float().contiguous())
+
+
+class SHEncodeFunction(torch.autograd.Function):
+    """SHEncoder.forward (external/sh_encoder.py:28-193): coords (n,3) -> (n, degree^2), with the
+    coords gradient of the reference's autograd graph."""
+
+    @staticmethod
+    def forward(ctx, coords, degree):
+        _require_device(coords)
+        n = coords.shape[0]
+        out = torch.empty(n, degree * degree, dtype=torch.float32, device=coords.device)
+        _check(lib().den_sh_encode_fwd(n, degree, _ptr(coords), _ptr(out), _stream(coords.device)))
+        ctx.save_for_backward(coords)
+        ctx.degree = degree
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (coords,) = ctx.saved_tensors
+        d = torch.empty_like(coords)
+        _check(lib().den_sh_encode_bwd(coords.shape[0], ctx.degree, _ptr(coords), _ptr(g.float().contiguous()),
+                                       _ptr(d), _stream(coords.device)))
+        return d, None
+
+
+def sh_encode(coords, degree):
+    if not 1 <= int(degree) <= 8:
+        raise DenError(f"SH degree {degree} outside 1..8 (external/sh_encoder.py:24)")
+    return SHEncodeFunction.apply(coords.float().contiguous(), int(degree))
 
 
 # ----------------------------------------------------------------------------- reductions / adam

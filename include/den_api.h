@@ -501,6 +501,13 @@ int den_hashgrid_fwd(const den_ngp_desc* desc, int64_t n, const float* x, const 
                      void* stream);
 int den_hashgrid_bwd(const den_ngp_desc* desc, int64_t n, const float* x, const float* d_out, float* d_table,
                      void* stream);
+/* SHEncoder alone (external/sh_encoder.py:15-193): real spherical harmonics of degree 1..8 of
+ * coords (n,3) -> out (n, degree^2), the tcnn basis and sign convention, f32; the polynomials are
+ * evaluated as written (unit length is not assumed).  The backward writes d_coords (n,3) =
+ * sum_k d_out[:,k] dY_k/d(x,y,z), the autograd gradient of the reference module. */
+int den_sh_encode_fwd(int64_t n, int32_t degree, const float* coords, float* out, void* stream);
+int den_sh_encode_bwd(int64_t n, int32_t degree, const float* coords, const float* d_out, float* d_coords,
+                      void* stream);
 
 /* ---------------------------------------------------------------- reductions / optimizer */
 /* out[j] = sum_b partial[j*n_blocks + b] for j < n (deterministic order). */

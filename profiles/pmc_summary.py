@@ -85,6 +85,46 @@ def mfma_summary(out_dir, tag, n_simd=1024, prefix=""):
     return res
 
 
+def roofline_check(out_dir, tag, prefix="", phase_reps=3):
+    """roofline.frac reproduced from the rocprofv3 kernel trace of the SAME process that printed the
+    bench line (``<prefix>prof/run_kernel_trace.csv`` + the JSON line in ``<prefix>prof.log``).
+
+    bench.py times the dominant kernel with HIP events during its phase-timing leg (PHASE_REPS
+    steps after the timed region); those are the LAST ``launches_per_step x PHASE_REPS`` launches of
+    that kernel in the trace.  Their rocprof mean, the mean over every launch (cold first steps
+    included -- the r03 discrepancy), and the bench's HIP-event mean are written side by side with
+    the fraction each implies, to ``profiles/<tag>_roofline_check.json``."""
+    with open(os.path.join(out_dir, prefix + "prof.log")) as f:
+        line = [ln for ln in f if ln.startswith("{")][-1]
+    b = json.loads(line)
+    rf = b["roofline"]
+    k = rf["kernel"]
+    ke = rf["kernels"][k]
+    n_phase = ke["launches_per_step"] * phase_reps
+    durs = []
+    with open(os.path.join(out_dir, prefix + "prof", "run_kernel_trace.csv")) as f:
+        for row in csv.DictReader(f):
+            if short(row["Kernel_Name"]) == k:
+                durs.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+    durs = [d for _, d in sorted(durs)]
+    phase = durs[-n_phase:]
+    avg_phase = sum(phase) / len(phase) / 1e6
+    avg_all = sum(durs) / len(durs) / 1e6
+    flop, peak = ke["flop_per_launch"], rf["peak"]
+    frac = lambda ms: round(flop / (ms * 1e-3) / 1e12 / peak, 4)  # noqa: E731
+    res = {"source": f"rocprofv3 --kernel-trace of the bench process whose JSON line is in {prefix}prof.log ({tag})",
+           "kernel": k, "flop_per_launch": flop, "peak_tflops": peak, "launches_total": len(durs),
+           "launches_phase_leg": len(phase),
+           "bench_hip_event_avg_ms": ke["avg_ms"], "bench_frac": rf["frac"],
+           "rocprof_phase_leg_avg_ms": round(avg_phase, 4), "rocprof_phase_leg_frac": frac(avg_phase),
+           "rocprof_all_launches_avg_ms": round(avg_all, 4), "rocprof_all_launches_frac": frac(avg_all),
+           "rocprof_phase_leg_durations_ms": [round(d / 1e6, 4) for d in phase],
+           "hip_event_vs_rocprof": round(ke["avg_ms"] / avg_phase, 4)}
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), f"{tag}_roofline_check.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    return res
+
+
 def main(out_dir, tag, prefix=""):
     here = os.path.dirname(os.path.abspath(__file__))
     fetch = per_launch(os.path.join(out_dir, prefix + "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
@@ -130,6 +170,13 @@ def main(out_dir, tag, prefix=""):
                          f"{v['wave_frac_wait_inst_any']:.2f} | {v['wave_frac_active_inst_any']:.2f} | "
                          f"{v['wave_frac_wait_inst_lds']:.3f} | {v['lds_bank_conflict_frac']:.2f} | "
                          f"{v['valu_mfma_coexec_frac']:.2f} | {v['valu_insts_per_mfma']:.2f} |")
+    if os.path.exists(os.path.join(out_dir, prefix + "prof", "run_kernel_trace.csv")):
+        rc = roofline_check(out_dir, tag, prefix)
+        lines += ["", f"roofline.frac from this trace (profiles/{tag}_roofline_check.json): `{rc['kernel']}`, the "
+                  f"bench's phase-timing launches: HIP events {rc['bench_hip_event_avg_ms']:.3f} ms "
+                  f"(frac {rc['bench_frac']}), rocprof {rc['rocprof_phase_leg_avg_ms']:.3f} ms "
+                  f"(frac {rc['rocprof_phase_leg_frac']}); all {rc['launches_total']} launches incl. cold steps "
+                  f"{rc['rocprof_all_launches_avg_ms']:.3f} ms (frac {rc['rocprof_all_launches_frac']})."]
     with open(os.path.join(here, f"{tag}_kernel_stats.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print(json.dumps(kern, indent=1))

@@ -1199,6 +1199,31 @@ def gen_step_ngp():
     gen_step(False, 1, seed=7, tag="step_ngp_nopixbw_rd1.npz", arch="ngp")
 
 
+def gen_sh():
+    """sh_encoder.npz -- the reference's SHEncoder (external/sh_encoder.py:15-193) at every degree
+    1..8: out = forward(coords) and d_coords = the autograd gradient of sum(out * g).  Coords: 300
+    random unit directions, then 40 non-unit vectors (length 0.3..1.7: the module evaluates its
+    polynomials as written), f32."""
+    she = _refload.load("external.sh_encoder")
+    gen = torch.Generator().manual_seed(31)
+    u = torch.randn(340, 3, generator=gen)
+    u = u / u.norm(dim=-1, keepdim=True)
+    u[300:] *= torch.rand(40, 1, generator=gen) * 1.4 + 0.3
+    coords = u.float()
+    out = {"coords": coords.numpy()}
+    for deg in range(1, 9):
+        enc = she.SHEncoder(n_input_dims=3, degree=deg)
+        x = coords.clone().requires_grad_(True)
+        y = enc(x)
+        g = torch.randn(y.shape, generator=gen)
+        if y.requires_grad:  # degree 1 is the constant band alone: no graph, a zero gradient
+            (y * g).sum().backward()
+        out[f"out_{deg}"] = y.detach().numpy()
+        out[f"g_{deg}"] = g.numpy()
+        out[f"dcoords_{deg}"] = (x.grad if x.grad is not None else torch.zeros_like(x)).numpy()
+    save("sh_encoder.npz", **out)
+
+
 def gen_step_ziggy():
     """step_ziggy_rd1.npz -- configs[3]'s model composition (07_ziggy_and_fuzz_hdr.yaml:28-139): the
     ngp arch with the unbounded-sphere contraction of its aabb, near 0.01 / far 13, cone-angle

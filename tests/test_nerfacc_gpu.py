@@ -272,3 +272,55 @@ def test_trajectory_matches_reference(golden_dir):
     traj(torch.tensor([float(z["T_wc_timestamp"][-1]) + 1.0], dtype=torch.float64, device=DEV))
     with pytest.raises(AssertionError):
         traj.check()
+
+
+def test_vol_rendering_alpha_saturated_matches_autograd():
+    """rgb_alpha_fn with alphas at and beyond 1 (the kernel's min(alpha, 1)): renders and the alpha /
+    rgb / background gradients against torch autograd of the product form in f64 on the CPU
+    (w_i = a_i prod_{j<i} (1 - a_j), a = clamp(alpha, max=1)).  Ragged rays across the 64-sample
+    wave blocks, an empty ray, alpha = 0, alpha = 1 mid-ray (its derivative keeps the later samples'
+    terms) and alpha > 1 (zero derivative)."""
+    from deblur_e_nerf.external.vol_rendering import rendering
+    gen = torch.Generator().manual_seed(11)
+    lens = [0, 1, 5, 63, 64, 65, 130, 200, 17, 90]
+    R, rd = len(lens), 3
+    ri = torch.cat([torch.full((n,), r, dtype=torch.int32) for r, n in enumerate(lens)])
+    n = ri.numel()
+    t0 = torch.rand(n, 1, generator=gen)
+    t1 = t0 + torch.rand(n, 1, generator=gen) * 0.1
+    alpha = torch.rand(n, 1, generator=gen) * 0.08
+    starts = torch.tensor([0] + lens).cumsum(0)
+    alpha[starts[2] + 2] = 1.0     # saturates ray 2 mid-way
+    alpha[starts[6] + 70] = 1.0    # ray 6, second wave block
+    alpha[starts[7] + 10] = 1.3    # ray 7: clamp active, zero derivative
+    alpha[starts[8] + 3] = 0.0
+    rgb = torch.rand(n, rd, generator=gen)
+    bk = torch.rand(rd, generator=gen)
+    gc, go, gd = torch.randn(R, rd, generator=gen), torch.randn(R, 1, generator=gen), torch.randn(R, 1, generator=gen)
+
+    a_d, rgb_d, bk_d = (v.double().requires_grad_(True) for v in (alpha, rgb, bk))
+    cols, ops, dps = [], [], []
+    for r in range(R):
+        sl = slice(int(starts[r]), int(starts[r + 1]))
+        a = a_d[sl, 0].clamp(max=1.0)
+        T = torch.cat([torch.ones(1, dtype=torch.float64), torch.cumprod(1 - a, 0)[:-1]])
+        w = a * T
+        op = w.sum()
+        cols.append((w[:, None] * rgb_d[sl]).sum(0) + bk_d * (1 - op))
+        ops.append(op.reshape(1))
+        dps.append((w * ((t0[sl, 0] + t1[sl, 0]).double() / 2)).sum().reshape(1))
+    col_r, op_r, dp_r = torch.stack(cols), torch.stack(ops), torch.stack(dps)
+    ((col_r * gc.double()).sum() + (op_r * go.double()).sum() + (dp_r * gd.double()).sum()).backward()
+
+    a_g, rgb_g, bk_g = (v.to(DEV).requires_grad_(True) for v in (alpha, rgb, bk))
+    col, op, dp = rendering(t0.to(DEV), t1.to(DEV), ri.to(DEV), R, rgb_alpha_fn=lambda a, b, c: (rgb_g, a_g),
+                            render_bkgd=bk_g)
+    for x, ref in ((col, col_r), (op, op_r), (dp, dp_r)):
+        assert float((x.detach().cpu().double() - ref.detach()).abs().max()) <= 2e-6
+    ((col * gc.to(DEV)).sum() + (op * go.to(DEV)).sum() + (dp * gd.to(DEV)).sum()).backward()
+    for x, ref, k in ((a_g.grad, a_d.grad, "alpha"), (rgb_g.grad, rgb_d.grad, "rgb"), (bk_g.grad, bk_d.grad, "bkgd")):
+        e = float((x.cpu().double() - ref).abs().max() / ref.abs().max())
+        print(f"  d{k}: max err {e:.2e}")
+        assert e <= 1e-5, k
+    assert float(a_g.grad[starts[7] + 10]) == 0.0
+    assert float(a_d.grad[starts[2] + 2].abs()) > 0 and float(a_g.grad[starts[2] + 2].abs()) > 0

@@ -133,6 +133,38 @@ def test_ngp_field_large_batch_equals_chunks():
     assert max(errs.values()) < 1e-4, errs
 
 
+def test_ngp_query_density_under_autograd():
+    """query_density with autograd on is differentiable (the reference's tcnn path is): sigma and its
+    parameter and position gradients equal those of forward()'s density output; under no_grad it
+    takes the density-only kernel and returns the same values."""
+    from deblur_e_nerf.external import ngp
+    torch.manual_seed(6)
+    f = ngp.NGPradianceField(aabb=[-1.5, -1.5, -1.5, 1.5, 1.5, 1.5], pos_encoding_config=dict(ongp.POS_ENCODING),
+                             mlp_base_config=dict(ongp.MLP_BASE, hidden_activation=torch.nn.Softplus(beta=100),
+                                                  density_activation=ngp.shifted_trunc_exp),
+                             mlp_head_config=dict(ongp.MLP_HEAD, hidden_activation=torch.nn.Softplus(beta=100),
+                                                  radiance_activation=torch.nn.Softplus(beta=1), output_dim=1)).to(DEV)
+    with torch.no_grad():
+        f.mlp_base[0].params.mul_(1e3)
+    x = (torch.rand(3000, 3, device=DEV) * 3 - 1.5).requires_grad_(True)
+    g = torch.randn(3000, 1, device=DEV)
+    sig = f.query_density(x)
+    (sig * g).sum().backward()
+    gq = {k: p.grad.clone() for k, p in f.named_parameters()}
+    gx = x.grad.clone()
+    f.zero_grad()
+    x.grad = None
+    d = torch.zeros_like(x)
+    d[:, 2] = 1.0
+    _, sig_f = f(x, d)
+    (sig_f * g).sum().backward()
+    assert torch.equal(sig.detach(), sig_f.detach())
+    assert all(torch.equal(gq[k], p.grad) or _tensor_rel(gq[k], p.grad) < 1e-5 for k, p in f.named_parameters())
+    assert _tensor_rel(gx, x.grad) < 1e-5
+    with torch.no_grad():
+        assert torch.equal(f.query_density(x.detach()), sig.detach())
+
+
 @pytest.mark.parametrize("otype,log2", [("HashGrid", 19), ("HashGrid", 12), ("DenseGrid", 19)])
 def test_hashgrid_matches_oracle(otype, log2):
     """den_hashgrid_fwd / bwd (tcnn.Encoding) vs oracle/tcnn.py on random points, including

@@ -270,3 +270,17 @@ def test_trajectory_oracle_matches_reference(golden_dir):
     for q, kp, kr in (("query_ts", "position", "rotation"), ("query_ts_2d", "position_2d", "rotation_2d")):
         p, r = otr.linear_trajectory(T, P, Q, torch.from_numpy(z[q]))
         assert torch.equal(p, torch.from_numpy(z[kp])) and torch.equal(r, torch.from_numpy(z[kr]))
+
+
+@pytest.mark.parametrize("degree", range(1, 9))
+def test_sh_oracle_matches_reference(golden_dir, degree):
+    """oracle/sh.py (Legendre-derivative restatement) vs the reference SHEncoder's outputs and autograd
+    gradients (make_golden.gen_sh), degrees 1..8, unit and non-unit coords: f32 rounding only."""
+    from oracle import sh as osh
+    z = _load(golden_dir, "sh_encoder.npz")
+    out = osh.sh_encode(z["coords"], degree)
+    ref = z[f"out_{degree}"]
+    assert np.abs(out - ref).max() <= 1e-6 * np.abs(ref).max()
+    g = osh.sh_encode_grad(z["coords"], degree, z[f"g_{degree}"])
+    gref = z[f"dcoords_{degree}"]
+    assert np.abs(g - gref).max() <= 1e-6 * max(np.abs(gref).max(), 1.0)
