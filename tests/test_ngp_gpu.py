@@ -247,14 +247,19 @@ def test_ngp_sparse_gradient_scatter_matches_oracle():
 
 
 def test_ngp_density_only_refuses_grad():
-    """query_density's density-only pass keeps no backward state: under autograd it raises
-    instead of returning a zero gradient."""
+    """The density-only kernel pass keeps no backward state: asked for a parameter gradient it raises
+    instead of returning a zero one (query_density sends differentiable calls through the full field
+    instead: test_ngp_query_density_under_autograd)."""
+    from deblur_e_nerf import _native
     from deblur_e_nerf.external import ngp
     f = ngp.NGPradianceField(aabb=[-1.5, -1.5, -1.5, 1.5, 1.5, 1.5]).to(DEV)
+    x = torch.zeros(64, 3, device=DEV)
+    d = torch.zeros(64, 3, device=DEV)
+    d[:, 2] = 1.0
     with pytest.raises(NotImplementedError):
-        f.query_density(torch.zeros(64, 3, device=DEV))
+        _native.ngp_field(f.flat_leaf(), f.desc, x, d, density_only=True)
     with torch.no_grad():
-        assert f.query_density(torch.zeros(64, 3, device=DEV)).shape[0] == 64
+        assert f.query_density(x).shape[0] == 64
 
 
 def test_ngp_rejects_host_tensors():
