@@ -77,10 +77,6 @@ struct TimedLaunch {
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-#ifndef DEN_LB_HIDDEN
-#define DEN_LB_HIDDEN 1  // BF16: Lb^T + its weight gradient as a layer-major launch (den_hidden.hip);
-                         // 0 = in render_bwd_kernel + a streamed weight gradient (r03: 1.6-2 ms slower)
-#endif
 
 
 struct WsLayout {
@@ -138,7 +134,7 @@ WsLayout ws_layout(const den_render_desc* d) {
   // workgroup + the stage-1 rows of its reduction
   L.lr_partial = off;
   L.lr_stage1 = off;
-  if (d->train && use_hidden_path(d) && DEN_LR_FUSED) {
+  if (d->train && use_hidden_path(d)) {
     off += align256((size_t)(n / wg_samples(d->mode)) * LR_PART * 4);
     L.lr_stage1 = off;
     off += align256((size_t)LR_G1 * LR_PART * 4);
@@ -429,12 +425,12 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
         // head (compositing adjoint, Lr^T, Lg^T[, Lb^T]) sample-major, then [Lb,] L7..L1 layer-major
         {
           DEN_TIMED(T_RENDER_BWD, s);
-          hipLaunchKernelGGL((render_bwd_kernel<MODE, DEN_LB_HIDDEN ? 1 : 2>), dim3((unsigned)(n / wg_samples(MODE))),
+          hipLaunchKernelGGL((render_bwd_kernel<MODE, 1>), dim3((unsigned)(n / wg_samples(MODE))),
                              dim3(512), 0, s, A);
         }
         DEN_LAUNCHED();
-        if (DEN_LB_HIDDEN && DEN_LR_FUSED && (rc = launch_lr_reduce(d, L, ws, G, s)) != DEN_OK) return rc;
-        for (int l = DEN_LB_HIDDEN ? 8 : 7; l >= 1; --l)
+        if ((rc = launch_lr_reduce(d, L, ws, G, s)) != DEN_OK) return rc;
+        for (int l = 8; l >= 1; --l)
           if ((rc = launch_hidden(d, io, L, ws, l, G, s)) != DEN_OK) return rc;
       }
     }
@@ -452,17 +448,9 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
       return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s)) != DEN_OK) return rc;
-    if (!DEN_LB_HIDDEN) {
-      if ((rc = launch_dwstream<9, 9, 8, 8, DWS_NW2, 3>(d, L, ws, D_ZB, -1, A_S0 + 7, -1, s)) != DEN_OK) return rc;
-      if ((rc = launch_dwstream_reduce(d, L, ws, 9, 8, 0, 9, L_B, 256, 0, 1, G, s)) != DEN_OK) return rc;
-    }
     if ((rc = launch_dwstream<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 4, 9, 0, 4, L_G, 256, WIDTH, 1, G, s)) != DEN_OK) return rc;
-    if (!(DEN_LB_HIDDEN && DEN_LR_FUSED)) {  // else inside render_bwd_kernel<1, 1>
-      if ((rc = launch_dwstream<1, 1, 4, 4, DWS_NW4, DWS_D4, DWS_U4>(d, L, ws, D_ZR, -1, A_G, -1, s)) != DEN_OK)
-        return rc;
-      if ((rc = launch_dwstream_reduce(d, L, ws, 1, 4, 0, 1, L_R, 128, 0, 1, G, s)) != DEN_OK) return rc;
-    }
+    // (Lb's weight gradient comes from its hidden launch, Lr's from render_bwd_kernel<1, 1>)
     if (g->grad_bkgd) {
       hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(1024), 0, s, d->radiance_dim, d->n_rays,
                          (const float*)(ws + L.bkgd_partial), g->grad_bkgd);
@@ -764,7 +752,7 @@ int den_pixbw_fwd(int32_t S, int32_t N, int32_t reset, const float* it, const do
   if (!out || (reset && !delta_out)) return fail(DEN_EINVAL, "out (and delta_out for a reset call) are required");
   A.out = out;
   A.delta_out = delta_out;
-  if (DEN_PIXBW_SEGPAR && S - 1 <= PIXBW_WAVE_SEGS)
+  if (S - 1 <= PIXBW_WAVE_SEGS)
     hipLaunchKernelGGL(pixbw_fwd_wave_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, (hipStream_t)stream, A);
   else
     hipLaunchKernelGGL(pixbw_fwd_kernel, dim3((unsigned)den_pixbw_blocks(N)), dim3(PIXBW_BLOCK), 0, (hipStream_t)stream, A);
@@ -787,11 +775,9 @@ int den_pixbw_bwd(int32_t S, int32_t N, int32_t reset, const float* it, const do
   A.d_it = d_it;
   A.d_delta_in = d_delta_in;
   A.d_prm = d_prm;
-#if DEN_PIXBW_SEGPAR
   const int64_t seg_threads = 4 * (int64_t)(S - 1) * N;
   hipLaunchKernelGGL(pixbw_seg_kernel, dim3((unsigned)((seg_threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
   DEN_LAUNCHED();
-#endif
   hipLaunchKernelGGL(pixbw_bwd_kernel, dim3((unsigned)den_pixbw_blocks(N)), dim3(PIXBW_BLOCK), 0, (hipStream_t)stream, A);
   DEN_LAUNCHED();
   return DEN_OK;
@@ -980,7 +966,7 @@ int den_march_count(int32_t n_rays, const float* rays_o, const float* rays_d, co
   if (rc) return rc;
   if (!counts) return fail(DEN_EINVAL, "counts is required");
   M.counts = counts;
-  if (DEN_MARCH_WAVE && M.contraction != CONTRACT_AABB)
+  if (M.contraction != CONTRACT_AABB)
     hipLaunchKernelGGL(march_wave_kernel<false>, dim3((n_rays + 3) / 4), dim3(256), 0, (hipStream_t)stream, M);
   else
     hipLaunchKernelGGL(march_kernel<false>, dim3((n_rays + 127) / 128), dim3(128), 0, (hipStream_t)stream, M);
@@ -1000,7 +986,7 @@ int den_march_fill(int32_t n_rays, const float* rays_o, const float* rays_d, con
   M.ray_idx = ray_indices;
   M.t0 = t_starts;
   M.t1 = t_ends;
-  if (DEN_MARCH_WAVE && M.contraction != CONTRACT_AABB)
+  if (M.contraction != CONTRACT_AABB)
     hipLaunchKernelGGL(march_wave_kernel<true>, dim3((n_rays + 3) / 4), dim3(256), 0, (hipStream_t)stream, M);
   else
     hipLaunchKernelGGL(march_kernel<true>, dim3((n_rays + 127) / 128), dim3(128), 0, (hipStream_t)stream, M);

@@ -3,10 +3,7 @@
 // over all ray samples, for the GEMMs the layer-major hidden backward (den_hidden.hip) does not
 // cover, fused by shared operand so that every operand byte is read from HBM once:
 //   {L0, L5's pe columns}  A = [dz_0 | dz_5] (16 row tiles), B = pe (2 column tiles)
-//   {Lb, sigma}            A = dz_b (9 row tiles: bottleneck + sigma), B = S'_7 (8 column tiles) --
-//                          only in the DEN_LB_HIDDEN = 0 build (Lb runs layer-major in den_hidden.hip)
 //   Lg                     A = dz_g (4 row tiles), B = [bottleneck | ve] (9 column tiles)
-//   Lr                     A = dz_r (1 row tile),  B = g (4 column tiles)
 // Layout and machinery as den_hidden.hip: one persistent workgroup per CU sweeps a contiguous
 // range of 32-sample wave blocks; the (MT + NT) 2 KiB tiles of a block arrive by untracked LDS-DMA
 // DEPTH blocks ahead into an XOR-permuted ring slot (hb_slot: conflict-free transposed reads);
@@ -21,13 +18,13 @@
 
 namespace den {
 
-// waves per workgroup of the streamed weight-gradient launches {L0 + L5 pe}, Lb, Lg, Lr, and the
-// ring shapes of the Lg / Lr launches (r02 / r03 A/B, profiles/r0{2,3}_*experiments.txt: 4 -> 16
+// waves per workgroup of the streamed weight-gradient launches {L0 + L5 pe} and Lg, and the ring
+// shape of the Lg launch (Lb's and Lr's weight gradients come from den_hidden.hip and
+// render_bwd_kernel<1, 1>) (r02 / r03 A/B, profiles/r0{2,3}_*experiments.txt: 4 -> 16
 // waves took the {L0 + L5 pe} / Lg launches from 13.0 to 10.8 ms per step; U = 4 wave blocks per Lr
 // ring step with 3 steps in flight and U = 2 with 2 for Lg, 7.6 -> 6.6 ms)
-constexpr int DWS_NW1 = 16, DWS_NW2 = 8, DWS_NW3 = 16, DWS_NW4 = 4;
+constexpr int DWS_NW1 = 16, DWS_NW3 = 16;
 constexpr int DWS_D3 = 2, DWS_U3 = 2;  // Lg: ring steps in flight, wave blocks per step (26 KiB each)
-constexpr int DWS_D4 = 3, DWS_U4 = 4;  // Lr: the same (10 KiB each)
 
 struct DwStreamArgs {
   const char* a[2];     // dz tensors (wave-block major), row tiles [0, MA) from a[0], [MA, MT) from a[1]
@@ -172,10 +169,8 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
   }
 }
 
-// the launches of a BF16 backward (Lb + sigma: DEN_LB_HIDDEN = 0 only)
+// the launches of a BF16 backward
 template __global__ void dwstream_kernel<8, 16, 2, 2, DWS_NW1, 3>(DwStreamArgs);  // L0 + L5 pe
-template __global__ void dwstream_kernel<9, 9, 8, 8, DWS_NW2, 3>(DwStreamArgs);    // Lb + sigma
 template __global__ void dwstream_kernel<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3>(DwStreamArgs);    // Lg
-template __global__ void dwstream_kernel<1, 1, 4, 4, DWS_NW4, DWS_D4, DWS_U4>(DwStreamArgs);  // Lr
 
 }  // namespace den

@@ -213,9 +213,6 @@ __global__ void march_kernel(MarchArgs P) {
 // the occupied steps in order with a ballot prefix count.  One dependent occupancy load per 64 steps
 // instead of per step, and 64x the threads (march_kernel runs one thread per ray: a 2,040-ray call
 // is 32 waves on a 256-CU chip, latency-bound at ~0.6 ms).
-#ifndef DEN_MARCH_WAVE
-#define DEN_MARCH_WAVE 1  // 0: march_kernel for every contraction
-#endif
 template <bool FILL>
 __global__ __launch_bounds__(256) void march_wave_kernel(MarchArgs P) {
 #pragma clang fp contract(off)

@@ -25,12 +25,9 @@ namespace den {
 
 constexpr int PIXBW_BLOCK = 64;    // one wave per block
 constexpr int PIXBW_NPARAM = 7;
-#ifndef DEN_PIXBW_SEGPAR
-#define DEN_PIXBW_SEGPAR 1  // 0: the per-event serial backward (matrix exponentials inside the sweeps)
-#endif
 // workspace doubles per segment: Phi (16), Bd (4), Btd (4), then (segment-parallel backward) the four
 // Frechet derivatives L(X, E_m) (4 x 16)
-constexpr int PIXBW_SEG_F = DEN_PIXBW_SEGPAR ? 24 + 64 : 24;
+constexpr int PIXBW_SEG_F = 24 + 64;  // per segment: Phi, B_d, B~_d, then the four L(X, E_m)
 constexpr double PIXBW_NS = 1e-9;  // PixelBandwidth.NS_TO_S
 
 // ------------------------------------------------------------------ dual numbers
@@ -450,7 +447,6 @@ __device__ double pb_seg_bwd(const PixArgs& A, int n, const PixPrm& P, int k, co
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 1; j < 4; ++j) phib[4 * i + j] -= g1b[i];
-#if DEN_PIXBW_SEGPAR
   // Phi = e^X: the four entries of dL/dX = L(X^T, dL/dPhi) the parameters reach, as
   // <E_m, L(X^T, G)> = <L(X, E_m), G> with the L(X, E_m) of pixbw_seg_kernel
   double fr[4];
@@ -465,19 +461,6 @@ __device__ double pb_seg_bwd(const PixArgs& A, int n, const PixPrm& P, int k, co
   bb -= dt * fr[1];
   wsb += dt * fr[2];
   wdb += dt * fr[3];
-#else
-  // Phi = e^X:  dL/dX = L(X^T, dL/dPhi) = tangent of e^(X^T + eps dL/dPhi)
-  Mat4<Dual> XT, R;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) XT.e[4 * i + j] = Dual{X.e[4 * j + i], phib[4 * i + j]};
-  mat_exp(XT, R);
-  ab -= dt * R.e[0].d;
-  bb -= dt * R.e[1].d;
-  wsb += dt * (R.e[9].d - R.e[10].d);
-  wdb += dt * (R.e[14].d - R.e[15].d);
-#endif
   // linearized_sys_params (:183-191) chain rule
   const double tin = P.kin / I1, tmil = P.kmil / I1, pp = (tin + tmil) * P.tout;
   const double aamp = 1.0 / P.ainv, aloop = 1.0 / P.linv;
@@ -547,7 +530,7 @@ __global__ __launch_bounds__(PIXBW_BLOCK) void pixbw_bwd_kernel(PixArgs A) {
     const int S = A.S, N = A.N, no = A.reset ? 2 : 1;
     const PixPrm P = pb_params(A.prm);
     double y[2] = {0.0, 0.0}, den[2] = {1.0, 1.0};
-    pb_sweep<true, DEN_PIXBW_SEGPAR != 0>(A, n, P, y, den);
+    pb_sweep<true, true>(A, n, P, y, den);
     // adjoints of the weighted outputs
     double yb[2] = {0.0, 0.0};
     const double g = (double)A.d_out[n];

@@ -19,9 +19,6 @@
 namespace den {
 
 constexpr int LDS_BUF = CHUNK_MAX;  // bytes per ring slot
-#ifndef DEN_LR_FUSED
-#define DEN_LR_FUSED 1  // BF16 layer-major path: the Lr weight gradient inside render_bwd_kernel<1, 1>
-#endif
 
 template <int MODE>
 struct RenderArgs {
@@ -788,7 +785,7 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
 
 // LAST_J = NBL - 1: the whole chain (F32 parity mode).  LAST_J = 2: stop after Lb^T (writes
 // dz_7); the hidden layers then run layer-major in den_hidden.hip (BF16 mode).  LAST_J = 1: stop
-// after Lg^T (writes dz_b with the sigma tile; Lb^T runs layer-major too, DEN_LB_HIDDEN).
+// after Lg^T (writes dz_b with the sigma tile; Lb^T runs layer-major, den_hidden.hip).
 // Fused Lr weight gradient (BF16, LAST_J = 1): dW_r = dz_r^T G over the workgroup's samples by MFMA
 // (k = samples, both operands by transposed LDS reads as in den_hidden.hip), instead of a streamed
 // launch that re-reads G and dz_r.  Per wave an LDS scratch holds a dz_r tile replicated at stored
@@ -806,7 +803,7 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
   using Acc = typename T::Acc;
   constexpr int TM = T::TM, FPT = T::FPT, REGS = T::REGS;
   constexpr int WGS = wg_samples(MODE);
-  constexpr bool FUSE_LR = MODE == 1 && LAST_J == 1 && DEN_LR_FUSED;
+  constexpr bool FUSE_LR = MODE == 1 && LAST_J == 1;
   __shared__ __attribute__((aligned(16))) char lds[2 * LDS_BUF + WGS * 16 + (FUSE_LR ? 8 * LRW_SCR : 0)];
   float* rec_lds = (float*)(lds + 2 * LDS_BUF);
 
@@ -1052,6 +1049,5 @@ template __global__ void render_fwd_kernel<1, false>(RenderArgs<1>);
 template __global__ void render_fwd_kernel<1, true>(RenderArgs<1>);
 template __global__ void render_bwd_kernel<0, NBL - 1>(RenderArgs<0>);
 template __global__ void render_bwd_kernel<1, NBL - 1>(RenderArgs<1>);
-template __global__ void render_bwd_kernel<1, 2>(RenderArgs<1>);
 
 }  // namespace den
