@@ -724,7 +724,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
   wait_vm_lgkm0<0>();
 #ifdef DEN_FWD_PROF
   prof[6] = __builtin_amdgcn_s_memtime();
-  if (blockIdx.x < 512 && lane == 0) {
+  if (blockIdx.x < 512 && (threadIdx.x & 63) == 0) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) den_fwd_prof[(blockIdx.x * 8 + wave) * 8 + q] = prof[q];
   }

@@ -44,10 +44,13 @@ def main():
     assert lib.den_debug_fwd_prof(buf.ctypes.data) == 0
     p = buf.reshape(512, 8, 8).astype(np.float64)
     waves = p[:, :, 6] > 0
-    start, pro, lay, end = p[:, :, 3], p[:, :, 4], p[:, :, 5], p[:, :, 6]
+    # persistent kernel (r04): [0..2] summed body / vmcnt wait / barrier cycles of the weight-chunk
+    # steps, [3] kernel start, [4] summed item prologues (sampling + encoding), [5] summed item
+    # tails (activations + compositing), [6] kernel end
+    start, end = p[:, :, 3], p[:, :, 6]
     tot = (end - start)[waves]
-    print(f"train={train} waves={waves.sum()} (workgroups from DEN_FWD_PROF_BASE) wave cycles mean {tot.mean():.0f}")
-    for name, v in (("prologue", (pro - start)[waves]), ("layers", (lay - pro)[waves]), ("tail", (end - lay)[waves])):
+    print(f"train={train} waves={waves.sum()} (first 512 workgroups) wave cycles mean {tot.mean():.0f}")
+    for name, v in (("prologues", p[:, :, 4][waves]), ("tails", p[:, :, 5][waves])):
         print(f"  {name:9s} {v.mean():10.0f} cyc/wave ({v.mean() / tot.mean() * 100:5.1f} %)")
     for q, name in enumerate(["body", "vm wait", "barrier"]):
         v = p[:, :, q][waves]
