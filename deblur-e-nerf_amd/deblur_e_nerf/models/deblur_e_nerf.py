@@ -27,9 +27,10 @@ provides the few Trainer attributes the step reads (``trainer.accumulate_grad_ba
 ``global_step``, ``log``, ``all_gather``); ``fit_step`` runs one optimisation step (forward,
 backward, DDP-style gradient all-reduce, optimizer) without a Trainer.
 
-Evaluation (validation / test epochs with the affine + black-level correction and
-SSIM / LPIPS) is outside the hot path; ``render_image_eval`` + ``loss_metric.metric`` give the
-rendered image and its PSNR.
+Evaluation: ``render_image_eval`` renders an image, ``evaluation_correction``
+is the reference's CPU f64 intensity correction (affine log-intensity fit + the black-level
+refinement by Gauss-Newton / Levenberg-Marquardt) and ``loss_metric.metric`` gives the PSNR; the
+Lightning validation loop and SSIM / LPIPS are outside the scope.
 """
 import functools
 import math
@@ -459,14 +460,14 @@ class DeblurENeRF(_Base):
         return intensity
 
 
-def affine_log_intensity_correction(pred_intensity_img, target_intensity_img, gain_exposure_prod=None,
-                                    has_bayer_filter=False, per_channel_log_it_scale=False):
-    """The evaluation's affine log-intensity alignment (deblur_e_nerf.py:705-833, without the joint
-    black-level refinement, the LM step of :835-900, out of scope): the predicted log intensities
-    mapped by the least-squares (f64) scale and offset -- per channel, or one scale and per-channel
-    offsets for a Bayer sensor without ``per_channel_log_it_scale`` -- onto the targets'
-    (normalised by the mean-normalised gain-exposure product).  Images ([B,] [1/3,] H, W) ->
-    (corrected predicted intensities (B, 1/3, H, W), gamma, scale)."""
+def _affine_log_fit(pred_intensity_img, target_intensity_img, gain_exposure_prod, has_bayer_filter,
+                    per_channel_log_it_scale):
+    """deblur_e_nerf.py:705-811: the least-squares (f64) log-intensity scale and offset -- per
+    channel, or one scale and per-channel offsets for a Bayer sensor without
+    ``per_channel_log_it_scale`` -- of the predicted onto the target log intensities (normalised by
+    the mean-normalised gain-exposure product).  -> corrected log predictions (B, C, H, W) f64 in the
+    normalised domain, the targets (B, C, H, W), the normalised gain-exposure products (B,) f64,
+    their logs (B, 1, 1, 1), gamma, scale."""
     pred, target = pred_intensity_img.detach().cpu(), target_intensity_img.detach().cpu()
     while target.dim() < 3:
         pred, target = pred[None], target[None]
@@ -475,7 +476,8 @@ def affine_log_intensity_correction(pred_intensity_img, target_intensity_img, ga
     B, C, H, W = target.shape
     gep = torch.ones(B, dtype=torch.float64) if gain_exposure_prod is None else \
         torch.as_tensor(gain_exposure_prod, dtype=torch.float64).reshape(B)
-    log_gep = (gep / gep.mean()).log().view(B, 1, 1, 1).to(target.dtype)
+    nge = gep / gep.mean()
+    log_gep = nge.log().view(B, 1, 1, 1).to(target.dtype)
     # logs in the images' dtype, f64 only for the least squares (the reference's order, :729-792)
     plog = pred.log().to(torch.float64)
     tlog = (target.log() - log_gep).to(torch.float64)
@@ -491,14 +493,87 @@ def affine_log_intensity_correction(pred_intensity_img, target_intensity_img, ga
     if not per_channel:
         A, y = A.flatten(0, 1), y.flatten(0, 1)
     sol = torch.linalg.lstsq(A, y).solution
-    corr = (A @ sol)
-    corr = corr.view(C, B, H, W).transpose(0, 1)
+    corr = (A @ sol).view(C, B, H, W).transpose(0, 1)
     if per_channel:
         gamma, scale = sol[:, 0, 0], sol[:, 1, 0].exp()
     else:
         gamma, scale = sol[0, :], sol[1:, 0].exp()
+    return corr, target, nge, log_gep, gamma, scale
+
+
+def affine_log_intensity_correction(pred_intensity_img, target_intensity_img, gain_exposure_prod=None,
+                                    has_bayer_filter=False, per_channel_log_it_scale=False):
+    """The evaluation's affine log-intensity alignment alone (deblur_e_nerf.py:705-833 with
+    ``black_level_offset`` false): images ([B,] [1/3,] H, W) -> (corrected predicted intensities
+    (B, 1/3, H, W), gamma, scale).  ``evaluation_correction`` adds the black-level refinement."""
+    corr, _, _, log_gep, gamma, scale = _affine_log_fit(pred_intensity_img, target_intensity_img,
+                                                       gain_exposure_prod, has_bayer_filter, per_channel_log_it_scale)
     # black_level_offset off: the gain-exposure normalisation undone on the prediction (:819-826)
     return (corr + log_gep).exp(), gamma, scale
+
+
+def init_correction_params(has_bayer_filter, per_channel_log_it_scale=False):
+    """DeblurENeRF.__init__'s initial refinement parameters (deblur_e_nerf.py:173-195): scale 1,
+    offset 0 per radiance channel, gamma 1 per channel or shared (f64)."""
+    rd = 3 if has_bayer_filter else 1
+    per_channel = (not has_bayer_filter) or per_channel_log_it_scale
+    return (torch.ones((rd, 1, 1, 1), dtype=torch.float64),
+            torch.ones((rd if per_channel else 1, 1, 1, 1), dtype=torch.float64),
+            torch.zeros((rd, 1, 1, 1), dtype=torch.float64))
+
+
+def evaluation_correction(pred_intensity_img, target_intensity_img, gain_exposure_prod=None,
+                          has_bayer_filter=False, correction=None, init=None):
+    """The evaluation's intensity correction (deblur_e_nerf.py:705-935) on the CPU in f64, as the
+    reference runs it: the affine log-intensity fit, then -- with ``correction.black_level_offset``
+    (every shipped config) -- the joint gamma / scale / black-level refinement of an
+    ``OffsetGammaCorrection`` by Gauss-Newton or Levenberg-Marquardt (``correction.optimizer``: algo
+    "gn" | "lm", max_steps, lm.radius), stopped early once the error and the parameters stop moving.
+
+    ``correction`` is the config's EasyDict (per_channel_log_it_scale, black_level_offset,
+    optimizer); ``init`` the warm-start (scale, gamma, offset) the reference carries across
+    evaluations (``init_correction_params`` when None).  Returns an EasyDict: ``pred`` corrected
+    intensities (B, 1/3, H, W), ``target`` (B, 1/3, H, W), effective ``gamma``, ``scale``, ``offset``
+    (None without the refinement), per-step ``errors`` and the ``converged`` (scale, gamma, offset)
+    for the next warm start."""
+    from ..external import optimizer as opt_lib
+    from ..utils import modules as mod
+    from .offset_gamma_correction import OffsetGammaCorrection
+    cfg = correction if correction is not None else EasyDict(per_channel_log_it_scale=False,
+                                                              black_level_offset=False)
+    corr, target, nge, log_gep, gamma, scale = _affine_log_fit(pred_intensity_img, target_intensity_img,
+                                                               gain_exposure_prod, has_bayer_filter,
+                                                               cfg.per_channel_log_it_scale)
+    if not cfg.black_level_offset:
+        return EasyDict(pred=(corr + log_gep).exp(), target=target, gamma=gamma, scale=scale, offset=None,
+                        errors=None, converged=None)
+    pred = corr.exp().unsqueeze(-1)                      # (B, C, H, W, 1), f64
+    tgt = target.unsqueeze(-1)                           # (B, C, H, W, 1)
+    init = init_correction_params(has_bayer_filter, cfg.per_channel_log_it_scale) if init is None else init
+    model = OffsetGammaCorrection(nge.view(-1, 1, 1, 1, 1), *init)
+    o = cfg.optimizer
+    if o.algo == "gn":
+        optimizer = opt_lib.GaussNewton(model, solver=opt_lib.LSTSQ())
+    elif o.algo == "lm":
+        optimizer = opt_lib.LevenbergMarquardt(model, strategy=opt_lib.TrustRegion(**dict(o.lm)))
+    else:
+        raise NotImplementedError(o.algo)
+    n = tgt.numel()
+    with torch.no_grad():
+        errors = [float(optimizer.model.loss(input=pred, target=tgt)) / n]
+    for _ in range(1, int(o.max_steps) + 1):
+        prev = list(mod.detach_clone_named_parameters(model))
+        errors.append(float(optimizer.step(input=pred, target=tgt)) / n)
+        if (torch.allclose(torch.tensor(errors[-1], dtype=torch.float64), torch.tensor(errors[-2], dtype=torch.float64))
+                and mod.named_parameters_allclose(model, prev)):
+            break
+    conv = {k: v.detach().clone() for k, v in model.named_parameters()}
+    with torch.no_grad():
+        out = model(pred).squeeze(-1)
+    return EasyDict(pred=out, target=target, gamma=gamma * conv["gamma"][:, 0, 0, 0],
+                    scale=scale.pow(conv["gamma"][:, 0, 0, 0]) * conv["scale"][:, 0, 0, 0],
+                    offset=conv["offset"][:, 0, 0, 0], errors=torch.tensor(errors, dtype=torch.float64),
+                    converged=(conv["scale"], conv["gamma"], conv["offset"]))
 
 
 def allreduce_gradients(module):

@@ -46,3 +46,15 @@ def freeze(module):
 def unfreeze(module):
     for p in module.parameters():
         p.requires_grad_(True)
+
+
+def detach_clone_named_parameters(module):
+    """utils/modules.py:38-42: (name, detached copy) of every parameter."""
+    return ((name, p.detach().clone()) for name, p in module.named_parameters())
+
+
+def named_parameters_allclose(module, other_named_parameters):
+    """utils/modules.py:45-57: every parameter allclose to its recorded copy."""
+    mine, other = dict(module.named_parameters()), dict(other_named_parameters)
+    assert mine.keys() == other.keys()
+    return all(torch.allclose(mine[k], other[k]) for k in mine)

@@ -1224,6 +1224,29 @@ def gen_sh():
     save("sh_encoder.npz", **out)
 
 
+def gen_correction():
+    """correction.npz -- the reference's OffsetGammaCorrection (models/offset_gamma_correction.py:4-167)
+    on random positive inputs (B 3, C 3, H 4, W 5, R 1) with per-channel and shared parameters:
+    forward, jacobian(), param_jacobian()."""
+    ogc = _refload.load("models.offset_gamma_correction")
+    gen = torch.Generator().manual_seed(41)
+    x = torch.rand(3, 3, 4, 5, 1, generator=gen, dtype=torch.float64) * 0.9 + 0.05
+    cs = torch.rand(3, 1, 1, 1, 1, generator=gen, dtype=torch.float64) + 0.5
+    out = {"x": x.numpy(), "const_scale": cs.numpy()}
+    for tag, nS, nG, nO in (("pc", 3, 3, 3), ("shared_gamma", 3, 1, 3), ("scalar", 1, 1, 1)):
+        sc = torch.rand(nS, 1, 1, 1, generator=gen, dtype=torch.float64) + 0.5
+        ga = torch.rand(nG, 1, 1, 1, generator=gen, dtype=torch.float64) + 0.5
+        of = torch.rand(nO, 1, 1, 1, generator=gen, dtype=torch.float64) * 0.1
+        m = ogc.OffsetGammaCorrection(cs, sc, ga, of)
+        with torch.no_grad():
+            out[f"{tag}_scale"], out[f"{tag}_gamma"], out[f"{tag}_offset"] = sc.numpy(), ga.numpy(), of.numpy()
+            out[f"{tag}_y"] = m(x).numpy()
+            out[f"{tag}_jac"] = m.jacobian(x)[0].numpy()
+            for name, j in zip(("scale", "gamma", "offset"), m.param_jacobian(x)[0]):
+                out[f"{tag}_pjac_{name}"] = j.numpy()
+    save("correction.npz", **out)
+
+
 def gen_step_ziggy():
     """step_ziggy_rd1.npz -- configs[3]'s model composition (07_ziggy_and_fuzz_hdr.yaml:28-139): the
     ngp arch with the unbounded-sphere contraction of its aabb, near 0.01 / far 13, cone-angle

@@ -1,11 +1,21 @@
-"""The evaluation's affine log-intensity alignment (models/deblur_e_nerf.affine_log_intensity_correction,
-the reference's deblur_e_nerf.py:705-833 without the black-level LM refinement): host-side f64
-least squares, checked on CPU against a known affine map and against the closed-form regression."""
+"""The evaluation's intensity correction (the reference's deblur_e_nerf.py:705-935, CPU f64 as the
+reference runs it): the affine log-intensity alignment (``affine_log_intensity_correction``) against
+a known affine map and the closed-form regression; the black-level refinement
+(``evaluation_correction``): ``OffsetGammaCorrection`` forward / jacobians against the reference
+module's outputs (tests/golden/correction.npz, make_golden.gen_correction), the Levenberg-Marquardt
+and Gauss-Newton refinements against scipy.optimize.least_squares (MINPACK "lm") on the same
+residual -- pypose, whose optimizers the reference subclasses, is not installed: its per-step
+trajectory is parity unpinned, the converged correction is pinned."""
 import math
 
 import torch
 
-from deblur_e_nerf.models.deblur_e_nerf import affine_log_intensity_correction
+import numpy as np
+import pytest
+
+from deblur_e_nerf.models.deblur_e_nerf import affine_log_intensity_correction, evaluation_correction
+from deblur_e_nerf.models.offset_gamma_correction import OffsetGammaCorrection
+from deblur_e_nerf.utils.easydict import EasyDict
 
 
 def test_recovers_known_affine_map_grayscale():
@@ -49,3 +59,83 @@ def test_bayer_shared_scale_per_channel_offsets():
     _, gamma3, scale3 = affine_log_intensity_correction(pred, target, has_bayer_filter=True,
                                                         per_channel_log_it_scale=True)
     assert gamma3.shape == (3,) and scale3.shape == (3,)
+
+
+@pytest.mark.parametrize("tag", ["pc", "shared_gamma", "scalar"])
+def test_offset_gamma_correction_matches_reference(golden_dir, tag):
+    z = np.load(f"{golden_dir}/correction.npz")
+    x = torch.from_numpy(z["x"])
+    m = OffsetGammaCorrection(torch.from_numpy(z["const_scale"]), torch.from_numpy(z[f"{tag}_scale"]),
+                              torch.from_numpy(z[f"{tag}_gamma"]), torch.from_numpy(z[f"{tag}_offset"]))
+    with torch.no_grad():
+        assert np.array_equal(m(x).numpy(), z[f"{tag}_y"])
+        np.testing.assert_allclose(m.jacobian(x)[0].numpy(), z[f"{tag}_jac"], rtol=1e-14, atol=0)
+        for name, j in zip(("scale", "gamma", "offset"), m.param_jacobian(x)[0]):
+            np.testing.assert_allclose(j.numpy(), z[f"{tag}_pjac_{name}"], rtol=1e-14, atol=0)
+
+
+def _scene(seed, B=3, H=18, W=22, gep=(1.0, 2.0, 1.5), noise=0.01):
+    """Targets = a known offset-gamma map of the predictions, with per-image gain-exposure and noise."""
+    g = torch.Generator().manual_seed(seed)
+    pred = torch.rand(B, H, W, generator=g) * 0.85 + 0.1
+    nge = torch.tensor(gep, dtype=torch.float64)
+    nge = (nge / nge.mean()).view(B, 1, 1)
+    target = nge * (1.4 * pred.double().pow(0.8) - 0.06) + noise * torch.rand(B, H, W, generator=g, dtype=torch.float64)
+    return pred, target.float().clamp_min(1e-3), torch.tensor(gep)
+
+
+def _scipy_refine(res_pred, target, nge, x0):
+    from scipy.optimize import least_squares
+    p, t, c = res_pred.numpy().ravel(), target.double().numpy().ravel(), nge.numpy().ravel()
+
+    def f(v):
+        return c * (v[0] * p ** v[1] - v[2]) - t
+    return least_squares(f, x0, method="lm", xtol=1e-15, ftol=1e-15, gtol=1e-15, max_nfev=10000).x
+
+
+@pytest.mark.parametrize("algo", ["lm", "gn"])
+def test_black_level_refinement_converges_to_least_squares(algo):
+    pred, target, gep = _scene(7)
+    cfg = EasyDict(per_channel_log_it_scale=False, black_level_offset=True,
+                   optimizer=EasyDict(algo=algo, max_steps=60, lm=EasyDict(radius=1e6)))
+    r = evaluation_correction(pred, target, gep, False, cfg)
+    errs = r.errors.numpy()
+    assert (np.diff(errs) <= 1e-15).all(), errs                 # LM and GN never raise the error here
+    # the same problem for scipy: the refinement acts on the affine-corrected predictions
+    base = evaluation_correction(pred, target, gep, False, EasyDict(per_channel_log_it_scale=False,
+                                                                    black_level_offset=False))
+    lg = (gep.double() / gep.double().mean()).log().view(-1, 1, 1, 1)
+    res_pred = (base.pred.log() - lg).exp()                     # back to the normalised domain
+    nge = (gep.double() / gep.double().mean()).view(-1, 1, 1, 1).expand_as(res_pred)
+    x = _scipy_refine(res_pred, target.unsqueeze(1), nge, [1.0, 1.0, 0.0])
+    sc, ga, of = (float(v.reshape(-1)[0]) for v in r.converged)
+    print(f"  {algo}: {len(errs) - 1} steps, error {errs[0]:.3e} -> {errs[-1]:.3e}; "
+          f"(scale, gamma, offset) {sc:.6f} {ga:.6f} {of:.6f} vs scipy {x[0]:.6f} {x[1]:.6f} {x[2]:.6f}")
+    np.testing.assert_allclose([sc, ga, of], x, rtol=1e-6, atol=1e-9)
+    # the effective correction composes the affine fit with the refinement (:920-928)
+    assert torch.allclose(r.gamma, base.gamma * ga) and torch.allclose(r.offset, torch.tensor([of], dtype=torch.float64))
+
+
+def test_black_level_refinement_config_steps_and_warm_start():
+    """The shipped configs' refinement (lm, max_steps 10, radius 1e6): at most 10 steps, an early stop
+    once error and parameters settle, and a warm start from the converged values stops at once."""
+    pred, target, gep = _scene(8)
+    cfg = EasyDict(per_channel_log_it_scale=False, black_level_offset=True,
+                   optimizer=EasyDict(algo="lm", max_steps=10, lm=EasyDict(radius=1e6)))
+    r = evaluation_correction(pred, target, gep, False, cfg)
+    assert 2 <= len(r.errors) <= 11 and r.pred.shape == (3, 1, 18, 22)
+    again = evaluation_correction(pred, target, gep, False, cfg, init=r.converged)
+    assert len(again.errors) <= 3 and abs(float(again.errors[-1] - r.errors[-1])) <= 1e-12 * float(r.errors[-1])
+
+
+def test_black_level_refinement_bayer_shapes():
+    """A Bayer sensor without per-channel scale: scale / offset per channel, one gamma."""
+    g = torch.Generator().manual_seed(9)
+    pred = torch.rand(2, 3, 10, 12, generator=g) * 0.8 + 0.1
+    target = (1.2 * pred.double().pow(0.9) - 0.02).float().clamp_min(1e-3)
+    cfg = EasyDict(per_channel_log_it_scale=False, black_level_offset=True,
+                   optimizer=EasyDict(algo="lm", max_steps=10, lm=EasyDict(radius=1e6)))
+    r = evaluation_correction(pred, target, None, True, cfg)
+    assert [tuple(v.shape) for v in r.converged] == [(3, 1, 1, 1), (1, 1, 1, 1), (3, 1, 1, 1)]
+    assert r.scale.shape == (3,) and r.gamma.shape == (1,) and r.offset.shape == (3,)  # (:806-810, :924-928)
+    assert float((r.pred - target.double()).abs().max()) < 1e-3
