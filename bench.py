@@ -499,7 +499,7 @@ def aligned_psnr(pred, tgt, nv, view, dev=None):
     return fn(corr.float(), tgt[:, None], rng), fn(pred[:, None], tgt[:, None], rng), float(gamma[0]), float(scale[0])
 
 
-def psnr_long(rd, dev, steps=None, modes=("f32", "bf16"), n_events=None):
+def psnr_long(rd, dev, steps=None, modes=("f32", "bf16", "f32_reseeded"), n_events=None):
     """BASELINE's "PSNR vs ref" at convergence (PSNR_LEG): the HIP TrainStep in F32 (the reference's
     arithmetic, pinned to the reference at 1e-4 by tests/) and in BF16 (the benchmark's mode) train
     from ONE init on a teacher scene for `steps` Adam steps, each on a fresh batch of configs[0]'s
@@ -534,10 +534,13 @@ def psnr_long(rd, dev, steps=None, modes=("f32", "bf16"), n_events=None):
     if fx is not None and (int(fx["steps"]) != steps or n_events != L["n_events"]):
         fx = None
     out = {}
-    for mode in modes:
+    for name in modes:
+        # "f32_reseeded": F32 again on another batch sequence -- the spread of the run itself, the
+        # scale against which the BF16 and oracle differences are read (the leg is not at convergence)
+        mode = name.split("_")[0]
         ts = TrainStep(n_events, n_samples=n_samples, radiance_dim=rd, mode=mode, device=dev,
                        seed=L["student_seed"])
-        gen = torch.Generator().manual_seed(L["batch_seed"])
+        gen = torch.Generator().manual_seed(L["batch_seed"] + (1 if name.endswith("reseeded") else 0))
         t0 = time.perf_counter()
         lr0 = ts.lr
         for it in range(steps):
@@ -563,9 +566,11 @@ def psnr_long(rd, dev, steps=None, modes=("f32", "bf16"), n_events=None):
             # the HIP-trained views against the oracle-trained ones (range of the oracle's render)
             e["psnr_vs_oracle_render_db"] = round(psnr(hv[:, 0].reshape(nv, 1, view, view),
                                                        orc.reshape(nv, 1, view, view), float(orc.max())), 2)
-        out[mode] = e
+        out[name] = e
         del ts
         torch.cuda.empty_cache()
+    if "f32" in out and "f32_reseeded" in out:
+        out["run_spread_db"] = round(out["f32_reseeded"]["psnr_db"] - out["f32"]["psnr_db"], 4)
     if fx is not None:
         out["oracle"] = {"psnr_db": round(float(fx["psnr_db"]), 3),
                          "psnr_uncorrected_db": round(float(fx["psnr_uncorrected_db"]), 3),
@@ -756,13 +761,6 @@ def main():
                     psnr_info = dict(psnr_info or {}, converged=psnr_long(a.rd, dev, steps=a.psnr_steps))
                 except Exception as e:  # pragma: no cover - reported, not fatal
                     psnr_info = dict(psnr_info or {}, converged={"error": repr(e)})
-                try:  # the same from one init, twice as long on batches twice as large (HIP F32 vs BF16
-                    # only: the oracle would take ~9 h of CPU for it), where training has converged far
-                    # enough that ΔPSNR is the arithmetic's, not the run's
-                    psnr_info["converged_2x"] = psnr_long(a.rd, dev, steps=2 * a.psnr_steps,
-                                                          n_events=2 * PSNR_LEG["n_events"])
-                except Exception as e:  # pragma: no cover - reported, not fatal
-                    psnr_info["converged_2x"] = {"error": repr(e)}
     if rank == 0:
         out = {
             "metric": metric_name(a),
