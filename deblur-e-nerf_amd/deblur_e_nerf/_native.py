@@ -145,6 +145,9 @@ _SIGS = {
 }
 
 
+ABI_VERSION = 4  # include/den_api.h DEN_VERSION
+
+
 def lib():
     """Load libden.so (raises DenError if it is missing)."""
     global _lib
@@ -157,6 +160,8 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if L.den_version() != ABI_VERSION:  # the ctypes structs below must match the library's
+            raise DenError(f"{LIB_PATH} has C-ABI version {L.den_version()}, these bindings {ABI_VERSION}: rebuild it")
         _lib = L
     return _lib
 

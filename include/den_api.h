@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define DEN_VERSION 3
+#define DEN_VERSION 4  /* 4: density_activation in den_render_desc / den_ngp_desc; den_sh_encode_* */
 
 enum den_status {
   DEN_OK = 0,
