@@ -3,5 +3,5 @@
 set -e
 mkdir -p gpurun_out
 for r in 131072 65536 32768 16384; do
-  timeout -k 10 240 python bench.py --rays $r --steps 20 --warmup 3 --no-cpu-baseline --no-gemm-peak > gpurun_out/strong_$r.log 2>&1
+  timeout -k 10 240 python bench.py --rays $r --steps 20 --warmup 3 --no-cpu-baseline --no-gemm-peak --no-extra-legs --psnr-steps 0 > gpurun_out/strong_$r.log 2>&1
 done
