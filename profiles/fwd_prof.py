@@ -55,6 +55,11 @@ def main():
     for q, name in enumerate(["body", "vm wait", "barrier"]):
         v = p[:, :, q][waves]
         print(f"    {name:8s} {v.mean():10.0f} cyc/wave ({v.mean() / tot.mean() * 100:5.1f} %)")
+    # by wave index: waves w and w + 4 share SIMD w; waves 0 .. rays_per_wg - 1 composite a ray in each
+    # item's tail (den_render.hip)
+    for name, q in (("tails", 5), ("barrier", 2), ("body", 0)):
+        row = [p[:, w, q][waves[:, w]].mean() / tot.mean() * 100 for w in range(8)]
+        print(f"  {name:8s} by wave: " + " ".join(f"{x:5.1f}" for x in row) + " %")
     per_wave = p[:, :, 0][waves]
     print(f"  body min/max over waves {per_wave.min():.0f} / {per_wave.max():.0f}")
     wg0 = start[:, 0][waves[:, 0]]
