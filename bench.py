@@ -59,6 +59,9 @@ def parse():
                     help="skip the configs[2] (pixel bandwidth on) and F32-mode legs of the N = 1 line")
     ap.add_argument("--cpu-stub", action="store_true",
                     help="launcher test only: gloo on the CPU, a stub step of the same sharding, no GPU")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1 collective backend: nccl (= RCCL, one GPU per rank) or gloo (rehearsal of the "
+                         "N-rank GPU path with every rank on a shared GPU: rank r on device r mod count)")
     return ap.parse_args()
 
 
@@ -665,8 +668,14 @@ def main():
         return
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "gloo":
+            # rehearsal: RCCL refuses two ranks on one device, gloo all-reduces the GPU buffers
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         world = dist.get_world_size()
     dev = torch.device("cuda", local)
     from deblur_e_nerf import _native as nat
@@ -772,7 +781,9 @@ def main():
                                    f"mlp 8x256 rd={a.rd}, event prep+rays+fwd+bwd+allreduce+Adam",
                        "rays_per_step": a.rays, "rays_per_rank": rays_per_rank, "samples_per_ray": a.samples,
                        "events_per_step": a.rays // per_event,
-                       "parallelism": f"ray-dp{world}"},
+                       "parallelism": f"ray-dp{world}",
+                       "collective": (("rccl" if a.dist_backend == "nccl" else "gloo (shared-GPU rehearsal)")
+                                      if world > 1 else None)},
             "loss": [round(x, 6) for x in loss],
             "roofline": roofline,
             "cpu_baseline": cpu,
