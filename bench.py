@@ -540,10 +540,12 @@ def psnr_long(rd, dev, steps=None, modes=("f32", "bf16", "f32_reseeded"), n_even
     for name in modes:
         # "f32_reseeded": F32 again on another batch sequence -- the spread of the run itself, the
         # scale against which the BF16 and oracle differences are read (the leg is not at convergence)
-        mode = name.split("_")[0]
+        # ("<mode>_s<k>": batch sequence k, the seed study of profiles/psnr_seeds.py)
+        mode, _, tag = name.partition("_")
+        shift = 1 if tag == "reseeded" else int(tag[1:]) if tag.startswith("s") else 0
         ts = TrainStep(n_events, n_samples=n_samples, radiance_dim=rd, mode=mode, device=dev,
                        seed=L["student_seed"])
-        gen = torch.Generator().manual_seed(L["batch_seed"] + (1 if name.endswith("reseeded") else 0))
+        gen = torch.Generator().manual_seed(L["batch_seed"] + shift)
         t0 = time.perf_counter()
         lr0 = ts.lr
         for it in range(steps):

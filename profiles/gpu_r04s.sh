@@ -6,4 +6,5 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 400 python -u bench.py --gpus 2 --dist-backend gloo --steps 5 --warmup 2 --no-extra-legs --psnr-steps 0 > gpurun_out/r04s_n2.log 2>&1
 timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 --no-extra-legs --psnr-steps 0 --no-cpu-baseline > gpurun_out/r04s_n1.log 2>&1
+timeout -k 10 500 python -u profiles/psnr_seeds.py --seeds 8 > gpurun_out/r04s_psnr_seeds.log 2>&1
 echo done
