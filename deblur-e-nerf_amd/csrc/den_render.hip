@@ -114,17 +114,38 @@ DEN_HD constexpr int fwd_waves(int mode) { return 8; }
 DEN_HD constexpr int fwd_threads(int mode) { return 64 * fwd_waves(mode); }
 DEN_HD constexpr int fwd_wg_samples(int mode) { return fwd_waves(mode) * fwd_nb(mode) * tm_of(mode); }
 DEN_HD constexpr int fwd_min_waves(int mode) { return 2; }  // 256 registers per wave
+// LDS layout of the forward: [bias table | per-sample records | ring] with DEN_FWD_BIAS0 (the bias
+// reads' addresses then fit the 16-bit immediate offset of ds_read: no per-tile address VALU),
+// else [ring | bias table | records]
+#ifdef DEN_FWD_BIAS0
+DEN_HD constexpr int fwd_ring_off(int mode) {
+  return (int)((bias_floats(mode) * 4 + fwd_wg_samples(mode) * 16 + 1023) / 1024 * 1024);
+}
+DEN_HD constexpr int fwd_bias_off(int mode) { return 0; }
+#else
+DEN_HD constexpr int fwd_ring_off(int mode) { return 0; }
+DEN_HD constexpr int fwd_bias_off(int mode) { return FWD_RING * FWD_SLOT; }
+#endif
 
+// wofs: this wave's 1 KiB piece offset, wave * 1024, as a wave-uniform (SGPR) value
 template <int NTH>
-__device__ __forceinline__ void dma_chunk_untracked(const char* g, char* lds_slot, int bytes) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+__device__ __forceinline__ void dma_chunk_untracked(const char* g, char* lds_slot, int bytes, int wofs) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int q = 0; q < (FWD_SLOT + NTH * 16 - 1) / (NTH * 16); ++q) {
+#ifdef DEN_FWD_M0S
+    // scalar piece offset and LDS address: no per-piece readfirstlane (nor its SGPR hazard)
+    const int off = q * NTH * 16 + wofs;
+    if (off < bytes) {
+      const char* base = g + off;
+      const uint32_t m0 = (uint32_t)(uintptr_t)(lds_ptr_t)lds_slot + (uint32_t)off;
+#else
     // wave-uniform offset (readfirstlane is 32-bit: never pass it a 64-bit pointer)
-    const int off = __builtin_amdgcn_readfirstlane(q * NTH * 16 + wave * 1024);
+    const int off = __builtin_amdgcn_readfirstlane(q * NTH * 16 + (int)(threadIdx.x >> 6) * 1024);
     if (off < bytes) {
       const char* base = g + off;
       const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(lds_slot + off));
+#endif
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"((uint32_t)lane * 16),
                    "s"(base), "s"(m0) : "memory", "m0");
     }
@@ -167,6 +188,7 @@ __device__ __forceinline__ void wait_vm_lgkm0_rt(int n) {
 // so the counts restart at 0.
 struct FwdVm {
   int issued;
+  int wofs;  // this wave's DMA piece offset (wave * 1024), wave-uniform
   int hist[FWD_RING - 1];
 #ifdef DEN_FWD_PROF
   // experiment builds only: cycles in body / vmcnt wait / barrier, kernel start, item prologues,
@@ -181,7 +203,7 @@ __device__ uint64_t den_fwd_prof[512 * 8 * 8];
 // One forward step on chunk t (in ring slot `slot`, run-time 0..FWD_RING-1): issue chunk
 // t+FWD_RING-1 into the slot chunk t-1 used (free since the last barrier), run `body` on chunk t
 // (it issues n_st stores), wait for chunk t+1, barrier.
-template <int NTH, typename Body>
+template <int NTH, int RING_OFF, typename Body>
 __device__ __forceinline__ void fwd_step(char* lds, const char* wbase, int slot, int64_t off_n, int bytes_n,
                                          int n_st, FwdVm& vm, Body&& body) {
   constexpr int R = FWD_RING;
@@ -189,14 +211,14 @@ __device__ __forceinline__ void fwd_step(char* lds, const char* wbase, int slot,
   const uint64_t p0 = __builtin_amdgcn_s_memtime();
 #endif
   const int dst = slot == 0 ? R - 1 : slot - 1;  // (slot + R - 1) % R
-  dma_chunk_untracked<NTH>(wbase + off_n, lds + dst * FWD_SLOT, bytes_n);
+  dma_chunk_untracked<NTH>(wbase + off_n, lds + RING_OFF + dst * FWD_SLOT, bytes_n, vm.wofs);
   // the DMA ops EVERY wave issues (some issue one more): an under-count, so the count stays a
   // compile-time constant and each wait an immediate
   vm.issued += bytes_n / (NTH * 16);
 #pragma unroll
   for (int k = 0; k + 1 < R - 1; ++k) vm.hist[k] = vm.hist[k + 1];
   vm.hist[R - 2] = vm.issued;
-  body(lds + slot * FWD_SLOT);
+  body(lds + RING_OFF + slot * FWD_SLOT);
 #ifdef DEN_FWD_PROF
   const uint64_t p1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -400,7 +422,7 @@ __device__ __forceinline__ void fwd_layer(const AT& A, char* lds, int slot0, int
         if (i < NT) {
           const char* tile = chunk + j * TILE_BYTES;
           Acc acc[NB];
-          const float* bias = (const float*)(lds + FWD_RING * FWD_SLOT) + (CB + i) * TM + grp * T::REGS;
+          const float* bias = (const float*)(lds + fwd_bias_off(MODE)) + (CB + i) * TM + grp * T::REGS;
 #pragma unroll
           for (int r = 0; r < T::REGS; ++r) acc[0][r] = bias[r];
 #pragma unroll
@@ -430,7 +452,7 @@ __device__ __forceinline__ void fwd_layer(const AT& A, char* lds, int slot0, int
       const int i = c * FWD_G + j;
       if (i < NT && i >= 2) n_st += fwd_store_ops<MODE, TRAIN, EPI, NB>(i - 2);
     }
-    fwd_step<fwd_threads(MODE)>(lds, A.w, fwd_slot(slot0, GB + c), noff, nbytes, n_st, vm, body);
+    fwd_step<fwd_threads(MODE), fwd_ring_off(MODE)>(lds, A.w, fwd_slot(slot0, GB + c), noff, nbytes, n_st, vm, body);
   }
   if constexpr (DEFER) {
 #pragma unroll
@@ -454,8 +476,8 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
   constexpr int NTH = fwd_threads(MODE);
   constexpr int NBIAS = (int)bias_floats(MODE);
   constexpr int NCH = fwd_item_chunks(MODE);
-  __shared__ __attribute__((aligned(16))) char lds[FWD_RING * FWD_SLOT + NBIAS * 4 + WGS * 16];
-  float* bias_lds = (float*)(lds + FWD_RING * FWD_SLOT);
+  __shared__ __attribute__((aligned(1024))) char lds[FWD_RING * FWD_SLOT + (fwd_ring_off(MODE) > 0 ? fwd_ring_off(MODE) : NBIAS * 4 + WGS * 16)];
+  float* bias_lds = (float*)(lds + fwd_bias_off(MODE));
   float* rec_lds = bias_lds + NBIAS;
 
   const int wave = threadIdx.x >> 6;
@@ -471,7 +493,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
     int64_t off_c;
     int bytes_c;
     fwd_ahead<MODE>(0, 0, ch, &off_c, &bytes_c);
-    dma_chunk_untracked<NTH>(A0.w + off_c, lds + ch * FWD_SLOT, bytes_c);
+    dma_chunk_untracked<NTH>(A0.w + off_c, lds + fwd_ring_off(MODE) + ch * FWD_SLOT, bytes_c, __builtin_amdgcn_readfirstlane(wave * 1024));
   }
   int slot0 = 0;  // ring slot of the current item's chunk 0
 
@@ -500,6 +522,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
     for (int b = 0; b < NB; ++b) sample[b] = item * WGS + (wave * NB + b) * TM + c;
     FwdVm vm;
     vm.issued = 0;
+    vm.wofs = __builtin_amdgcn_readfirstlane((tid >> 6) * 1024);
 #pragma unroll
     for (int k = 0; k < FWD_RING - 1; ++k) vm.hist[k] = 0;
 #ifdef DEN_FWD_PROF
