@@ -114,18 +114,14 @@ DEN_HD constexpr int fwd_waves(int mode) { return 8; }
 DEN_HD constexpr int fwd_threads(int mode) { return 64 * fwd_waves(mode); }
 DEN_HD constexpr int fwd_wg_samples(int mode) { return fwd_waves(mode) * fwd_nb(mode) * tm_of(mode); }
 DEN_HD constexpr int fwd_min_waves(int mode) { return 2; }  // 256 registers per wave
-// LDS layout of the forward: [bias table | per-sample records | ring] with DEN_FWD_BIAS0 (the bias
-// reads' addresses then fit the 16-bit immediate offset of ds_read: no per-tile address VALU),
-// else [ring | bias table | records]
-#ifdef DEN_FWD_BIAS0
+// LDS layout of the forward: [bias table | per-sample records | weight ring].  With the bias table
+// first, a tile's bias reads address it by the 16-bit immediate offset of ds_read (behind the ring,
+// at 120 KiB, every tile computed its bias addresses by VALU; r04 ISA budget: -2.7 % issue cycles
+// together with the scalar DMA offsets below).
 DEN_HD constexpr int fwd_ring_off(int mode) {
   return (int)((bias_floats(mode) * 4 + fwd_wg_samples(mode) * 16 + 1023) / 1024 * 1024);
 }
 DEN_HD constexpr int fwd_bias_off(int mode) { return 0; }
-#else
-DEN_HD constexpr int fwd_ring_off(int mode) { return 0; }
-DEN_HD constexpr int fwd_bias_off(int mode) { return FWD_RING * FWD_SLOT; }
-#endif
 
 // wofs: this wave's 1 KiB piece offset, wave * 1024, as a wave-uniform (SGPR) value
 template <int NTH>
@@ -133,19 +129,11 @@ __device__ __forceinline__ void dma_chunk_untracked(const char* g, char* lds_slo
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int q = 0; q < (FWD_SLOT + NTH * 16 - 1) / (NTH * 16); ++q) {
-#ifdef DEN_FWD_M0S
     // scalar piece offset and LDS address: no per-piece readfirstlane (nor its SGPR hazard)
     const int off = q * NTH * 16 + wofs;
     if (off < bytes) {
       const char* base = g + off;
       const uint32_t m0 = (uint32_t)(uintptr_t)(lds_ptr_t)lds_slot + (uint32_t)off;
-#else
-    // wave-uniform offset (readfirstlane is 32-bit: never pass it a 64-bit pointer)
-    const int off = __builtin_amdgcn_readfirstlane(q * NTH * 16 + (int)(threadIdx.x >> 6) * 1024);
-    if (off < bytes) {
-      const char* base = g + off;
-      const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(lds_slot + off));
-#endif
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"((uint32_t)lane * 16),
                    "s"(base), "s"(m0) : "memory", "m0");
     }
@@ -476,7 +464,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
   constexpr int NTH = fwd_threads(MODE);
   constexpr int NBIAS = (int)bias_floats(MODE);
   constexpr int NCH = fwd_item_chunks(MODE);
-  __shared__ __attribute__((aligned(1024))) char lds[FWD_RING * FWD_SLOT + (fwd_ring_off(MODE) > 0 ? fwd_ring_off(MODE) : NBIAS * 4 + WGS * 16)];
+  __shared__ __attribute__((aligned(1024))) char lds[fwd_ring_off(MODE) + FWD_RING * FWD_SLOT];
   float* bias_lds = (float*)(lds + fwd_bias_off(MODE));
   float* rec_lds = bias_lds + NBIAS;
 
