@@ -453,6 +453,7 @@ __device__ __forceinline__ void fwd_layer(const AT& A, char* lds, int slot0, int
 
 // ------------------------------------------------------------------ forward kernel
 template <int MODE, bool TRAIN>
+__attribute__((aligned(4096)))  // page-aligned code (r04y A/B)
 __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render_fwd_kernel(RenderArgs<MODE> A0) {
   using T = Tr<MODE>;
   using Frag = typename T::Frag;
@@ -808,8 +809,8 @@ constexpr int LRW_SCR = 4096;  // bytes of LDS scratch per wave
 constexpr int LR_PART = 388;   // floats per workgroup partial: 4 x 3 x 32 + 3 bias + 1 pad
 
 template <int MODE, int LAST_J>
-// Page-aligned code: the same instructions ran 2.84-2.85 ms at 0x...100 / 0x...000 page offsets and
-// 2.95-3.14 ms at 0x...900 (r04u / r04w same-box A/B, profiles/r04w_ab.json)
+// Page-aligned code, as every hot kernel here: the same render_bwd instructions ran 0.1-0.3 ms
+// apart at different code addresses (r04u / r04w / r04y same-box A/B, profiles/r04{w,y}_ab.json)
 __attribute__((aligned(4096)))
 __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) {
   using T = Tr<MODE>;
