@@ -442,37 +442,51 @@ def _teacher_batch(gen, n_events, dev="cpu", motion=0.3, radius=4.03):
     return {k: t.to(dev) for k, t in b.items()}
 
 
-VIEW_DIRS = ((0.62, -0.55, 0.56), (-0.7, 0.3, 0.4), (0.1, 0.8, -0.5), (-0.4, -0.6, -0.3))
-# the converged-PSNR leg: Adam steps, events per batch, samples per ray, view size, lr cuts, seeds
-PSNR_LEG = dict(steps=1000, n_events=512, n_samples=64, view=64, milestones=(0.5, 0.8), batch_seed=123,
-                teacher_seed=77, student_seed=0)
+VIEW_DIRS = ((0.62, -0.55, 0.56), (-0.7, 0.3, 0.4), (0.1, 0.8, -0.5), (-0.4, -0.6, -0.3),
+             (0.3, 0.3, 0.9), (-0.8, -0.5, 0.2), (0.7, 0.6, -0.2), (-0.2, 0.4, -0.9))
+# the converged-PSNR leg: Adam steps, events per batch, samples per ray, views (count, size), lr cuts
+# (x lr_gamma at each milestone fraction of the run), the teacher's density bias and colour-head
+# output scale, seeds (teacher init, student init, the first batch sequence)
+# (r05: chosen by profiles/psnr_sweep.py -- the sequence-to-sequence std of the converged PSNR,
+# profiles/r05a_psnr_sweep.jsonl; 1,500 steps reach the plateau that 3,000 do)
+PSNR_LEG = dict(steps=1500, n_events=128, n_samples=64, view=32, n_views=8, milestones=(0.3, 0.6, 0.85), lr_gamma=0.3,
+                lr0=0.01, teacher_sigma_bias=3.0, teacher_rgb_scale=1.0, batch_seed=123, teacher_seed=77,
+                student_seed=0)
 
 
-def teacher_field(rd):
+def psnr_leg(**over):
+    """PSNR_LEG with overrides (profiles/psnr_sweep.py, make_psnr_oracle.py --leg)."""
+    bad = set(over) - set(PSNR_LEG)
+    if bad:
+        raise KeyError(f"unknown PSNR leg keys {sorted(bad)}")
+    return dict(PSNR_LEG, **over)
+
+
+def teacher_field(rd, leg=None):
     """The converged leg's teacher: the benchmark architecture with another seeded init, the
-    density raised (an opaque scene) and the colour head's output weights x8 (colour contrast on
-    the surfaces: view std ~0.14 of a [0.18, 1] range, against ~0.06 unscaled); -> flat f32
-    parameters (CPU)."""
+    density raised by `teacher_sigma_bias` (an opaque scene) and the colour head's output weights
+    x `teacher_rgb_scale` (colour contrast on the surfaces); -> flat f32 parameters (CPU)."""
     from deblur_e_nerf.external import mlp, ngp
-    torch.manual_seed(PSNR_LEG["teacher_seed"])
+    L = leg or PSNR_LEG
+    torch.manual_seed(L["teacher_seed"])
     field = mlp.VanillaNeRFRadianceField([-1.5, -1.5, -1.5, 1.5, 1.5, 1.5], radiance_dim=rd,
                                          hidden_activation=torch.nn.Softplus(beta=100),
                                          density_activation=ngp.shifted_trunc_exp,
                                          radiance_activation=torch.nn.Softplus(beta=1), mode="f32")
     with torch.no_grad():
-        field.mlp.sigma_layer.output_layer.bias.add_(3.0)
-        field.mlp.rgb_layer.output_layer.weight.mul_(8.0)
+        field.mlp.sigma_layer.output_layer.bias.add_(float(L["teacher_sigma_bias"]))
+        field.mlp.rgb_layer.output_layer.weight.mul_(float(L["teacher_rgb_scale"]))
     return field.flat_params.detach().clone()
 
 
-def psnr_views(view):
-    """The converged leg's four held-out views: rays (CPU) and their count."""
-    rays = [_view_rays(view, direction=v) for v in VIEW_DIRS]
-    return torch.cat([r[0] for r in rays]), torch.cat([r[1] for r in rays]), len(VIEW_DIRS)
+def psnr_views(view, n_views=4):
+    """The converged leg's held-out views: rays (CPU) and their count."""
+    rays = [_view_rays(view, direction=v) for v in VIEW_DIRS[:n_views]]
+    return torch.cat([r[0] for r in rays]), torch.cat([r[1] for r in rays]), n_views
 
 
-def lr_at(lr0, it, steps, milestones):
-    return lr0 * 0.3 ** sum(it >= int(m * steps) for m in milestones)
+def lr_at(lr0, it, steps, milestones, gamma=0.3):
+    return lr0 * gamma ** sum(it >= int(m * steps) for m in milestones)
 
 
 def _psnr_host(pred, tgt, rng):
@@ -502,91 +516,112 @@ def aligned_psnr(pred, tgt, nv, view, dev=None):
     return fn(corr.float(), tgt[:, None], rng), fn(pred[:, None], tgt[:, None], rng), float(gamma[0]), float(scale[0])
 
 
-def psnr_long(rd, dev, steps=None, modes=("f32", "bf16", "f32_reseeded"), n_events=None):
-    """BASELINE's "PSNR vs ref" at convergence (PSNR_LEG): the HIP TrainStep in F32 (the reference's
-    arithmetic, pinned to the reference at 1e-4 by tests/) and in BF16 (the benchmark's mode) train
-    from ONE init on a teacher scene for `steps` Adam steps, each on a fresh batch of configs[0]'s
-    shape (512 events = 2048 rays x 64 samples, drawn on a seeded CPU generator) whose measured
-    log-intensity changes are the teacher's; the learning rate is cut x0.3 at the milestones (the
-    reference's multi_step_lr); four held-out views are aligned to the teacher's by the reference's
-    affine log-intensity correction (deblur_e_nerf.py:705-833) and scored with its PSNR
-    (metric.py:68-72).  The reference side: tests/golden/psnr_oracle_converged.npz, the ORACLE
-    trained the same way on the same batch sequence in the build container
-    (tests/golden/make_psnr_oracle.py); delta_db = HIP - oracle, and the HIP views are scored
-    against the oracle's own renders as well."""
+def oracle_fixture_path(seq):
+    return os.path.join(ROOT, "tests", "golden", f"psnr_oracle_s{seq}.npz")
+
+
+def _load_oracle_fixture(seq, leg, rd):
+    """tests/golden/psnr_oracle_s<seq>.npz when it was trained on exactly this leg, else None."""
     import numpy as np
+    path = oracle_fixture_path(seq)
+    if not os.path.exists(path):
+        return None
+    fx = np.load(path)
+    if str(fx["leg"]) != json.dumps(leg, sort_keys=True) or int(fx["rd"]) != rd:
+        return None
+    return fx
+
+
+def _stats(xs):
+    if not xs:
+        return None
+    m = sum(xs) / len(xs)
+    sd = math.sqrt(sum((x - m) ** 2 for x in xs) / (len(xs) - 1)) if len(xs) > 1 else float("nan")
+    return {"n": len(xs), "mean": round(m, 4), "std": round(sd, 4), "sem": round(sd / math.sqrt(len(xs)), 4)}
+
+
+def psnr_long(rd, dev, steps=None, modes=("f32", "bf16"), sequences=(0, 1, 2), leg=None):
+    """BASELINE's "PSNR vs ref" at convergence (PSNR_LEG): for each batch sequence k, the HIP
+    TrainStep in F32 (the reference's arithmetic, pinned to the reference at 1e-4 per step by tests/)
+    and in BF16 (the benchmark's mode) train from ONE init on a teacher scene for `steps` Adam steps,
+    each on a fresh batch of events (drawn on a CPU generator seeded batch_seed + k) whose measured
+    log-intensity changes are the teacher's; the learning rate is cut at the milestones (the
+    reference's multi_step_lr); the held-out views are aligned to the teacher's by the reference's
+    affine log-intensity correction (deblur_e_nerf.py:705-833) and scored with its PSNR
+    (metric.py:68-72).  The reference side: tests/golden/psnr_oracle_s<k>.npz, the ORACLE trained the
+    same way on the same batch sequence in the build container (tests/golden/make_psnr_oracle.py).
+    Reported per sequence and as mean / std / standard error over the sequences: each mode's PSNR,
+    each mode - the oracle (paired, same sequence) and BF16 - F32."""
     from deblur_e_nerf import _native as nat
     from deblur_e_nerf.loss_metric.metric import psnr
     from deblur_e_nerf.train import TrainStep
-    L = PSNR_LEG
-    steps = steps or L["steps"]
-    n_events = n_events or L["n_events"]
-    n_samples, view, milestones = L["n_samples"], L["view"], L["milestones"]
-    tflat = teacher_field(rd).to(dev).contiguous()
+    L = dict(leg or PSNR_LEG)
+    if steps:
+        L["steps"] = steps
+    steps, n_events, n_samples, view = L["steps"], L["n_events"], L["n_samples"], L["view"]
+    tflat = teacher_field(rd, L).to(dev).contiguous()
     tcfg = dict(mode=nat.mode_id("f32"), rd=rd, aabb=[-1.5, -1.5, -1.5, 1.5, 1.5, 1.5], near=1.43, far=6.63)
     tpacked = nat.PackedWeights("f32", rd, dev)
     tpacked.pack(tflat)
     ones = torch.ones(rd, device=dev)
-    vo, vd, nv = psnr_views(view)
+    vo, vd, nv = psnr_views(view, L["n_views"])
     vo, vd = vo.to(dev), vd.to(dev)
     vu = torch.full((vo.shape[0],), 0.5, device=dev)
     with torch.no_grad():
         target, _, _ = nat.render(vo, vd, vu, ones, tflat, tcfg, tpacked, n_samples)
-    fx_path = os.path.join(ROOT, "tests", "golden", "psnr_oracle_converged.npz")
-    fx = np.load(fx_path) if os.path.exists(fx_path) else None
-    if fx is not None and (int(fx["steps"]) != steps or n_events != L["n_events"]):
-        fx = None
-    out = {}
-    for name in modes:
-        # "f32_reseeded": F32 again on another batch sequence -- the spread of the run itself, the
-        # scale against which the BF16 and oracle differences are read (the leg is not at convergence)
-        # ("<mode>_s<k>": batch sequence k, the seed study of profiles/psnr_seeds.py)
-        mode, _, tag = name.partition("_")
-        shift = 1 if tag == "reseeded" else int(tag[1:]) if tag.startswith("s") else 0
-        ts = TrainStep(n_events, n_samples=n_samples, radiance_dim=rd, mode=mode, device=dev,
-                       seed=L["student_seed"])
-        gen = torch.Generator().manual_seed(L["batch_seed"] + shift)
-        t0 = time.perf_counter()
-        lr0 = ts.lr
-        for it in range(steps):
-            ts.lr = lr_at(lr0, it, steps, milestones)
-            b = _teacher_batch(gen, n_events, dev)
+    rows = []
+    for seq in sequences:
+        fx = _load_oracle_fixture(seq, L, rd)
+        row = {"seq": seq}
+        for mode in modes:
+            ts = TrainStep(n_events, n_samples=n_samples, radiance_dim=rd, mode=mode, device=dev,
+                           seed=L["student_seed"], lr=L["lr0"])
+            gen = torch.Generator().manual_seed(L["batch_seed"] + seq)
+            t0 = time.perf_counter()
+            for it in range(steps):
+                ts.lr = lr_at(L["lr0"], it, steps, L["milestones"], L["lr_gamma"])
+                b = _teacher_batch(gen, n_events, dev)
+                with torch.no_grad():
+                    col, _, _ = nat.render(b["rays_o"], b["rays_d"], b["jitter"], ones, tflat, tcfg, tpacked,
+                                           n_samples)
+                y = torch.log(col[:, 0] + 1e-3).view(4, n_events)
+                ts.load_batch(lid=(y[1] - y[0]).float().contiguous(), **b)
+                ts.step()
+            torch.cuda.synchronize()
+            train_s = time.perf_counter() - t0
             with torch.no_grad():
-                col, _, _ = nat.render(b["rays_o"], b["rays_d"], b["jitter"], ones, tflat, tcfg, tpacked, n_samples)
-            y = torch.log(col[:, 0] + 1e-3).view(4, n_events)
-            ts.load_batch(lid=(y[1] - y[0]).float().contiguous(), **b)
-            ts.step()
-        torch.cuda.synchronize()
-        train_s = time.perf_counter() - t0
-        with torch.no_grad():
-            hv, _, _ = nat.render(vo, vd, vu, torch.nn.functional.softplus(ts.bkgd_orig.detach()), ts.flat.detach(),
-                                  dict(ts.cfg), ts.packed, n_samples)
-        ps, ps_raw, gamma, scale = aligned_psnr(hv, target, nv, view, dev)
-        e = {"psnr_db": round(ps, 3), "psnr_uncorrected_db": round(ps_raw, 3), "gamma": round(gamma, 4),
-             "scale": round(scale, 4), "train_s": round(train_s, 2),
-             "final_loss": [round(x, 6) for x in ts.loss[:3].tolist()]}
+                hv, _, _ = nat.render(vo, vd, vu, torch.nn.functional.softplus(ts.bkgd_orig.detach()),
+                                      ts.flat.detach(), dict(ts.cfg), ts.packed, n_samples)
+            ps, ps_raw, gamma, scale = aligned_psnr(hv, target, nv, view, dev)
+            e = {"psnr_db": round(ps, 4), "psnr_uncorrected_db": round(ps_raw, 3), "gamma": round(gamma, 4),
+                 "train_s": round(train_s, 2), "final_loss": [round(x, 6) for x in ts.loss[:3].tolist()]}
+            if fx is not None:
+                orc = torch.from_numpy(fx["pred"]).reshape(-1, 1).to(dev)
+                e["minus_oracle_db"] = round(ps - float(fx["psnr_db"]), 4)
+                # the HIP-trained views against the oracle-trained ones (range of the oracle's render)
+                e["psnr_vs_oracle_render_db"] = round(psnr(hv[:, 0].reshape(nv, 1, view, view),
+                                                           orc.reshape(nv, 1, view, view), float(orc.max())), 2)
+            row[mode] = e
+            del ts
+            torch.cuda.empty_cache()
         if fx is not None:
-            orc = torch.from_numpy(fx["pred"]).reshape(-1, 1).to(dev)
-            e["delta_vs_oracle_db"] = round(ps - float(fx["psnr_db"]), 4)
-            # the HIP-trained views against the oracle-trained ones (range of the oracle's render)
-            e["psnr_vs_oracle_render_db"] = round(psnr(hv[:, 0].reshape(nv, 1, view, view),
-                                                       orc.reshape(nv, 1, view, view), float(orc.max())), 2)
-        out[name] = e
-        del ts
-        torch.cuda.empty_cache()
-    if "f32" in out and "f32_reseeded" in out:
-        out["run_spread_db"] = round(out["f32_reseeded"]["psnr_db"] - out["f32"]["psnr_db"], 4)
-    if fx is not None:
-        out["oracle"] = {"psnr_db": round(float(fx["psnr_db"]), 3),
-                         "psnr_uncorrected_db": round(float(fx["psnr_uncorrected_db"]), 3),
-                         "source": "tests/golden/psnr_oracle_converged.npz (make_psnr_oracle.py, build container CPU)"}
-    if "f32" in out and "bf16" in out:
-        out["delta_db"] = round(out["bf16"]["psnr_db"] - out["f32"]["psnr_db"], 4)
-    return dict(out, steps=steps, setup=f"teacher scene, {steps} Adam steps from one init (lr x0.3 at "
-                                        f"{list(milestones)} of the run), each on a fresh batch of {n_events} events = "
-                                        f"{4 * n_events} rays x {n_samples} samples; {nv} held-out {view}x{view} views, "
-                                        f"affine log-intensity correction, mean PSNR vs the teacher; delta_vs_oracle_db "
-                                        f"= HIP - the oracle trained identically")
+            row["oracle"] = {"psnr_db": round(float(fx["psnr_db"]), 4), "threads": int(fx["threads"])}
+        if "f32" in row and "bf16" in row:
+            row["bf16_minus_f32_db"] = round(row["bf16"]["psnr_db"] - row["f32"]["psnr_db"], 4)
+        rows.append(row)
+        print(json.dumps({"psnr_seq": row}), file=sys.stderr, flush=True)
+    summary = {m: _stats([r[m]["psnr_db"] for r in rows if m in r]) for m in modes}
+    summary["oracle"] = _stats([r["oracle"]["psnr_db"] for r in rows if "oracle" in r])
+    for m in modes:
+        summary[f"{m}_minus_oracle"] = _stats([r[m]["minus_oracle_db"] for r in rows
+                                               if "minus_oracle_db" in r.get(m, {})])
+    summary["bf16_minus_f32"] = _stats([r["bf16_minus_f32_db"] for r in rows if "bf16_minus_f32_db" in r])
+    return dict(rows=rows, summary=summary, leg=L,
+                setup=f"teacher scene, {steps} Adam steps from one init (lr {L['lr0']} x{L['lr_gamma']} at "
+                      f"{list(L['milestones'])} of the run), each on a fresh batch of {n_events} events = "
+                      f"{4 * n_events} rays x {n_samples} samples; {nv} held-out {view}x{view} views, affine "
+                      f"log-intensity correction, mean PSNR vs the teacher; per batch sequence, HIP F32 / BF16 "
+                      f"and the oracle trained identically (tests/golden/psnr_oracle_s<k>.npz)")
 
 
 def cpu_baseline_pixbw(n_rays, n_samples, rd, S, threads):

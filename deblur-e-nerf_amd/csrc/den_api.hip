@@ -24,6 +24,7 @@
 #include "den_render.hip"
 #include "den_raygrad.hip"
 #include "den_sh.hip"
+#include "den_dataset.hip"
 
 using namespace den;
 
@@ -1599,6 +1600,172 @@ int den_sh_encode_bwd(int64_t n, int32_t degree, const float* coords, const floa
   if (n < 0 || (n > 0 && (!coords || !d_out || !d_coords))) return fail(DEN_EINVAL, "bad arguments");
   if (n == 0) return DEN_OK;
   sh_dispatch(degree, true, n, coords, d_out, d_coords, (hipStream_t)stream);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+}  // extern "C"
+
+// ---- raw-event preprocessing (den_dataset.hip)
+namespace {
+struct QueueWs {
+  size_t keys[2], vals[2], counts, totals, scal, valid, start, offsets, scan, total;
+  int64_t n_tiles;
+};
+QueueWs queue_ws(int64_t n) {
+  QueueWs W{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off += align256(bytes); return o; };
+  W.n_tiles = (n + QS_TILE - 1) / QS_TILE;
+  for (int b = 0; b < 2; ++b) W.keys[b] = take((size_t)n * 4);
+  for (int b = 0; b < 2; ++b) W.vals[b] = take((size_t)n * 4);
+  W.counts = take((size_t)QS_RADIX * W.n_tiles * 4);
+  W.totals = take(QS_RADIX * 4);
+  W.scal = take(64);  // status i32 | min interval (biased u64) | interval count u64
+  W.valid = take((size_t)n * 4);
+  W.start = take((size_t)n * 8);
+  W.offsets = take((size_t)(n + 1) * 8);
+  W.scan = take(den_scan_workspace_bytes(n));
+  W.total = off;
+  return W;
+}
+__global__ void queue_init_kernel(int32_t* status, unsigned long long* min_biased, unsigned long long* n_int) {
+  *status = 0;
+  *min_biased = ~0ull;  // INT64_MAX biased
+  *n_int = 0;
+}
+__global__ void queue_empty_kernel(int64_t* stats) {
+  stats[0] = 0;
+  stats[1] = INT64_MAX;
+  stats[2] = 0;
+}
+
+// shared body of den_queue_raw_events / den_max_refractory_period (out_position == null: stats only)
+int queue_impl(int64_t n, int32_t H, int32_t W_, const int64_t* position, const int64_t* ts, const uint8_t* polarity,
+               void* workspace, size_t ws_bytes, int64_t* out_position, int64_t* out_start, int64_t* out_end,
+               int64_t* out_pos, int64_t* out_neg, int64_t* stats, hipStream_t st) {
+  if (n < 0 || H <= 0 || W_ <= 0 || !stats || (n > 0 && (!position || !ts || !workspace)))
+    return fail(DEN_EINVAL, "bad arguments");
+  if (out_position && (!polarity || !out_start || !out_end || !out_pos || !out_neg))
+    return fail(DEN_EINVAL, "bad arguments: queued-event outputs");
+  if (n > (int64_t)UINT32_MAX - 1 || (int64_t)H * W_ > (int64_t)UINT32_MAX)
+    return fail(DEN_EUNSUPPORTED, "more than 2^32 - 1 events or pixels");
+  if (n == 0) {
+    hipLaunchKernelGGL(queue_empty_kernel, dim3(1), dim3(1), 0, st, stats);
+    DEN_LAUNCHED();
+    return DEN_OK;
+  }
+  const QueueWs L = queue_ws(n);
+  if (ws_bytes < L.total) return fail(DEN_EINVAL, "workspace too small (den_queue_workspace_bytes)");
+  char* ws = (char*)workspace;
+  uint32_t* keys[2] = {(uint32_t*)(ws + L.keys[0]), (uint32_t*)(ws + L.keys[1])};
+  uint32_t* vals[2] = {(uint32_t*)(ws + L.vals[0]), (uint32_t*)(ws + L.vals[1])};
+  uint32_t* counts = (uint32_t*)(ws + L.counts);
+  uint32_t* totals = (uint32_t*)(ws + L.totals);
+  int32_t* status = (int32_t*)(ws + L.scal);
+  unsigned long long* min_biased = (unsigned long long*)(ws + L.scal + 8);
+  unsigned long long* n_int = (unsigned long long*)(ws + L.scal + 16);
+  int32_t* valid = (int32_t*)(ws + L.valid);
+  int64_t* start = (int64_t*)(ws + L.start);
+  int64_t* offsets = (int64_t*)(ws + L.offsets);
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(queue_init_kernel, dim3(1), dim3(1), 0, st, status, min_biased, n_int);
+  hipLaunchKernelGGL(queue_keys_kernel, dim3(blocks), dim3(256), 0, st, n, H, W_, position, keys[0], vals[0], status);
+  DEN_LAUNCHED();
+  // pixel keys need ceil(log2(H * W)) bits: 8-bit digits, LSD, stable
+  int bits = 0;
+  while (bits < 32 && (((int64_t)1) << bits) < (int64_t)H * W_) ++bits;
+  int cur = 0;
+  for (int shift = 0; shift < bits; shift += 8) {
+    hipLaunchKernelGGL(radix_hist_kernel, dim3((unsigned)L.n_tiles), dim3(QS_THREADS), 0, st, n, shift, keys[cur],
+                       counts, L.n_tiles);
+    hipLaunchKernelGGL(radix_scan_kernel, dim3(QS_RADIX), dim3(QS_THREADS), 0, st, L.n_tiles, counts, totals);
+    hipLaunchKernelGGL(radix_scatter_kernel, dim3((unsigned)L.n_tiles), dim3(QS_THREADS), 0, st, n, shift, keys[cur],
+                       vals[cur], counts, totals, L.n_tiles, keys[cur ^ 1], vals[cur ^ 1]);
+    DEN_LAUNCHED();
+    cur ^= 1;
+  }
+  hipLaunchKernelGGL(queue_mark_kernel, dim3(blocks), dim3(256), 0, st, n, keys[cur], vals[cur], ts, valid, start,
+                     min_biased, n_int);
+  DEN_LAUNCHED();
+  if (out_position) {
+    int rc = den_exclusive_scan(n, valid, offsets, ws + L.scan, st);
+    if (rc != DEN_OK) return rc;
+  }
+  QueueEmitArgs E{};
+  E.n = n;
+  E.position = position;
+  E.ts = ts;
+  E.polarity = polarity;
+  E.valid = valid;
+  E.offsets = offsets;
+  E.start_tmp = start;
+  E.out_position = out_position;
+  E.out_start_ts = out_start;
+  E.out_end_ts = out_end;
+  E.out_num_pos = out_pos;
+  E.out_num_neg = out_neg;
+  E.status = status;
+  E.min_biased = min_biased;
+  E.n_intervals = n_int;
+  E.out_count = stats;
+  E.out_min_interval = stats + 1;
+  E.out_n_intervals = stats + 2;
+  if (!out_position) E.offsets = nullptr;
+  hipLaunchKernelGGL(queue_emit_kernel, dim3(out_position ? blocks : 1), dim3(256), 0, st, E);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+}  // namespace
+
+extern "C" {
+
+size_t den_queue_workspace_bytes(int64_t n) { return n <= 0 ? 256 : queue_ws(n).total; }
+
+int den_queue_raw_events(int64_t n, int32_t img_height, int32_t img_width, const int64_t* position,
+                         const int64_t* timestamp, const uint8_t* polarity, void* workspace, size_t workspace_bytes,
+                         int64_t* out_position, int64_t* out_start_ts, int64_t* out_end_ts, int64_t* out_num_pos,
+                         int64_t* out_num_neg, int64_t* out_stats, void* stream) {
+  if (!out_position) return fail(DEN_EINVAL, "bad arguments: out_position");
+  return queue_impl(n, img_height, img_width, position, timestamp, polarity, workspace, workspace_bytes, out_position,
+                    out_start_ts, out_end_ts, out_num_pos, out_num_neg, out_stats, (hipStream_t)stream);
+}
+
+int den_colorize_events(int64_t n, const int64_t* position, const int32_t* bayer_channel, uint8_t* out_channel_idx,
+                        void* stream) {
+  if (n < 0 || !bayer_channel || (n > 0 && (!position || !out_channel_idx))) return fail(DEN_EINVAL, "bad arguments");
+  Bayer B{};
+  for (int q = 0; q < 4; ++q) {
+    if (bayer_channel[q] < 0 || bayer_channel[q] > 2) return fail(DEN_EINVAL, "bayer channel indices must be 0..2");
+    B.ch[q] = bayer_channel[q];
+  }
+  if (n == 0) return DEN_OK;
+  hipLaunchKernelGGL(colorize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
+                     position, B, out_channel_idx);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_max_refractory_period(int64_t n, int32_t img_height, int32_t img_width, const int64_t* position,
+                              const int64_t* timestamp, void* workspace, size_t workspace_bytes, int64_t* out_stats,
+                              void* stream) {
+  return queue_impl(n, img_height, img_width, position, timestamp, nullptr, workspace, workspace_bytes, nullptr,
+                    nullptr, nullptr, nullptr, nullptr, out_stats, (hipStream_t)stream);
+}
+
+int den_undistort_events(int64_t n, int32_t model, const int64_t* position, const float* intrinsics,
+                         const float* distortion, float* out, void* stream) {
+  if (n < 0 || model < 0 || model > 2 || (n > 0 && (!position || !out)) || (model > 0 && (!intrinsics || !distortion)))
+    return fail(DEN_EINVAL, "bad arguments");
+  if (n == 0) return DEN_OK;
+  UndistortArgs A{};
+  A.n = n;
+  A.model = model;
+  for (int q = 0; q < 9; ++q) A.K[q] = intrinsics ? (double)intrinsics[q] : 0.0;
+  for (int q = 0; q < 4; ++q) A.D[q] = distortion ? (double)distortion[q] : 0.0;
+  A.position = position;
+  A.out = out;
+  hipLaunchKernelGGL(undistort_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
   DEN_LAUNCHED();
   return DEN_OK;
 }

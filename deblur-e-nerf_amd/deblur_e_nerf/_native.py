@@ -142,10 +142,18 @@ _SIGS = {
                        + [ctypes.c_void_p] * 4),
     "den_occ_update": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_float] * 3
                        + [ctypes.c_int64] + [ctypes.c_void_p] * 5),
+    # dataset preprocessing, den_dataset.hip
+    "den_queue_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "den_queue_raw_events": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 4
+                             + [ctypes.c_size_t] + [ctypes.c_void_p] * 7),
+    "den_colorize_events": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_void_p] * 4),
+    "den_max_refractory_period": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
+                                  + [ctypes.c_void_p] * 3 + [ctypes.c_size_t] + [ctypes.c_void_p] * 2),
+    "den_undistort_events": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 5),
 }
 
 
-ABI_VERSION = 4  # include/den_api.h DEN_VERSION
+ABI_VERSION = 5  # include/den_api.h DEN_VERSION
 
 
 def lib():
@@ -518,7 +526,8 @@ class HashGridFunction(torch.autograd.Function):
     def backward(ctx, g):
         desc, x, shape = ctx.keep
         d_table = torch.zeros(shape, dtype=torch.float32, device=x.device)
-        _check(lib().den_hashgrid_bwd(ctypes.byref(desc), x.shape[0], _ptr(x), _ptr(g.contiguous()), _ptr(d_table),
+        g = g.contiguous()  # bound: a temporary's block could be reused before the kernel runs
+        _check(lib().den_hashgrid_bwd(ctypes.byref(desc), x.shape[0], _ptr(x), _ptr(g), _ptr(d_table),
                                       _stream(x.device)))
         return d_table, None, None
 
@@ -545,8 +554,9 @@ class SHEncodeFunction(torch.autograd.Function):
     def backward(ctx, g):
         (coords,) = ctx.saved_tensors
         d = torch.empty_like(coords)
-        _check(lib().den_sh_encode_bwd(coords.shape[0], ctx.degree, _ptr(coords), _ptr(g.float().contiguous()),
-                                       _ptr(d), _stream(coords.device)))
+        g = g.float().contiguous()
+        _check(lib().den_sh_encode_bwd(coords.shape[0], ctx.degree, _ptr(coords), _ptr(g), _ptr(d),
+                                       _stream(coords.device)))
         return d, None
 
 
@@ -602,9 +612,11 @@ def event_target(ts_diff, lid, end_ts, start_ts, c):
     _require_device(ts_diff, lid, end_ts, start_ts, c)
     N = lid.numel()
     out = torch.empty(N, dtype=torch.float32, device=lid.device)
-    _check(lib().den_event_target(N, _ptr(ts_diff.double().contiguous()), _ptr(lid.float().contiguous()),
-                                  _ptr(end_ts.long().contiguous()), _ptr(start_ts.double().contiguous()),
-                                  _ptr(c.float().reshape(1).contiguous()), _ptr(out), _stream(lid.device)))
+    # every converted input stays bound until the launch: a freed temporary's block could be
+    # handed to the next conversion (and overwritten) before the kernel reads it
+    args = (ts_diff.double().contiguous(), lid.float().contiguous(), end_ts.long().contiguous(),
+            start_ts.double().contiguous(), c.float().reshape(1).contiguous())
+    _check(lib().den_event_target(N, *(_ptr(t) for t in args), _ptr(out), _stream(lid.device)))
     return out
 
 
@@ -635,8 +647,8 @@ class SampleTsFunction(torch.autograd.Function):
     def backward(ctx, g_ts):
         S, N, batch, dt = ctx.meta
         d = torch.empty(N, dtype=torch.float64, device=g_ts.device)
-        _check(lib().den_pixbw_sample_ts_bwd(S, N, _ptr(g_ts.to(torch.float64).reshape(S, N).contiguous()), _ptr(d),
-                                             _stream(g_ts.device)))
+        g = g_ts.to(torch.float64).reshape(S, N).contiguous()
+        _check(lib().den_pixbw_sample_ts_bwd(S, N, _ptr(g), _ptr(d), _stream(g_ts.device)))
         return None, d.reshape(batch).to(dt), None, None
 
 
@@ -947,4 +959,89 @@ def image_error(pred, target):
     ws = torch.empty(lib().den_image_error_workspace_bytes(B) // 8, dtype=torch.float64, device=p.device)
     out = torch.empty(B, 2, dtype=torch.float64, device=p.device)
     _check(lib().den_image_error(B, p.shape[1], _ptr(p), _ptr(t), _ptr(ws), _ptr(out), _stream(p.device)))
+    return out
+
+
+# ---------------------------------------------------------------- dataset preprocessing
+INT64_MAX = (1 << 63) - 1
+UNDISTORT_MODELS = {None: 0, "": 0, "plumb_bob": 1, "equidistant": 2}
+
+
+def _queue_inputs(position, timestamp, img_height, img_width):
+    _require_device(position, timestamp)
+    if position.dtype != torch.int64 or position.dim() != 2 or position.shape[1] != 2:
+        raise DenError("position must be (n, 2) int64 (datasets.py:207: raw uint16 positions cast to np.int64)")
+    if timestamp.dtype != torch.int64 or timestamp.shape != (position.shape[0],):
+        raise DenError("timestamp must be (n) int64 ns")
+    n = position.shape[0]
+    ws = torch.empty(lib().den_queue_workspace_bytes(n), dtype=torch.uint8, device=position.device)
+    return n, int(img_height), int(img_width), ws, position.contiguous(), timestamp.contiguous()
+
+
+def _stats(stats, img_height, img_width):
+    count, min_iv, n_iv = (int(x) for x in stats.tolist())  # one device -> host read
+    if count < 0:
+        raise IndexError(f"an event position lies outside the {img_height} x {img_width} image")
+    return count, (None if n_iv == 0 else min_iv), n_iv
+
+
+def queue_raw_events(position, timestamp, polarity, img_height, img_width):
+    """Event.queue_raw_events on the device (den_queue_raw_events): raw position (n,2) i64,
+    timestamp (n) i64, polarity (n) bool -> (dict of the queued events' position, start_ts,
+    end_ts, num_pos, num_neg device tensors, in input order; the maximum refractory period = the
+    minimum queued interval, None when there is no interval)."""
+    n, H, W, ws, position, timestamp = _queue_inputs(position, timestamp, img_height, img_width)
+    _require_device(polarity)
+    if polarity.shape != (n,):
+        raise DenError("polarity must be (n)")
+    pol = polarity.to(torch.uint8).contiguous()
+    dev = position.device
+    out = {"position": torch.empty(n, 2, dtype=torch.int64, device=dev)}
+    for k in ("start_ts", "end_ts", "num_pos", "num_neg"):
+        out[k] = torch.empty(n, dtype=torch.int64, device=dev)
+    stats = torch.empty(3, dtype=torch.int64, device=dev)
+    _check(lib().den_queue_raw_events(n, H, W, _ptr(position), _ptr(timestamp), _ptr(pol), _ptr(ws), ws.numel(),
+                                      _ptr(out["position"]), _ptr(out["start_ts"]), _ptr(out["end_ts"]),
+                                      _ptr(out["num_pos"]), _ptr(out["num_neg"]), _ptr(stats), _stream(dev)))
+    count, min_iv, _ = _stats(stats, H, W)
+    return {k: v[:count] for k, v in out.items()}, min_iv
+
+
+def colorize_events(position, bayer_channel):
+    """Event.colorize_events' index map on the device (den_colorize_events): (n,2) i64 positions,
+    4 channel indices (top-left, top-right, bottom-left, bottom-right) -> (n) u8."""
+    _require_device(position)
+    position = position.contiguous()
+    out = torch.empty(position.shape[0], dtype=torch.uint8, device=position.device)
+    bayer = (ctypes.c_int32 * 4)(*[int(c) for c in bayer_channel])
+    _check(lib().den_colorize_events(position.shape[0], _ptr(position), bayer, _ptr(out), _stream(position.device)))
+    return out
+
+
+def max_refractory_period(position, timestamp, img_height, img_width):
+    """Event.extract_max_refractory_period on the device (den_max_refractory_period): the minimum
+    interval between consecutive distinct timestamps at a pixel, as an int (ns), or None when no
+    pixel has two (the reference's inf)."""
+    n, H, W, ws, position, timestamp = _queue_inputs(position, timestamp, img_height, img_width)
+    stats = torch.empty(3, dtype=torch.int64, device=position.device)
+    _check(lib().den_max_refractory_period(n, H, W, _ptr(position), _ptr(timestamp),
+                                           _ptr(ws), ws.numel(), _ptr(stats), _stream(position.device)))
+    return _stats(stats, H, W)[1]
+
+
+def undistort_events(position, distortion_model, intrinsics, distortion_params):
+    """Event.undistort_events' arithmetic (den_undistort_events): (n,2) i64 positions -> (n,2) f32."""
+    _require_device(position)
+    n = position.shape[0]
+    params = [float(x) for x in distortion_params]
+    model = 0 if len(params) == 0 else UNDISTORT_MODELS.get(str(distortion_model))
+    if model is None:
+        raise NotImplementedError(f"distortion model {distortion_model!r}")  # datasets.py:360-363 (fov and others)
+    if model and len(params) != 4:
+        raise DenError("distortion_params must hold 4 values")
+    K = (ctypes.c_float * 9)(*[float(x) for x in torch.as_tensor(intrinsics).reshape(-1).tolist()])
+    D = (ctypes.c_float * 4)(*(params or [0.0] * 4))
+    position = position.contiguous()
+    out = torch.empty(n, 2, dtype=torch.float32, device=position.device)
+    _check(lib().den_undistort_events(n, model, _ptr(position), K, D, _ptr(out), _stream(position.device)))
     return out

@@ -12,6 +12,7 @@ background).  Forward only: the configurations in BASELINE.json freeze these
 parameters for the synthetic path (configs/train/synthetic.yaml:29-40).
 """
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -88,21 +89,31 @@ class ContrastThreshold(torch.nn.Module):
 
 
 class RefractoryPeriod(torch.nn.Module):
-    """event_generation_params.py:121-237.  ``max_refractory_period`` is given
-    (the reference extracts and caches it from the raw events)."""
+    """event_generation_params.py:121-237.  ``max_refractory_period`` is the cached
+    ``max_refractory_period.pt``, else extracted from ``raw_events.npz`` on the GPU
+    (datasets.Event.extract_max_refractory_period, den_max_refractory_period) and cached, as the
+    reference does (:135-149); it may also be given directly."""
+    REFRACTORY_PERIOD_KEY = "refractory_period"
     REDEFINED_CALIBRATED_REFRACTORY_PERIOD_FACTOR = 0.999
     MIN_SCALED_SHIFTED_SIGMOID_GRAD_MAGNITUDE = 0.0001
 
     def __init__(self, dataset_directory=None, max_refractory_period=None, calibration=None):
         super().__init__()
         cal = _load_calibration(dataset_directory, calibration)
-        tau = torch.as_tensor(np.asarray(cal["refractory_period"]))
+        tau = torch.as_tensor(np.asarray(cal[self.REFRACTORY_PERIOD_KEY]))
         if max_refractory_period is None:
-            path = os.path.join(dataset_directory, "max_refractory_period.pt")
-            max_refractory_period = torch.load(path, weights_only=True)
+            from ..data import datasets
+            max_refractory_period = datasets.Event.load_max_refractory_period(dataset_directory)
+            if max_refractory_period is None:
+                raw_events = datasets.Event.load_raw_events(dataset_directory)
+                max_refractory_period = datasets.Event.extract_max_refractory_period(raw_events, cal)
+                datasets.Event.save_max_refractory_period(max_refractory_period, dataset_directory)
         mx = torch.as_tensor(max_refractory_period)
         if not (0 <= tau < mx):
+            warnings.warn(f"Calibrated refractory period ({tau}) >= Max. possible refractory period ({mx}).")
             tau = self.REDEFINED_CALIBRATED_REFRACTORY_PERIOD_FACTOR * mx
+            warnings.warn(f"Redefining calibrated refractory period to {self.REDEFINED_CALIBRATED_REFRACTORY_PERIOD_FACTOR}"
+                          f" of max. possible refractory period ({tau}).")
         self.register_buffer("init_refractory_period", tau, persistent=False)
         self.register_buffer("max_refractory_period", mx, persistent=False)
         self.register_buffer("max_scaled_logit_magnitude",

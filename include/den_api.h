@@ -52,6 +52,9 @@
  *   den_ngp_* / den_hashgrid_*
  *                    <- deblur_e_nerf/external/ngp.py:109-280 NGPradianceField (tcnn.Encoding
  *                       HashGrid + MLP + SHEncoder) forward / backward
+ *   den_queue_raw_events / den_max_refractory_period / den_colorize_events / den_undistort_events
+ *                    <- deblur_e_nerf/data/datasets.py:133-187, 190-328, 331-364 (Event's
+ *                       raw_events.npz -> events.pt / max_refractory_period.pt build path)
  */
 #ifndef DEN_API_H
 #define DEN_API_H
@@ -63,7 +66,9 @@
 extern "C" {
 #endif
 
-#define DEN_VERSION 4  /* 4: density_activation in den_render_desc / den_ngp_desc; den_sh_encode_* */
+#define DEN_VERSION 5  /* 5: den_queue_raw_events / den_max_refractory_period / den_colorize_events /
+                          den_undistort_events;
+                          4: density_activation in den_render_desc / den_ngp_desc; den_sh_encode_* */
 
 enum den_status {
   DEN_OK = 0,
@@ -521,6 +526,47 @@ int den_adam_step(int64_t n, float* param, const float* grad, float* exp_avg, fl
 /* The same for f64 parameters (the refractory period, event_generation_params.py:196-201). */
 int den_adam_step_f64(int64_t n, double* param, const double* grad, double* exp_avg, double* exp_avg_sq, double lr,
                       double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream);
+
+/* ---------------------------------------------------------------- dataset preprocessing */
+/* Raw events (raw_events.npz: position (n,2) cast to i64, timestamp (n) i64 ns, polarity (n) bool
+ * as u8 0/1) -> queued events, replacing the per-event Python loops of
+ *   data/datasets.py:190-284 Event.queue_raw_events and
+ *   data/datasets.py:133-187 Event.extract_max_refractory_period
+ *   (called from models/event_generation_params.py:136-149 RefractoryPeriod.__init__).
+ * An event is queued iff an earlier raw event (input order) lies at its pixel with a different
+ * timestamp t_prev (the immediately preceding one at that pixel); it becomes [start_ts = t_prev,
+ * end_ts = t], num_pos = its polarity, num_neg = 1 - num_pos, in input order.  The maximum
+ * refractory period is the minimum of t - t_prev over the queued events (the reference's
+ * per-pixel deduplicated sliding window gives the same intervals).
+ * Outputs (device, caller-allocated with room for n events): out_position (n,2) i64, out_start_ts,
+ * out_end_ts, out_num_pos, out_num_neg (n) i64.  out_stats (device, 3 i64): [queued count M (-1 if
+ * any position lies outside the img_height x img_width image: the reference raises IndexError),
+ * minimum interval (INT64_MAX when none: the reference's inf), number of intervals].  The first M
+ * entries of each output are the queued events.  Bit-exact integer work: a stable LSD radix sort
+ * of the pixel keys (values = event indices), then neighbours. */
+size_t den_queue_workspace_bytes(int64_t n);
+int den_queue_raw_events(int64_t n, int32_t img_height, int32_t img_width, const int64_t* position,
+                         const int64_t* timestamp, const uint8_t* polarity, void* workspace, size_t workspace_bytes,
+                         int64_t* out_position, int64_t* out_start_ts, int64_t* out_end_ts, int64_t* out_num_pos,
+                         int64_t* out_num_neg, int64_t* out_stats, void* stream);
+/* data/datasets.py:287-328 Event.colorize_events: out_channel_idx (n) u8 = bayer_channel[(x odd) +
+ * 2 (y odd)] for positions (n,2) i64; bayer_channel is a HOST pointer to the 4 channel indices
+ * (0..2) of the pattern's letters (R 0, G 1, B 2) in top-left, top-right, bottom-left,
+ * bottom-right order.  (A monochrome camera, pattern "", has no channel: the caller skips it.) */
+int den_colorize_events(int64_t n, const int64_t* position, const int32_t* bayer_channel, uint8_t* out_channel_idx,
+                        void* stream);
+/* Only out_stats of den_queue_raw_events (Event.extract_max_refractory_period); the same workspace. */
+int den_max_refractory_period(int64_t n, int32_t img_height, int32_t img_width, const int64_t* position,
+                              const int64_t* timestamp, void* workspace, size_t workspace_bytes, int64_t* out_stats,
+                              void* stream);
+/* data/datasets.py:331-364 Event.undistort_events: positions (n,2) i64 cast to f32 (the default
+ * dtype), then model 0 = none (the cast only), 1 = plumb_bob (cv2.undistortPoints, k1 k2 p1 p2,
+ * 5 fixed-point iterations), 2 = equidistant (cv2.fisheye.undistortPoints, k1..k4, Newton on
+ * theta, 10 iterations / 1e-8; unconverged or flipped points -> -1e6), re-projected with
+ * P = intrinsics; double arithmetic, f32 out (n,2).  intrinsics (row-major 3x3 f32) and distortion
+ * (4 f32) are HOST pointers.  OpenCV is absent from this image: parity unpinned. */
+int den_undistort_events(int64_t n, int32_t model, const int64_t* position, const float* intrinsics,
+                         const float* distortion, float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -18,8 +18,9 @@ modules the reference imports get stand-ins:
   the trajectory fixture);
 * ``pytorch_lightning``: ``LightningModule`` = ``torch.nn.Module`` (the
   DeblurENeRF fixture binds the reference's methods to a plain module);
-* ``cv2``, ``pypose``, ``tqdm``, ``tinycudann``, ``lpips``, ``torchmetrics``:
-  import-only (never called on these paths).
+* ``cv2``, ``pypose``, ``tinycudann``, ``lpips``, ``torchmetrics``: import-only (never called on
+  these paths); ``tqdm`` is the real package when importable (the dataset queueing fixture runs
+  datasets.py's loops, which call it), else import-only too.
 """
 import importlib
 import os
@@ -65,6 +66,10 @@ def install():
     ed = types.ModuleType("easydict")
     ed.EasyDict = _EasyDict
     sys.modules["easydict"] = ed
+    try:  # the real progress bar when the image has it (datasets.py's queueing loops call tqdm.tqdm)
+        import tqdm  # noqa: F401
+    except ImportError:
+        pass
     for name in ("cv2", "pypose", "tqdm", "tinycudann", "lpips", "torchmetrics"):
         sys.modules.setdefault(name, types.ModuleType(name))
     sys.modules["roma"] = oroma.as_module()

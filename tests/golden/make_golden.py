@@ -34,6 +34,11 @@ enum/tinycudann).  What each fixture pins:
 * ``rays.npz``          -- models/nerf.py NeRF.pixel_params_to_ray (pixel + pose ->
                            ray origin / unit direction), with and without the
                            leading render-group dimension.
+* ``queue_*.npz``       -- data/datasets.py Event.queue_raw_events, colorize_events,
+                           undistort_events (no distortion: the cast) and
+                           extract_max_refractory_period, the reference's loops run on
+                           synthetic raw_events.npz directories (repeated timestamps,
+                           bursts, single-event pixels, unsorted input, hot pixels).
 """
 import json
 import os
@@ -1257,6 +1262,86 @@ def gen_step_ziggy():
              aabb=[0.2, -0.4, 0.0, 3.7, 3.7, 1.8], near=0.01, far=13.0, cone=0.004, res=32, tv=0.1, pixbw_free=True)
 
 
+# ----------------------------------------------------------------------------
+# raw-event queueing (data/datasets.py:133-187, 190-328): the reference's own per-event loops
+QUEUE_CASES = {
+    # name: (H, W, N, bayer pattern, timestamps sorted?, seed)
+    "small_rggb": (7, 9, 600, "RGGB", True, 1),
+    "unsorted_mono": (5, 6, 400, "", False, 2),
+    "davis_grbg": (260, 346, 20000, "GRBG", True, 3),
+    "hot_pixels_bggr": (2, 3, 30000, "BGGR", True, 4),
+}
+
+
+def synthetic_raw_events(H, W, N, sorted_ts, seed):
+    """raw_events.npz-shaped arrays (preprocess_esim.py:314-316, 340-345): position (N,2) uint16
+    (x, y), timestamp (N) int64 ns, polarity (N) bool.  Repeated timestamps (zero steps, and
+    bursts at one pixel within one timestamp), pixels with a single event, both polarities."""
+    g = np.random.default_rng(seed)
+    # skewed pixel popularity: some pixels hot, many cold
+    wts = g.pareto(1.2, size=H * W) + 1e-3
+    wts[g.random(H * W) < 0.3] = 0.0  # never fire
+    wts /= wts.sum()
+    pix = g.choice(H * W, size=N, p=wts)
+    steps = g.integers(0, 4, size=N) * g.integers(1, 500, size=N)  # ~1/4 zero steps
+    ts = 1_000_000 + np.cumsum(steps).astype(np.int64)
+    # bursts: an event repeated at its own pixel with its own timestamp
+    rep = g.random(N) < 0.05
+    pix[1:][rep[1:]] = pix[:-1][rep[1:]]
+    ts[1:][rep[1:]] = ts[:-1][rep[1:]]
+    if not sorted_ts:
+        ts = ts[g.permutation(N)]
+    pos = np.stack([pix % W, pix // W], axis=1).astype(np.uint16)
+    pol = g.random(N) < 0.5
+    return pos, ts, pol
+
+
+def gen_queue():
+    """queue_<case>.npz: Event.queue_raw_events -> colorize_events -> undistort_events (no
+    distortion parameters: the f32 cast only) and Event.extract_max_refractory_period, the
+    reference's classmethods run as-is on a temporary dataset directory."""
+    ds = _refload.load("data.datasets")
+    for name, (H, W, N, bayer, sorted_ts, seed) in QUEUE_CASES.items():
+        pos, ts, pol = synthetic_raw_events(H, W, N, sorted_ts, seed)
+        d = tempfile.mkdtemp(prefix="den_raw_")
+        np.savez(os.path.join(d, "raw_events.npz"), position=pos, timestamp=ts, polarity=pol)
+        cal = dict(img_height=np.array(H, dtype=np.uint16), img_width=np.array(W, dtype=np.uint16),
+                   bayer_pattern=np.array(bayer), distortion_model=np.array("plumb_bob"),
+                   distortion_params=np.zeros(0, dtype=np.float32),
+                   intrinsics=np.array([[200.0, 0, W / 2], [0, 200.0, H / 2], [0, 0, 1]], dtype=np.float32))
+        np.savez(os.path.join(d, "camera_calibration.npz"), **cal)
+        calib = np.load(os.path.join(d, "camera_calibration.npz"))
+        q = ds.Event.queue_raw_events(d, calib)
+        queued = {k: v.clone() for k, v in q.items()}
+        col = ds.Event.colorize_events(q, calib)
+        und = ds.Event.undistort_events(col, calib)
+        mx = ds.Event.extract_max_refractory_period(np.load(os.path.join(d, "raw_events.npz")), calib)
+        out = dict(raw_position=pos, raw_timestamp=ts, raw_polarity=pol, img_height=H, img_width=W,
+                   bayer_pattern=np.array(bayer), max_refractory_period=mx.numpy(),
+                   max_refractory_period_dtype=np.array(str(mx.dtype)),
+                   final_position=und.position.numpy(), final_position_dtype=np.array(str(und.position.dtype)))
+        for k, v in queued.items():
+            out["q_" + k] = v.numpy()
+        if "channel_idx" in col:
+            out["channel_idx"] = col.channel_idx.numpy()
+        save(f"queue_{name}.npz", **out)
+    # no interval anywhere: every pixel fires once, or repeats its own timestamp -> inf, nothing queued
+    H, W = 4, 4
+    pos = np.array([[0, 0], [1, 0], [1, 0], [2, 3], [3, 3], [3, 3], [3, 3]], dtype=np.uint16)
+    ts = np.array([5, 9, 9, 11, 20, 20, 20], dtype=np.int64)
+    pol = np.array([1, 0, 1, 1, 0, 0, 1], dtype=bool)
+    d = tempfile.mkdtemp(prefix="den_raw_")
+    np.savez(os.path.join(d, "raw_events.npz"), position=pos, timestamp=ts, polarity=pol)
+    np.savez(os.path.join(d, "camera_calibration.npz"), img_height=np.array(H, dtype=np.uint16),
+             img_width=np.array(W, dtype=np.uint16), bayer_pattern=np.array(""))
+    calib = np.load(os.path.join(d, "camera_calibration.npz"))
+    q = ds.Event.queue_raw_events(d, calib)
+    mx = ds.Event.extract_max_refractory_period(np.load(os.path.join(d, "raw_events.npz")), calib)
+    save("queue_no_interval.npz", raw_position=pos, raw_timestamp=ts, raw_polarity=pol, img_height=H, img_width=W,
+         q_count=np.array(len(q.position)), max_refractory_period=mx.numpy(),
+         max_refractory_period_dtype=np.array(str(mx.dtype)))
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.set_num_threads(8)
     for name in sys.argv[1:]:
@@ -1280,3 +1365,4 @@ elif __name__ == "__main__":
     gen_step(False, 1)
     gen_step(True, 1)
     gen_ngp_all()
+    gen_queue()
