@@ -113,7 +113,10 @@ WsLayout ws_layout(const den_render_desc* d) {
       continue;
     }
     L.act[a] = off;
-    if (d->train) off += align256((size_t)n * act_width(d->mode, a) * es);
+    // pe / ve: kept by the F32 forward only; the BF16 layer-major backward recomputes them (the
+    // sample-major BF16 path writes them itself, enc_store_kernel)
+    const bool enc = a == A_PE || a == A_VE;
+    if (d->train && !(enc && use_hidden_path(d))) off += align256((size_t)n * act_width(d->mode, a) * es);
   }
   L.rec = off;
   if (d->train) off += align256((size_t)n * 16);
@@ -241,18 +244,19 @@ int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, 
   return DEN_OK;
 }
 
-// One streamed weight-gradient launch (den_dwstream.hip) over the whole sample range.
-template <int MA, int MT, int NB, int NT, int NW, int DEPTH, int U = 1>
-int launch_dwstream(const den_render_desc* d, const WsLayout& L, char* ws, int a0, int a1, int b0, int b1,
-                    hipStream_t s) {
+// One streamed weight-gradient launch (den_dwstream.hip) over the whole sample range; ENC: the
+// column tiles it recomputes from the samples (b0 / b1 then unused).
+template <int MA, int MT, int NB, int NT, int NW, int DEPTH, int U = 1, int ENC = 0>
+int launch_dwstream(const den_render_desc* d, const den_render_io* io, const WsLayout& L, char* ws, int a0, int a1,
+                    int b0, int b1, hipStream_t s) {
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
   DwStreamArgs P{};
   P.a[0] = ws + L.act[a0];
   P.a_tiles[0] = act_width(DEN_MODE_BF16, a0) / 32;
   P.a[1] = a1 >= 0 ? ws + L.act[a1] : nullptr;
   P.a_tiles[1] = a1 >= 0 ? act_width(DEN_MODE_BF16, a1) / 32 : 0;
-  P.b[0] = ws + L.act[b0];
-  P.b_tiles[0] = act_width(DEN_MODE_BF16, b0) / 32;
+  P.b[0] = b0 >= 0 ? ws + L.act[b0] : nullptr;
+  P.b_tiles[0] = b0 >= 0 ? act_width(DEN_MODE_BF16, b0) / 32 : 0;
   P.b[1] = b1 >= 0 ? ws + L.act[b1] : nullptr;
   P.b_tiles[1] = b1 >= 0 ? act_width(DEN_MODE_BF16, b1) / 32 : 0;
   P.partial = (float*)(ws + L.dw_partial);
@@ -260,9 +264,22 @@ int launch_dwstream(const den_render_desc* d, const WsLayout& L, char* ws, int a
   P.n_blocks = n / 32 / U;
   const int64_t grid = hidden_grid(n);
   P.per_wg = (P.n_blocks + grid - 1) / grid;
+  P.points = d->points;
+  P.n_samples = d->n_samples;
+  P.contraction = d->contraction;
+  for (int i = 0; i < 6; ++i) P.aabb[i] = d->aabb[i];
+  P.near_p = d->near_plane;
+  P.far_p = d->far_plane;
+  P.rays_o = io->rays_o;
+  P.rays_d = io->rays_d;
+  P.jitter = io->jitter;
+  P.ray_idx = io->ray_indices;
+  P.t_start = io->t_starts;
+  P.t_end = io->t_ends;
   {
     DEN_TIMED(T_DW_GEMM, s);
-    hipLaunchKernelGGL((dwstream_kernel<MA, MT, NB, NT, NW, DEPTH, U>), dim3((unsigned)grid), dim3(64 * NW), 0, s, P);
+    hipLaunchKernelGGL((dwstream_kernel<MA, MT, NB, NT, NW, DEPTH, U, ENC>), dim3((unsigned)grid), dim3(64 * NW), 0, s,
+                       P);
   }
   DEN_LAUNCHED();
   return DEN_OK;
@@ -445,11 +462,15 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
   if (!(parts & 2)) return DEN_OK;
   if (hidden) {
     // streamed, operand-sharing weight gradients (den_dwstream.hip)
-    if ((rc = launch_dwstream<8, 16, 2, 2, DWS_NW1, 3>(d, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK)
+    // (pe and ve are recomputed from the samples: the BF16 forward does not store them)
+    if ((rc = launch_dwstream<8, 16, 2, 2, DWS_NW1, 3, 1, ENC_PE>(d, io, L, ws, D_Z0 + 0, D_Z0 + 5, -1, -1, s)) !=
+        DEN_OK)
       return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3>(d, L, ws, D_ZG, -1, A_BT, A_VE, s)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3, ENC_VE>(d, io, L, ws, D_ZG, -1, A_BT, -1, s)) !=
+        DEN_OK)
+      return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 4, 9, 0, 4, L_G, 256, WIDTH, 1, G, s)) != DEN_OK) return rc;
     // (Lb's weight gradient comes from its hidden launch, Lr's from render_bwd_kernel<1, 1>)
     if (g->grad_bkgd) {
@@ -458,6 +479,11 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
       DEN_LAUNCHED();
     }
     return DEN_OK;
+  }
+  if constexpr (MODE == DEN_MODE_BF16) {
+    const int64_t nb = n / 32;
+    hipLaunchKernelGGL(enc_store_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, make_args<MODE>(d, io, L), nb);
+    DEN_LAUNCHED();
   }
   if ((rc = launch_dw<MODE, 8, 64, 0>(d, L, ws, 0, D_Z0 + 0, A_PE, -1, 0, G, s)) != DEN_OK) return rc;
   if (hidden) {
@@ -1726,7 +1752,7 @@ int den_queue_raw_events(int64_t n, int32_t img_height, int32_t img_width, const
                          const int64_t* timestamp, const uint8_t* polarity, void* workspace, size_t workspace_bytes,
                          int64_t* out_position, int64_t* out_start_ts, int64_t* out_end_ts, int64_t* out_num_pos,
                          int64_t* out_num_neg, int64_t* out_stats, void* stream) {
-  if (!out_position) return fail(DEN_EINVAL, "bad arguments: out_position");
+  if (!out_position && n > 0) return fail(DEN_EINVAL, "bad arguments: out_position");
   return queue_impl(n, img_height, img_width, position, timestamp, polarity, workspace, workspace_bytes, out_position,
                     out_start_ts, out_end_ts, out_num_pos, out_num_neg, out_stats, (hipStream_t)stream);
 }

@@ -211,7 +211,8 @@ struct QueueEmitArgs {
 __global__ void queue_emit_kernel(QueueEmitArgs A) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
-    A.out_count[0] = A.status[0] ? -1 : A.offsets[A.n];
+    // stats only (den_max_refractory_period: no scan, offsets null): the count of intervals
+    A.out_count[0] = A.status[0] ? -1 : (A.offsets ? A.offsets[A.n] : (int64_t)A.n_intervals[0]);
     if (A.out_min_interval) A.out_min_interval[0] = (int64_t)(A.min_biased[0] ^ 0x8000000000000000ull);
     if (A.out_n_intervals) A.out_n_intervals[0] = (int64_t)A.n_intervals[0];
   }

@@ -316,6 +316,96 @@ __device__ __forceinline__ float enc_feature(const float* v, int f, int n_deg) {
   return 0.0f;
 }
 
+// The render samples' field inputs, shared by the forward and the kernels that recompute the
+// encodings instead of reading stored ones (BF16: den_dwstream.hip, den_render.hip's backward).
+// Sample s of a render call (den_render_desc.points): 0 the fixed-count stratified sampler (ray
+// s / n_samples), 1 a given point, 2 a packed ray-marching sample -> contracted position xc, view
+// direction, selector.  AT: any argument struct with the RenderArgs sampler fields.
+template <typename AT>
+__device__ __forceinline__ void sample_point(const AT& A, const float* aabb, int64_t s, float* xc, float* dir,
+                                             float* sel) {
+  float o[3];
+  if (A.points == 1) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      o[a] = A.rays_o[s * 3 + a];
+      dir[a] = A.rays_d[s * 3 + a];
+    }
+    contract_point(o, aabb, xc, sel, A.contraction);
+  } else if (A.points == 2) {
+    // packed ray-marching samples: position o + d (t0 + t1)/2 of the sample's ray (utils.py:83-87)
+    const int64_t r = A.ray_idx[s];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      o[a] = A.rays_o[r * 3 + a];
+      dir[a] = A.rays_d[r * 3 + a];
+    }
+    contract(o, dir, A.t_start[s], A.t_end[s], aabb, xc, sel, A.contraction);
+  } else {
+    const int64_t ray = s / A.n_samples;
+    const int k = (int)(s - ray * A.n_samples);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      o[a] = A.rays_o[ray * 3 + a];
+      dir[a] = A.rays_d[ray * 3 + a];
+    }
+    const float u = A.jitter[ray];
+    RayGeom g = ray_geom(o, dir, aabb, A.near_p, A.far_p);
+    float t0, t1;
+    sample_interval(g, k, u, A.n_samples, &t0, &t1);
+    contract(o, dir, t0, t1, aabb, xc, sel);
+  }
+}
+
+// the view-encoding input d * pi (mlp.py:353-355)
+__device__ __forceinline__ void view_input(const float* dir, float* dv) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int a = 0; a < 3; ++a) dv[a] = dir[a] * 3.1415927f;
+}
+
+// the sine argument of encoding feature f (f in the sine range), exactly as enc_feature forms it
+__device__ __forceinline__ float enc_arg(const float* v, int f, int n_deg) {
+#pragma clang fp contract(off)
+  const int nd = 3 * n_deg;
+  int q = f - 3;
+  const bool cosine = q >= nd;
+  if (cosine) q -= nd;
+  float xb = v[q % 3] * (float)(1 << (q / 3));
+  if (cosine) xb = xb + 1.5707964f;
+  return xb;
+}
+
+// accumulator tile p of the encoding of v (n_deg 10: pe of the position, 4: ve of the view input):
+// register r of lane group grp = feature p * TM + acc_row(grp, r), as the forward's fake tiles.
+// BF16 (two lane groups): the two groups' features of a register differ by 4 and are compile-time
+// constants, so the argument is one select between two constant-index products and ONE sine --
+// not a per-lane choice of the coordinate (v[q % 3] with a lane-dependent q), whose lane masks
+// filled the forward's scalar registers.  The same values as enc_feature, bit for bit.
+template <int MODE>
+__device__ __forceinline__ typename Tr<MODE>::Acc enc_tile(const float* v, int p, int grp, int n_deg) {
+  typename Tr<MODE>::Acc a;
+  if constexpr (MODE == 1) {
+    const int nd = 3 * n_deg;
+    const bool hi = grp != 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int f0 = p * 32 + acc_row(1, 0, r), f1 = f0 + 4;
+      const bool sin0 = f0 >= 3 && f0 < 3 + 2 * nd, sin1 = f1 >= 3 && f1 < 3 + 2 * nd;
+      if (sin0 && sin1) {
+        const float x = hi ? enc_arg(v, f1, n_deg) : enc_arg(v, f0, n_deg);
+        a[r] = __sinf(x);
+      } else {
+        a[r] = hi ? enc_feature<false>(v, f1, n_deg) : enc_feature<false>(v, f0, n_deg);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < Tr<MODE>::REGS; ++r) a[r] = enc_feature<true>(v, p * Tr<MODE>::TM + acc_row(MODE, grp, r), n_deg);
+  }
+  return a;
+}
+
 // ------------------------------------------------------------------ wave primitives
 __device__ __forceinline__ float wave_incl_scan(float v) {
   const int lane = threadIdx.x & 63;

@@ -29,36 +29,75 @@ constexpr int DWS_D3 = 2, DWS_U3 = 2;  // Lg: ring steps in flight, wave blocks 
 struct DwStreamArgs {
   const char* a[2];     // dz tensors (wave-block major), row tiles [0, MA) from a[0], [MA, MT) from a[1]
   int a_tiles[2];       // tiles per wave block of each dz tensor
-  const char* b[2];     // x tensors, column tiles [0, NB) from b[0], [NB, NT) from b[1]
+  const char* b[2];     // x tensors, column tiles [0, NB) from b[0], [NB, NT) from b[1] (unused when computed)
   int b_tiles[2];
   float* partial;       // [gridDim.x][MT][NT + 1][64][16]
   int64_t n_blocks;
   int64_t per_wg;
+  // the render samples (RenderArgs' sampler fields, sample_point): the encodings recomputed (ENC)
+  int points, n_samples, contraction;
+  float aabb[6];
+  float near_p, far_p;
+  const float* rays_o;
+  const float* rays_d;
+  const float* jitter;
+  const int* ray_idx;
+  const float* t_start;
+  const float* t_end;
 };
+
+// A BF16 accumulator tile into LDS where the LDS-DMA of its stored copy would put it (the
+// XOR-permuted slots of hb_slot, piece f = registers 8f .. 8f + 7)
+__device__ __forceinline__ void lds_tile_store(char* tile, const f32x16& a) {
+  bf16x8 f[2];
+  acc_to_frags<1>(a, f);
+  const int lane = threadIdx.x & 63;
+  *(bf16x8*)(tile + hb_slot(lane, 0) * 16) = f[0];
+  *(bf16x8*)(tile + 1024 + hb_slot(lane, 1) * 16) = f[1];
+}
+
+// ENC bits: 1 = column tiles [0, NB) are the positional encoding (PE_PAD = 2 tiles), 2 = column
+// tiles [NB, NT) are the view encoding (VE_PAD = 1 tile) -- computed from the samples' rays into
+// the ring slot instead of stored by the forward and read back (192 B per sample each way)
+constexpr int ENC_PE = 1, ENC_VE = 2;
 
 // DMA of one 1 KiB piece of tile `t` (fragment f) of a wave block into its ring-slot position
 __device__ __forceinline__ void dws_dma_piece(const char* tile_src, char* dst, int f) {
   const int lane = threadIdx.x & 63;
   const uint32_t off = (uint32_t)hb_slot(lane, f) * 16;
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)dst);
-  const char* base = tile_src + f * 1024;
+  // the 64-bit source as scalars (two readfirstlanes, each through uint32_t: the low word must not
+  // sign-extend into the high one): the "s" operand then never lands in VGPRs, whatever the
+  // compiler concludes about the uniformity of the address arithmetic around it
+  const uint64_t a64 = (uint64_t)(uintptr_t)(tile_src + f * 1024);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a64);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a64 >> 32));
+  const char* base = (const char*)(uintptr_t)(((uint64_t)hi << 32) | lo);
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"(off), "s"(base), "s"(m0)
                : "memory", "m0");
 }
 
 // U: wave blocks per ring slot (one barrier per U blocks); P.n_blocks / P.per_wg count U-block steps
-template <int MA, int MT, int NB, int NT, int NW, int DEPTH, int U = 1>
+template <int MA, int MT, int NB, int NT, int NW, int DEPTH, int U = 1, int ENC = 0>
 __attribute__((aligned(4096)))  // page-aligned code (r04y A/B)
 __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
   constexpr int TILES = MT + NT;
   constexpr int BLK = TILES * HB_TILE;              // one wave block's tiles
   constexpr int SLOT = U * BLK;
   constexpr int RING = DEPTH + 1;
-  constexpr int PIECES = 2 * TILES * U;             // 1 KiB pieces per step
+  constexpr int T_PE = (ENC & ENC_PE) ? NB : 0;     // computed column tiles: [MT, MT + T_PE) pe,
+  constexpr int T_VE = (ENC & ENC_VE) ? NT - NB : 0;  // [MT + NB, MT + NT) ve
+  static_assert(!(ENC & ENC_PE) || NB == PE_PAD / 32, "pe is PE_PAD / 32 column tiles");
+  static_assert(!(ENC & ENC_VE) || NT - NB == VE_PAD / 32, "ve is VE_PAD / 32 column tiles");
+  static_assert(!(ENC & ENC_VE) || !(ENC & ENC_PE), "one encoding per launch");
+  constexpr int T_DMA = TILES - T_PE - T_VE;        // stored tiles, fetched by LDS-DMA
+  constexpr int T_ENC = T_PE + T_VE;
+  constexpr int PIECES = 2 * T_DMA * U;             // 1 KiB DMA pieces per step
   constexpr int TPW = (MT * NT + NW - 1) / NW;      // output tiles per wave
   static_assert(RING * SLOT <= 160 * 1024, "ring exceeds the LDS");
   __shared__ __attribute__((aligned(16))) char lds[RING * SLOT];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR) for the DMA operands
   const int64_t b0 = (int64_t)blockIdx.x * P.per_wg;
   const int64_t b1 = b0 + P.per_wg < P.n_blocks ? b0 + P.per_wg : P.n_blocks;
 
@@ -67,15 +106,70 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
     for (int q = 0; q < (PIECES + NW - 1) / NW; ++q) {
       const int pc = __builtin_amdgcn_readfirstlane(q * NW + wave);
       if (pc < PIECES) {
-        const int ub = pc / (2 * TILES), tp = pc % (2 * TILES);
-        const int t = tp >> 1, f = tp & 1;
+        const int ub = pc / (2 * T_DMA), tp = pc % (2 * T_DMA);
+        const int td = tp >> 1, f = tp & 1;
+        const int t = (td >= MT && T_PE) ? td + T_PE : td;  // the stored tiles skip the computed pe range
         const int64_t wb = blk * U + ub;
         const char* src;
         if (t < MA) src = P.a[0] + (wb * P.a_tiles[0] + t) * HB_TILE;
         else if (t < MT) src = P.a[1] + (wb * P.a_tiles[1] + (t - MA)) * HB_TILE;
         else if (t < MT + NB) src = P.b[0] + (wb * P.b_tiles[0] + (t - MT)) * HB_TILE;
         else src = P.b[1] + (wb * P.b_tiles[1] + (t - MT - NB)) * HB_TILE;
-        dws_dma_piece(src, dst + pc * 1024, f);
+        dws_dma_piece(src, dst + ub * BLK + t * 2048 + f * 1024, f);
+      }
+    }
+    if constexpr (T_ENC > 0) {
+      // the encoding tiles: one wave per (wave block, tile), lane = sample (l & 31), lane group
+      // l >> 5, the forward's sampler and enc_tile -- bit-identical to the tiles it would store
+#pragma unroll
+      for (int e0 = 0; e0 < T_ENC * U; e0 += NW) {
+        const int e = e0 + wave;
+        if (e < T_ENC * U) {
+          const int ub = e / T_ENC, te = e % T_ENC;
+          // lane-derived values from an opaque copy of the thread index: loop-invariant, the
+          // encoding's per-lane-group constants were hoisted out of the block loop and spilled
+          int tid = threadIdx.x;
+          asm volatile("" : "+v"(tid));
+          const int ln = tid & 63;
+          const int64_t s = (blk * U + ub) * 32 + (ln & 31);
+          // the sampler's arguments read here, from the kernarg segment through an opaque pointer:
+          // preloaded, the dozen extra argument words stay live in scalar registers across the loop
+          typedef __attribute__((address_space(4))) const DwStreamArgs KArgs;
+          KArgs* Pp = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // P is the kernel's only argument
+          asm volatile("" : "+s"(Pp));
+          float aabb[6];
+#pragma unroll
+          for (int q = 0; q < 6; ++q) aabb[q] = Pp->aabb[q];
+          float xc[3], dir[3], sel;
+          if (Pp->points == 0) {
+            // the fixed-count sampler of sample_point, with the ray wave-uniform: a 32-sample wave
+            // block lies within one ray (n_samples is 64, 128 or 256, den_render_desc)
+            const int64_t s0 = (blk * U + ub) * 32;
+            const int64_t ray = s0 / Pp->n_samples;
+            const int k = (int)(s0 - ray * Pp->n_samples) + (ln & 31);
+            float o[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+              o[a] = Pp->rays_o[ray * 3 + a];
+              dir[a] = Pp->rays_d[ray * 3 + a];
+            }
+            const RayGeom g = ray_geom(o, dir, aabb, Pp->near_p, Pp->far_p);
+            float t0, t1;
+            sample_interval(g, k, Pp->jitter[ray], Pp->n_samples, &t0, &t1);
+            contract(o, dir, t0, t1, aabb, xc, &sel);
+          } else {
+            sample_point(*Pp, aabb, s, xc, dir, &sel);
+          }
+          f32x16 v;
+          float dv[3];
+          view_input(dir, dv);
+          // the tile index as a compile-time constant (wave-uniform branches): enc_tile's feature
+          // indices then fold, with no per-lane coordinate choice
+#pragma unroll
+          for (int tt = 0; tt < T_ENC; ++tt)
+            if (te == tt) v = T_PE ? enc_tile<1>(xc, tt, ln >> 5, 10) : enc_tile<1>(dv, tt, ln >> 5, 4);
+          lds_tile_store(dst + ub * BLK + (MT + (T_PE ? 0 : NB) + te) * HB_TILE, v);
+        }
       }
     }
   };
@@ -171,7 +265,7 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
 }
 
 // the launches of a BF16 backward
-template __global__ void dwstream_kernel<8, 16, 2, 2, DWS_NW1, 3>(DwStreamArgs);  // L0 + L5 pe
-template __global__ void dwstream_kernel<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3>(DwStreamArgs);    // Lg
+template __global__ void dwstream_kernel<8, 16, 2, 2, DWS_NW1, 3, 1, ENC_PE>(DwStreamArgs);  // L0 + L5 pe
+template __global__ void dwstream_kernel<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3, ENC_VE>(DwStreamArgs);    // Lg
 
 }  // namespace den

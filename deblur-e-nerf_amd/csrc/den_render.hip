@@ -519,7 +519,10 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
     for (int q = 0; q < 8; ++q) vm.prof[q] = 0;
 #endif
 
-    // sample positions -> positional encoding as PE_PAD/TM fake accumulator tiles -> fragments
+    // sample positions -> positional encoding as PE_PAD/TM fake accumulator tiles -> fragments.
+    // Kept for the backward in F32 mode only: the BF16 backward recomputes pe / ve where it needs
+    // them (den_dwstream.hip: 192 B per sample neither stored nor read back)
+    constexpr bool STORE_ENC = TRAIN && MODE == 0;
     constexpr int PE_T = PE_PAD / TM, PE_S = PE_T * FPT;
     float dir[NB][3], sel[NB];
     Frag pe[NB * PE_S];
@@ -534,7 +537,6 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
         }
         contract_point(o, aabb, xc, &sel[b], A.contraction);
       } else if (A.points == 2) {
-        // packed ray-marching samples: position o + d (t0 + t1)/2 of the sample's ray (utils.py:83-87)
         const int64_t r = A.ray_idx[sample[b]];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
@@ -558,10 +560,8 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
       }
 #pragma unroll
       for (int p = 0; p < PE_T; ++p) {
-        Acc a;
-#pragma unroll
-        for (int r = 0; r < REGS; ++r) a[r] = enc_feature<EXACT>(xc, p * TM + acc_row(MODE, grp, r), 10);
-        if (TRAIN) store_tile_vals<MODE>(act_ptr<MODE>(A, A_PE, sample[b], p), a);
+        const Acc a = enc_tile<MODE>(xc, p, grp, 10);
+        if (STORE_ENC) store_tile_vals<MODE>(act_ptr<MODE>(A, A_PE, sample[b], p), a);
         acc_to_frags<MODE>(a, pe + b * PE_S + p * FPT);
       }
     }
@@ -569,7 +569,12 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
     // the pe stores (the youngest vector-memory ops) may stay in flight -- vmcnt is in-order, so
     // waiting for all but them covers the DMAs (older ops left in flight only make the later counted
     // waits stricter)
-    constexpr int PE_ST = TRAIN ? NB * PE_T * (MODE == 1 ? 2 : 1) : 0;
+    // the pe fragments are complete here: without this (or the stores of the F32 forward) the
+    // compiler sinks the encoding into layer 0's schedule, whose lane masks then spill (the BF16
+    // inference forward did, 52 SGPRs + 27 VGPRs, before r05)
+#pragma unroll
+    for (int q = 0; q < NB * PE_S; ++q) asm volatile("" : "+v"(pe[q]));
+    constexpr int PE_ST = STORE_ENC ? NB * PE_T * (MODE == 1 ? 2 : 1) : 0;
     static_assert(PE_ST < 64, "vmcnt is 6 bits");
     wait_vm_lgkm0<PE_ST>();
     __syncthreads();
@@ -610,16 +615,12 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
     Frag ve[NB * VE_S];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-#pragma clang fp contract(off)
       float dv[3];
-#pragma unroll
-      for (int a = 0; a < 3; ++a) dv[a] = dir[b][a] * 3.1415927f;
+      view_input(dir[b], dv);
 #pragma unroll
       for (int p = 0; p < VE_T; ++p) {
-        Acc a;
-#pragma unroll
-        for (int r = 0; r < REGS; ++r) a[r] = enc_feature<EXACT>(dv, p * TM + acc_row(MODE, grp, r), 4);
-        if (TRAIN) {
+        const Acc a = enc_tile<MODE>(dv, p, grp, 4);
+        if (STORE_ENC) {
           store_tile_vals<MODE>(act_ptr<MODE>(A, A_VE, sample[b], p), a);
           vm.issued += MODE == 1 ? 2 : 1;
         }
@@ -1056,6 +1057,25 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
     bwd_layer_run<MODE, LAST_J, 8, KS, 0>(A, lds, sample, xb, xa, A_S0 + 1, D_Z0 + 1);
     bwd_layer_run<MODE, LAST_J, 9, KS, 0>(A, lds, sample, xa, xb, A_S0 + 0, D_Z0 + 0);
   }
+}
+
+// BF16 sample-major backward (bwd_path = 1, the A/B reference path): the pe / ve tiles its split-K
+// GEMMs read, written from the samples (the BF16 forward keeps neither); one wave per wave block
+__global__ __launch_bounds__(256) void enc_store_kernel(RenderArgs<1> A, int64_t n_blocks) {
+  const int64_t wb = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wb >= n_blocks) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t s = wb * 32 + (lane & 31);
+  float aabb[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) aabb[q] = A.aabb[q];
+  float xc[3], dir[3], sel, dv[3];
+  sample_point(A, aabb, s, xc, dir, &sel);
+  view_input(dir, dv);
+#pragma unroll
+  for (int p = 0; p < PE_PAD / 32; ++p) store_tile_vals<1>(act_ptr<1>(A, A_PE, s, p), enc_tile<1>(xc, p, lane >> 5, 10));
+#pragma unroll
+  for (int p = 0; p < VE_PAD / 32; ++p) store_tile_vals<1>(act_ptr<1>(A, A_VE, s, p), enc_tile<1>(dv, p, lane >> 5, 4));
 }
 
 template __global__ void render_fwd_kernel<0, false>(RenderArgs<0>);

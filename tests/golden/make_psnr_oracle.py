@@ -59,31 +59,43 @@ def main():
     ap.add_argument("--rd", type=int, default=1)
     ap.add_argument("--ckpt", default=None)
     ap.add_argument("--render-only", action="store_true", help="re-render the views from a finished checkpoint")
+    ap.add_argument("--device", default="cpu",
+                    help="where torch executes the oracle: cpu (the build container), or cuda -- torch's own GPU "
+                         "kernels (rocBLAS / hipBLASLt GEMMs, elementwise ops), never libden -- for the many "
+                         "sequences of the oracle's own seed study")
+    ap.add_argument("--out-dir", default=None, help="fixture directory (default tests/golden)")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
+    if a.device != "cpu":
+        torch.backends.cuda.matmul.allow_tf32 = False  # the oracle is f32 arithmetic
+        torch.backends.cudnn.allow_tf32 = False
+        torch.set_default_device(a.device)
     L = dict(bench.PSNR_LEG)
     train_cfg = json.dumps({k: L[k] for k in TRAIN_KEYS}, sort_keys=True)
-    ckpt = a.ckpt or f"/tmp/psnr_oracle_s{a.seq}.pt"
+    ckpt = a.ckpt or (f"/tmp/psnr_oracle_s{a.seq}.pt" if a.device == "cpu" else f"/tmp/psnr_oracle_{a.device}_s{a.seq}.pt")
     rd, n_events, n_samples, steps = a.rd, L["n_events"], L["n_samples"], L["steps"]
-    teacher = {k: v.clone() for k, v in unflat(bench.teacher_field(rd, L), rd).items()}
+    with torch.device("cpu"):
+        tflat = bench.teacher_field(rd, L)
+        flat0, bk0 = student_init(rd, L)
+    teacher = {k: v.clone().to(a.device) for k, v in unflat(tflat.to(a.device), rd).items()}
     ones = torch.ones(rd)
-    flat0, bk0 = student_init(rd, L)
+    flat0, bk0 = flat0.to(a.device), bk0.to(a.device)
     p = {k: v.clone().requires_grad_(True) for k, v in unflat(flat0, rd).items()}
     bk = bk0.clone().requires_grad_(True)
     names = [n for n, _, _ in onerf.layer_specs(rd)]
     leaves = [p[n + s] for n in names for s in (".weight", ".bias")]
     opt = torch.optim.Adam([{"params": leaves, "weight_decay": 1e-6}, {"params": [bk], "weight_decay": 0.0}],
                            lr=L["lr0"])
-    gen = torch.Generator().manual_seed(L["batch_seed"] + a.seq)
+    gen = torch.Generator(device="cpu").manual_seed(L["batch_seed"] + a.seq)
     start, losses, threads = 0, [], a.threads
     if os.path.exists(ckpt):
-        ck = torch.load(ckpt, weights_only=False)  # this script's own checkpoint
+        ck = torch.load(ckpt, weights_only=False, map_location=a.device)  # this script's own checkpoint
         if ck["train_cfg"] != train_cfg:
             raise SystemExit(f"{ckpt} was trained on another leg: {ck['train_cfg']}")
         for t, v in zip(leaves + [bk], ck["params"]):
             t.data.copy_(v)
         opt.load_state_dict(ck["opt"])
-        gen.set_state(ck["gen"])
+        gen.set_state(ck["gen"].cpu())
         start, losses, threads = ck["step"], ck["losses"], ck.get("threads", a.threads)
         print(f"resumed at step {start}", flush=True)
     elif a.render_only:
@@ -92,7 +104,9 @@ def main():
     for it in range(start, steps):
         for g in opt.param_groups:
             g["lr"] = bench.lr_at(L["lr0"], it, steps, L["milestones"], L["lr_gamma"])
-        b = bench._teacher_batch(gen, n_events)
+        with torch.device("cpu"):  # the CPU generator's draws, as the HIP leg's
+            b = bench._teacher_batch(gen, n_events)
+        b = {k: v.to(a.device) for k, v in b.items()}
         with torch.no_grad():
             col, _, _, _ = onerf.render_rays(teacher, b["rays_o"], b["rays_d"], b["jitter"], n_samples=n_samples,
                                              bkgd=ones)
@@ -112,19 +126,25 @@ def main():
             print(f"seq {a.seq} step {it + 1}/{steps}  loss {float(total):.6f}  {el / (it + 1 - start):.2f} s/step",
                   flush=True)
     view = L["view"]
-    vo, vd, nv = bench.psnr_views(view, L["n_views"])
+    with torch.device("cpu"):
+        vo, vd, nv = bench.psnr_views(view, L["n_views"])
+    vo, vd = vo.to(a.device), vd.to(a.device)
     vu = torch.full((vo.shape[0],), 0.5)
     with torch.no_grad():
         target, _, _, _ = onerf.render_rays(teacher, vo, vd, vu, n_samples=n_samples, bkgd=ones)
         pred, _, _, _ = onerf.render_rays(p, vo, vd, vu, n_samples=n_samples, bkgd=torch.nn.functional.softplus(bk))
-    ps, ps_raw, gamma, scale = bench.aligned_psnr(pred, target, nv, view)
+    pred, target = pred.cpu(), target.cpu()
+    with torch.device("cpu"):
+        ps, ps_raw, gamma, scale = bench.aligned_psnr(pred, target, nv, view)
     print(f"oracle seq {a.seq}: PSNR {ps:.4f} dB (uncorrected {ps_raw:.3f}), gamma {gamma:.4f}, scale {scale:.4f}")
-    out = bench.oracle_fixture_path(a.seq)
+    out = bench.oracle_fixture_path(a.seq) if a.out_dir is None else \
+        os.path.join(a.out_dir, os.path.basename(bench.oracle_fixture_path(a.seq)))
     np.savez_compressed(out, psnr_db=np.array(ps), psnr_uncorrected_db=np.array(ps_raw), gamma=np.array(gamma),
                         scale=np.array(scale), pred=pred[:, 0].reshape(nv, view, view).numpy().astype(np.float32),
                         target=target[:, 0].reshape(nv, view, view).numpy().astype(np.float32),
                         losses=np.array(losses, dtype=np.float64), rd=np.array(rd), seq=np.array(a.seq),
-                        threads=np.array(threads), leg=np.array(json.dumps(L, sort_keys=True)))
+                        threads=np.array(threads), device=np.array(a.device),
+                        leg=np.array(json.dumps(L, sort_keys=True)))
     print("wrote", out, os.path.getsize(out), "bytes")
 
 
