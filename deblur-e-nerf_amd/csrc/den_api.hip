@@ -22,6 +22,7 @@
 #include "den_ngp_mfma.hip"
 #include "den_pixbw.hip"
 #include "den_render.hip"
+#include "den_head_bwd.hip"
 #include "den_raygrad.hip"
 #include "den_sh.hip"
 #include "den_dataset.hip"
@@ -115,7 +116,8 @@ WsLayout ws_layout(const den_render_desc* d) {
     L.act[a] = off;
     // pe / ve: kept by the F32 forward only; the BF16 layer-major backward recomputes them (the
     // sample-major BF16 path writes them itself, enc_store_kernel)
-    const bool enc = a == A_PE || a == A_VE;
+    // dz_g: kept in registers by the BF16 head backward (render_head_bwd_kernel, the fused Lg weight gradient)
+    const bool enc = a == A_PE || a == A_VE || a == D_ZG;
     if (d->train && !(enc && use_hidden_path(d))) off += align256((size_t)n * act_width(d->mode, a) * es);
   }
   L.rec = off;
@@ -288,10 +290,11 @@ int launch_dwstream(const den_render_desc* d, const den_render_io* io, const WsL
 // Reduction of row tiles [mt0, mt0 + MT) of a streamed partial with NT_ALL column tiles into layer
 // `layer`'s gradient (red_n1 / n1_feat / bias as in launch_dw).
 int launch_dwstream_reduce(const den_render_desc* d, const WsLayout& L, char* ws, int MT_ALL, int NT_ALL, int mt0,
-                           int MT, int layer, int red_n1, int n1_feat, int bias, float* grad, hipStream_t s) {
+                           int MT, int layer, int red_n1, int n1_feat, int bias, float* grad, hipStream_t s,
+                           int splits = -1) {
   DwReduceArgs R{};
   R.partial = (float*)(ws + L.dw_partial);
-  R.splits = (int)hidden_grid((int64_t)d->n_rays * d->n_samples);
+  R.splits = splits > 0 ? splits : (int)hidden_grid((int64_t)d->n_rays * d->n_samples);
   R.MT = MT;
   R.NT = NT_ALL;
   R.m_off = 0;
@@ -314,8 +317,7 @@ int launch_dwstream_reduce(const den_render_desc* d, const WsLayout& L, char* ws
 }
 
 // Reduction of the fused Lr weight-gradient partials (render_bwd_kernel<1, 1>) into the gradient.
-int launch_lr_reduce(const den_render_desc* d, const WsLayout& L, char* ws, float* grad, hipStream_t s) {
-  const int64_t n_wg = (int64_t)d->n_rays * d->n_samples / wg_samples(DEN_MODE_BF16);
+int launch_lr_reduce(const den_render_desc* d, const WsLayout& L, char* ws, float* grad, hipStream_t s, int64_t n_wg) {
   const int G1 = (int)std::min<int64_t>(LR_G1, n_wg);
   DwReduceArgs R{};
   R.MT = 1;
@@ -440,14 +442,19 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
   if (parts & 1) {
     if constexpr (MODE == DEN_MODE_BF16) {
       if (hidden) {
-        // head (compositing adjoint, Lr^T, Lg^T[, Lb^T]) sample-major, then [Lb,] L7..L1 layer-major
+        // head (compositing adjoint, Lr^T + dW_r, Lg^T + dW_g) sample-major and persistent, then Lb,
+        // L7..L1 layer-major.  The Lg partial shares dw_partial with the hidden launches: reduced first.
+        const int64_t items = n / wg_samples(MODE);
+        const int head_grid = (int)std::min<int64_t>(items, HB_GRID_MAX);
         {
           DEN_TIMED(T_RENDER_BWD, s);
-          hipLaunchKernelGGL((render_bwd_kernel<MODE, 1>), dim3((unsigned)(n / wg_samples(MODE))),
-                             dim3(512), 0, s, A);
+          hipLaunchKernelGGL(render_head_bwd_kernel, dim3((unsigned)head_grid), dim3(512), 0, s, A,
+                             (float*)(ws + L.dw_partial));
         }
         DEN_LAUNCHED();
-        if ((rc = launch_lr_reduce(d, L, ws, G, s)) != DEN_OK) return rc;
+        if ((rc = launch_lr_reduce(d, L, ws, G, s, head_grid)) != DEN_OK) return rc;
+        if ((rc = launch_dwstream_reduce(d, L, ws, 4, 9, 0, 4, L_G, 256, WIDTH, 1, G, s, head_grid)) != DEN_OK)
+          return rc;
         for (int l = 8; l >= 1; --l)
           if ((rc = launch_hidden(d, io, L, ws, l, G, s)) != DEN_OK) return rc;
       }
@@ -468,11 +475,7 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
       return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3, ENC_VE>(d, io, L, ws, D_ZG, -1, A_BT, -1, s)) !=
-        DEN_OK)
-      return rc;
-    if ((rc = launch_dwstream_reduce(d, L, ws, 4, 9, 0, 4, L_G, 256, WIDTH, 1, G, s)) != DEN_OK) return rc;
-    // (Lb's weight gradient comes from its hidden launch, Lr's from render_bwd_kernel<1, 1>)
+    // (Lb's weight gradient comes from its hidden launch, Lr's and Lg's from render_head_bwd_kernel)
     if (g->grad_bkgd) {
       hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(1024), 0, s, d->radiance_dim, d->n_rays,
                          (const float*)(ws + L.bkgd_partial), g->grad_bkgd);

@@ -266,6 +266,7 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
 
 // the launches of a BF16 backward
 template __global__ void dwstream_kernel<8, 16, 2, 2, DWS_NW1, 3, 1, ENC_PE>(DwStreamArgs);  // L0 + L5 pe
-template __global__ void dwstream_kernel<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3, ENC_VE>(DwStreamArgs);    // Lg
+// (the Lg launch, dwstream_kernel<4, 4, 8, 9, DWS_NW3, DWS_D3, DWS_U3, ENC_VE>, was replaced in r05 by the
+// weight gradient fused into render_head_bwd_kernel)
 
 }  // namespace den

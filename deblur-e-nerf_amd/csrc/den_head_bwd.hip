@@ -1,0 +1,243 @@
+// den_head_bwd.hip -- the BF16 head backward as a persistent kernel with the Lg weight gradient fused.
+//
+// Per 256-sample item (whole rays), as render_bwd_kernel<1, 1>: the compositing adjoint, Lr^T (with
+// the fused Lr weight gradient) -> dz_g, Lg^T -> dz_b (+ sigma's dz) for the layer-major hidden
+// backward.  In addition the Lg weight gradient
+//   dW_g[o][i] = sum_n dz_g[n][o] x[n][i],  x = [bottleneck (256) | ve (27, padded 32)],  db_g = sum_n dz_g
+// is accumulated here, where dz_g is born: dz_g is no longer written to HBM and read back by a
+// streamed launch (den_dwstream.hip's Lg launch is gone: -512 B per sample of traffic and a launch).
+//   * one workgroup (8 waves) per CU walks items blockIdx.x, + gridDim.x, ...; the weight chunks
+//     of the chain wrap to the next item's first chunk (bwd_layer_run WRAP);
+//   * after Lr^T each wave stages its dz_g tiles (4 x 2 KiB, the XOR-permuted slot layout of
+//     den_hidden.hip) in LDS; a barrier; wave w then owns output column tile w of the bottleneck part
+//     (all 4 row tiles, k = the item's 256 samples): the bottleneck tile (block b, column w) of each
+//     of the item's 8 wave blocks arrives by untracked LDS-DMA in a private double buffer, both
+//     MFMA operands by transposed LDS reads;
+//   * the view encoding is a function of the ray alone (a wave block lies within one ray), so its
+//     B operand is computed in registers -- feature (lane & 31)'s value in all 8 k-slots -- and
+//     waves 0..3 own its four (row tile w, ve) output tiles plus the bias of row tile w;
+//   * the accumulators live in registers for the whole launch; each workgroup writes one split-K
+//     partial in den_dwstream.hip's layout [wg][4][10][64][16] (column 9: the bias), reduced in a
+//     fixed order by dw_reduce_kernel -- deterministic.
+// Reference: the nn.Linear backward of rgb_layer.hidden_layers.0 (external/mlp.py:193-205), fed by
+// the view encoding of mlp.py:353-355.
+
+namespace den {
+
+constexpr int HD_STAGE = 8 * 4 * HB_TILE;  // dz_g of the item: 8 waves x 4 tiles (also each wave's Lr scratch)
+constexpr int HD_XBUF = 2 * HB_TILE;       // per wave: a double buffer of one bottleneck tile
+
+// One bottleneck tile (2 KiB, two 1 KiB pieces) into this wave's private LDS buffer, untracked (the
+// waits are explicit); lane p fetches the tile lane whose fragment belongs in LDS slot p (hb_dma)
+__device__ __forceinline__ void hd_dma_piece(const char* src, char* dst, int f) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)dst);
+  const uint64_t a64 = (uint64_t)(uintptr_t)src;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a64);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a64 >> 32));
+  const char* base = (const char*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  const uint32_t off = (uint32_t)hb_slot(lane, f) * 16;
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"(off), "s"(base), "s"(m0)
+               : "memory", "m0");
+}
+__device__ __forceinline__ void hd_dma_tile(const char* src, char* dst) {
+  hd_dma_piece(src, dst, 0);
+  hd_dma_piece(src + 1024, dst + 1024, 1);
+}
+
+__attribute__((aligned(4096)))  // page-aligned code (r04y A/B)
+__global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A0, float* lg_partial) {
+  constexpr int MODE = 1;
+  using T = Tr<MODE>;
+  using Frag = typename T::Frag;
+  using Acc = typename T::Acc;
+  constexpr int TM = T::TM, FPT = T::FPT;
+  constexpr int WGS = wg_samples(MODE);
+  __shared__ __attribute__((aligned(16))) char lds[2 * LDS_BUF + WGS * 16 + HD_STAGE + 8 * HD_XBUF];
+  float* rec_lds = (float*)(lds + 2 * LDS_BUF);
+  char* stage = lds + 2 * LDS_BUF + WGS * 16;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char* xbuf = stage + HD_STAGE + wave * HD_XBUF;
+  char* lscr = stage + wave * (4 * HB_TILE);  // this wave's Lr scratch = its own dz_g staging area
+
+  // first item's weight chunk 0 (later items: wrapped in by the previous item's last chain step)
+  dma_chunk(A0.w, lds, chunk_bytes_K(bwd_K(MODE, 0)));
+
+  f32x16 lacc;  // dW_r (the fused Lr weight gradient), as render_bwd_kernel<1, 1>
+  f32x16 gacc[5];  // dW_g: [0..3] = (row tile mt, column tile wave); [4] = (row tile wave, ve) for waves < 4
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lacc[r] = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gacc[q][r] = 0.0f;
+  float ldb[3] = {0.f, 0.f, 0.f}, gdb = 0.0f;
+  const int64_t n_items = (int64_t)A0.n_rays * A0.n_samples / WGS;
+
+  for (int64_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+    // the arguments re-read from the kernarg segment per item through an opaque pointer (as the
+    // forward): hoisted out of the loop, every chunk's per-lane DMA address stayed live and spilled
+    typedef __attribute__((address_space(4))) const RenderArgs<1> KArgs;
+    KArgs* Ap = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // A0 is the kernel's first argument
+    asm volatile("" : "+s"(Ap));
+    KArgs& A = *Ap;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));  // lane-derived values per item (not hoisted across the loop)
+    const int lane = tid & 63, c = lane % TM, grp = lane / TM;
+    const int64_t sample = item * WGS + wave * TM + c;
+
+    head_adjoint<MODE>(A, rec_lds, item, sample, wave, lane, c, grp);
+    __syncthreads();  // also: every wave is done with the previous item's staged dz_g
+
+    // fake dz tiles from the per-sample raw gradients (render_bwd_kernel<1, 1>)
+    const f32x4 g4 = *(const f32x4*)(rec_lds + (wave * TM + c) * 4);
+    Acc dzr = acc_zero<MODE>();
+    if (grp == 0) {
+      dzr[0] = g4[1];
+      if (A.rd > 1) dzr[1] = g4[2];
+      if (A.rd > 2) dzr[2] = g4[3];
+    }
+    {
+      const __bf16 z0 = (__bf16)g4[1], z1 = A.rd > 1 ? (__bf16)g4[2] : (__bf16)0.0f,
+                   z2 = A.rd > 2 ? (__bf16)g4[3] : (__bf16)0.0f, zz = (__bf16)0.0f;
+      const bf16x8 v = {z0, z1, z2, zz, zz, zz, zz, zz};
+      *(bf16x8*)(lscr + hb_slot(lane, 0) * 16) = v;
+      *(bf16x8*)(lscr + 1024 + hb_slot(lane, 1) * 16) = v;
+      if (grp == 0) {
+        ldb[0] += (float)z0;
+        ldb[1] += (float)z1;
+        ldb[2] += (float)z2;
+      }
+    }
+    auto lr_hook = [&](int i, const Acc& sv) {
+      Frag gf[FPT];
+      acc_to_frags<MODE>(sv, gf);
+      char* gs = lscr + 2048;
+      *(bf16x8*)(gs + hb_slot(lane, 0) * 16) = gf[0];
+      *(bf16x8*)(gs + 1024 + hb_slot(lane, 1) * 16) = gf[1];
+      const bool keep = ((lane & 31) >> 3) == i;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 a = hb_tr_frag(lscr, kk);
+        const bf16x8 zero = {};
+        a = keep ? a : zero;
+        lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hb_tr_frag(gs, kk), lacc, 0, 0, 0);
+      }
+    };
+
+    constexpr int KS = WIDTH / T::KI;
+    Frag fr[FPT];
+    acc_to_frags<MODE>(dzr, fr);
+    Frag xa[KS + 2 * FPT], xb[KS + 2 * FPT];
+    // j=0 Lr^T: dz_r -> dz_g in registers only (xa, 4 tiles) + the fused Lr weight gradient
+    bwd_layer_run<MODE, 1, 0, FPT, 0, true>(A, lds, sample, fr, xa, A_G, -1, lr_hook);
+    // dz_g into this wave's staging area (its Lr scratch, done with): 4 tiles, the DMA'd-tile layout
+#pragma unroll
+    for (int t = 0; t < WIDTH_COND / TM; ++t) {
+      *(bf16x8*)(lscr + t * HB_TILE + hb_slot(lane, 0) * 16) = xa[t * FPT];
+      *(bf16x8*)(lscr + t * HB_TILE + 1024 + hb_slot(lane, 1) * 16) = xa[t * FPT + 1];
+    }
+    // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles; its last step wraps in the next
+    // item's chunk 0
+    bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true>(A, lds, sample, xa, xb, 0, D_ZB);
+    // sigma's dz: 32 bf16 per wave block in dz_b's ninth tile (hidden_bwd_kernel<true>)
+    if (grp == 0) *(__bf16*)(act_ptr<MODE>(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)g4[0];
+    // (the chain's steps end in barriers: every wave's dz_g is staged)
+
+    // ---- Lg weight gradient over the item: wave w = bottleneck column tile w (x 4 row tiles), and
+    // for w < 4 the (row tile w, ve) tile + row tile w's bias
+    const int64_t wb0 = item * (WGS / TM);  // the item's first wave block
+    auto bt_src = [&](int b) { return A.act[A_BT] + ((wb0 + b) * (WIDTH / TM) + wave) * (int64_t)HB_TILE; };
+    hd_dma_tile(bt_src(0), xbuf);
+#pragma unroll 1
+    for (int b = 0; b < 8; ++b) {
+      if (b + 1 < 8) hd_dma_tile(bt_src(b + 1), xbuf + ((b + 1) & 1) * HB_TILE);
+      // block b's two pieces landed (only block b + 1's two may stay in flight; vmcnt is in-order)
+      asm volatile("" ::: "memory");
+      if (b + 1 < 8) __builtin_amdgcn_s_waitcnt((2 & 15) | (7 << 4) | (0 << 8));  // vmcnt(2) lgkmcnt(0)
+      else __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8));                  // vmcnt(0) lgkmcnt(0)
+      asm volatile("" ::: "memory");
+      const char* xt = xbuf + (b & 1) * HB_TILE;
+      const char* zt = stage + b * (4 * HB_TILE);  // wave b's dz_g tiles = wave block b of the item
+      // the view encoding of block b's ray, feature (stored position) lane & 31, in every k-slot
+      bf16x8 bve;
+      if (wave < 4) {
+        const int64_t ray = (item * WGS + b * TM) / A.n_samples;
+        float d[3], dv[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) d[a] = A.rays_d[ray * 3 + a];
+        view_input(d, dv);
+        const float v = enc_feature<false>(dv, stored_to_row(MODE, lane & 31), 4);
+        const __bf16 vb = (__bf16)v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bve[e] = vb;
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 bx = hb_tr_frag(xt, kk);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          gacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hb_tr_frag(zt + mt * HB_TILE, kk), bx, gacc[mt], 0, 0, 0);
+        if (wave < 4) {
+          const bf16x8 a = hb_tr_frag(zt + wave * HB_TILE, kk);
+          gacc[4] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bve, gacc[4], 0, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gdb += (float)a[e];
+        }
+      }
+    }
+  }
+  // drain (nothing of ours in flight past here but the wrapped chunk DMA of a non-existent item)
+  __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8));
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  // ---- Lr partial (as render_bwd_kernel<1, 1>), through the weight ring
+  {
+    float* red = (float*)lds;
+    if (lane < 32) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) red[wave * LR_PART + (t * 3 + ch) * 32 + lane] = lacc[4 * t + ch];
+    }
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float b = wave_sum(ldb[ch]);
+      if (lane == 0) red[wave * LR_PART + 384 + ch] = b;
+    }
+    if (lane == 0) red[wave * LR_PART + 387] = 0.0f;
+    __syncthreads();
+    for (int e = threadIdx.x; e < LR_PART; e += blockDim.x) {
+      float v = red[e];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) v += red[w * LR_PART + e];
+      A0.lr_partial[(int64_t)blockIdx.x * LR_PART + e] = v;
+    }
+  }
+  // ---- Lg partial [wg][mt][nt][lane][16], nt = 9 the bias (den_dwstream.hip's layout)
+  constexpr int NT = 9;
+  float* base = lg_partial + (int64_t)blockIdx.x * 4 * (NT + 1) * 1024;
+  auto put = [&](int mt, int nt, const f32x16& acc) {
+    float* o = base + ((int64_t)mt * (NT + 1) + nt) * 1024 + lane * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+      *(f32x4*)(o + 4 * q) = v;
+    }
+  };
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) put(mt, wave, gacc[mt]);
+  if (wave < 4) {
+    put(wave, 8, gacc[4]);
+    // lane l holds feature (l & 31) of row tile `wave` (two lane halves: samples 8 (l >> 5) ..)
+    const float bsum = gdb + __shfl_xor(gdb, 32, 64);
+    float* o = base + ((int64_t)wave * (NT + 1) + NT) * 1024;
+    if (lane < 32) {
+      const int m = lane;
+      o[(32 * ((m >> 2) & 1)) * 16 + (m & 3) + 4 * (m >> 3)] = bsum;
+    }
+  }
+}
+
+}  // namespace den

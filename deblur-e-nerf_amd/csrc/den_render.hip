@@ -251,11 +251,15 @@ __device__ __forceinline__ int fwd_slot(int slot0, int gc) {
   return s >= FWD_RING ? s - FWD_RING : s;
 }
 
-template <int MODE, int LAST_J>
+// WRAP (persistent kernels): past the last chunk the stream wraps to chunk 0, the next item's
+template <int MODE, int LAST_J, bool WRAP = false>
 __device__ __forceinline__ void bwd_next(int j, int i, int64_t* off, int* bytes) {
   int nj = j, ni = i + 1;
   if (ni >= bwd_tiles(MODE, j)) { nj = j + 1; ni = 0; }
-  if (nj > LAST_J) { *off = 0; *bytes = 0; return; }
+  if (nj > LAST_J) {
+    if (!WRAP) { *off = 0; *bytes = 0; return; }
+    nj = 0;
+  }
   *bytes = chunk_bytes_K(bwd_K(MODE, nj));
   *off = bwd_layer_offset(MODE, nj) + (int64_t)ni * *bytes;
 }
@@ -755,9 +759,11 @@ struct NoTileHook {
   template <typename Acc>
   __device__ __forceinline__ void operator()(int, const Acc&) const {}
 };
-template <int MODE, int LAST_J, int J, int KS, int DER, typename Frag, typename Hook = NoTileHook>
-__device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* lds, int64_t sample, const Frag* x,
-                                              Frag* xo, int SA, int DZ, Hook&& hook = Hook{}) {
+// DZ < 0: the dz tiles stay in registers only (xo), nothing is stored.
+template <int MODE, int LAST_J, int J, int KS, int DER, bool WRAP = false, typename AT, typename Frag,
+          typename Hook = NoTileHook>
+__device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sample, const Frag* x, Frag* xo, int SA,
+                                              int DZ, Hook&& hook = Hook{}) {
   using T = Tr<MODE>;
   using Acc = typename T::Acc;
   constexpr int NT = bwd_tiles(MODE, J);
@@ -775,12 +781,14 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
     acc_to_frags<MODE>(acc, xo + i * FPT);
   };
   // dz stores deferred to the start of the next chunk interval (see fwd_store)
-  auto store = [&](int i) { store_tile_frags<MODE>(act_ptr<MODE>(A, DZ, sample, i), xo + i * FPT); };
+  auto store = [&](int i) {
+    if (DZ >= 0) store_tile_frags<MODE>(act_ptr<MODE>(A, DZ, sample, i), xo + i * FPT);
+  };
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     int64_t noff;
     int nbytes;
-    bwd_next<MODE, LAST_J>(J, i, &noff, &nbytes);
+    bwd_next<MODE, LAST_J, WRAP>(J, i, &noff, &nbytes);
     if constexpr (DER == 0) s_cur = load_tile_vals<MODE>(act_ptr<MODE>(A, SA, sample, i));
     chunk_step(lds, A.w, cb + i, noff, nbytes, [&](const char* chunk) {
       if (i >= 2) store(i - 2);
@@ -809,26 +817,13 @@ __device__ __forceinline__ void bwd_layer_run(const RenderArgs<MODE>& A, char* l
 constexpr int LRW_SCR = 4096;  // bytes of LDS scratch per wave
 constexpr int LR_PART = 388;   // floats per workgroup partial: 4 x 3 x 32 + 3 bias + 1 pad
 
-template <int MODE, int LAST_J>
-// Page-aligned code, as every hot kernel here: the same render_bwd instructions ran 0.1-0.3 ms
-// apart at different code addresses (r04u / r04w / r04y same-box A/B, profiles/r04{w,y}_ab.json)
-__attribute__((aligned(4096)))
-__global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) {
-  using T = Tr<MODE>;
-  using Frag = typename T::Frag;
-  using Acc = typename T::Acc;
-  constexpr int TM = T::TM, FPT = T::FPT, REGS = T::REGS;
+// ---- compositing adjoint of one item (WGS samples = whole rays), one wave per ray -> the per-sample
+// raw-output gradients {d sigma_raw, d rgb_raw} in rec_lds (points: the per-point upstream gradients)
+template <int MODE, typename AT>
+__device__ __forceinline__ void head_adjoint(const AT& A, float* rec_lds, int64_t item, int64_t sample, int wave,
+                                             int lane, int c, int grp) {
+  constexpr int TM = Tr<MODE>::TM;
   constexpr int WGS = wg_samples(MODE);
-  constexpr bool FUSE_LR = MODE == 1 && LAST_J == 1;
-  __shared__ __attribute__((aligned(16))) char lds[2 * LDS_BUF + WGS * 16 + (FUSE_LR ? 8 * LRW_SCR : 0)];
-  float* rec_lds = (float*)(lds + 2 * LDS_BUF);
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane % TM, grp = lane / TM;
-  const int64_t sample = (int64_t)blockIdx.x * WGS + wave * TM + c;
-
-  dma_chunk(A.w, lds, chunk_bytes_K(bwd_K(MODE, 0)));
-
   // ---- compositing adjoint, one wave per ray
   const int rays_per_wg = WGS / A.n_samples;
   if (A.points) {
@@ -845,14 +840,17 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
       *(f32x4*)(rec_lds + (wave * TM + c) * 4) = o4;
     }
   } else if (wave < rays_per_wg) {
-    const int64_t r = (int64_t)blockIdx.x * rays_per_wg + wave;
+    const int64_t r = item * rays_per_wg + wave;
     float ro[3], rdv[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       ro[a] = A.rays_o[r * 3 + a];
       rdv[a] = A.rays_d[r * 3 + a];
     }
-    RayGeom rg = ray_geom(ro, rdv, A.aabb, A.near_p, A.far_p);
+    float aabb[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) aabb[q] = A.aabb[q];
+    RayGeom rg = ray_geom(ro, rdv, aabb, A.near_p, A.far_p);
     const float ru = A.jitter[r];
     const int spl = A.n_samples / 64;
     float dC[3] = {0.f, 0.f, 0.f};
@@ -944,6 +942,30 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
         A.bkgd_partial[(int64_t)ch * A.n_rays + r] = (ch < A.rd && A.has_bkgd) ? dC[ch] * (1.0f - opacity) : 0.0f;
     }
   }
+}
+
+template <int MODE, int LAST_J>
+// Page-aligned code, as every hot kernel here: the same render_bwd instructions ran 0.1-0.3 ms
+// apart at different code addresses (r04u / r04w / r04y same-box A/B, profiles/r04{w,y}_ab.json)
+__attribute__((aligned(4096)))
+__global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) {
+  using T = Tr<MODE>;
+  using Frag = typename T::Frag;
+  using Acc = typename T::Acc;
+  constexpr int TM = T::TM, FPT = T::FPT, REGS = T::REGS;
+  constexpr int WGS = wg_samples(MODE);
+  constexpr bool FUSE_LR = MODE == 1 && LAST_J == 1;
+  __shared__ __attribute__((aligned(16))) char lds[2 * LDS_BUF + WGS * 16 + (FUSE_LR ? 8 * LRW_SCR : 0)];
+  float* rec_lds = (float*)(lds + 2 * LDS_BUF);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane % TM, grp = lane / TM;
+  const int64_t sample = (int64_t)blockIdx.x * WGS + wave * TM + c;
+
+  dma_chunk(A.w, lds, chunk_bytes_K(bwd_K(MODE, 0)));
+
+  // ---- compositing adjoint, one wave per ray
+  head_adjoint<MODE>(A, rec_lds, blockIdx.x, sample, wave, lane, c, grp);
   __syncthreads();
 
   // ---- fake dz tiles from the per-sample raw gradients
