@@ -116,8 +116,9 @@ WsLayout ws_layout(const den_render_desc* d) {
     L.act[a] = off;
     // pe / ve: kept by the F32 forward only; the BF16 layer-major backward recomputes them (the
     // sample-major BF16 path writes them itself, enc_store_kernel)
-    // dz_g: kept in registers by the BF16 head backward (render_head_bwd_kernel, the fused Lg weight gradient)
-    const bool enc = a == A_PE || a == A_VE || a == D_ZG;
+    // dz_g: kept on chip by the BF16 head backward (render_head_bwd_kernel, the fused Lg weight
+    // gradient) unless den_render_ray_grad will read it
+    const bool enc = a == A_PE || a == A_VE || (a == D_ZG && !d->ray_grad);
     if (d->train && !(enc && use_hidden_path(d))) off += align256((size_t)n * act_width(d->mode, a) * es);
   }
   L.rec = off;
@@ -201,6 +202,7 @@ RenderArgs<MODE> make_args(const den_render_desc* d, const den_render_io* io, co
   A.out_opacity = io->out_opacity;
   A.out_depth = io->out_depth;
   A.density_act = d->density_activation;
+  A.keep_dzg = d->ray_grad;
   return A;
 }
 
@@ -637,6 +639,9 @@ int den_render_ray_grad(const den_render_desc* d, const den_render_io* io, const
   int rc = check_desc(d);
   if (rc) return rc;
   if (!d->train) return fail(DEN_EINVAL, "den_render_ray_grad needs a train=1 forward and its den_render_bwd");
+  if (use_hidden_path(d) && !d->ray_grad)
+    return fail(DEN_EINVAL, "den_render_ray_grad needs desc.ray_grad = 1 on the forward and backward (BF16 keeps "
+                            "dz_g only then)");
   if (!io || !io->workspace || !io->rays_o || !io->rays_d || !params || !rg_workspace || !d_rays_o || !d_rays_d ||
       (d->points == 0 && !io->jitter) || (d->points == 2 && (!io->ray_indices || !io->t_starts || !io->t_ends)))
     return fail(DEN_EINVAL, "null pointer");

@@ -129,8 +129,9 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     Frag fr[FPT];
     acc_to_frags<MODE>(dzr, fr);
     Frag xa[KS + 2 * FPT], xb[KS + 2 * FPT];
-    // j=0 Lr^T: dz_r -> dz_g in registers only (xa, 4 tiles) + the fused Lr weight gradient
-    bwd_layer_run<MODE, 1, 0, FPT, 0, true>(A, lds, sample, fr, xa, A_G, -1, lr_hook);
+    // j=0 Lr^T: dz_r -> dz_g in registers (xa, 4 tiles; stored only for den_render_ray_grad) + the
+    // fused Lr weight gradient
+    bwd_layer_run<MODE, 1, 0, FPT, 0, true>(A, lds, sample, fr, xa, A_G, A.keep_dzg ? D_ZG : -1, lr_hook);
     // dz_g into this wave's staging area (its Lr scratch, done with): 4 tiles, the DMA'd-tile layout
 #pragma unroll
     for (int t = 0; t < WIDTH_COND / TM; ++t) {

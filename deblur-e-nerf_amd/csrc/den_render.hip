@@ -53,6 +53,7 @@ struct RenderArgs {
   float* lr_partial;      // [workgroup][LR_PART]: the fused Lr weight gradient (render_bwd_kernel, LAST_J = 1)
   int64_t n_items;        // forward: 256-sample (BF16) / 128-sample (F32) blocks, walked by a persistent grid
   int density_act;        // den_render_desc.density_activation
+  int keep_dzg;           // den_render_desc.ray_grad: the BF16 head backward also stores dz_g (D_ZG)
 };
 
 // ------------------------------------------------------------------ helpers

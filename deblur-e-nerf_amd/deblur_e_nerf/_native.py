@@ -28,7 +28,7 @@ class RenderDesc(ctypes.Structure):
                 ("n_samples", ctypes.c_int32), ("aabb", ctypes.c_float * 6), ("near_plane", ctypes.c_float),
                 ("far_plane", ctypes.c_float), ("train", ctypes.c_int32), ("has_bkgd", ctypes.c_int32),
                 ("points", ctypes.c_int32), ("contraction", ctypes.c_int32), ("bwd_path", ctypes.c_int32),
-                ("density_activation", ctypes.c_int32)]
+                ("density_activation", ctypes.c_int32), ("ray_grad", ctypes.c_int32)]
 
 
 class RenderIO(ctypes.Structure):
@@ -248,7 +248,7 @@ class PackedWeights:
 
 
 # ----------------------------------------------------------------------------- render
-def _desc(cfg, n_rays, n_samples, train, has_bkgd, points=0):
+def _desc(cfg, n_rays, n_samples, train, has_bkgd, points=0, ray_grad=False):
     d = RenderDesc()
     d.mode = cfg["mode"]
     d.radiance_dim = cfg["rd"]
@@ -264,6 +264,7 @@ def _desc(cfg, n_rays, n_samples, train, has_bkgd, points=0):
     d.contraction = int(cfg.get("contraction", 0))
     d.bwd_path = int(cfg.get("bwd_path", 0))
     d.density_activation = int(cfg.get("density", 0))
+    d.ray_grad = int(bool(ray_grad))
     return d
 
 
@@ -301,7 +302,9 @@ class RenderFunction(torch.autograd.Function):
         train = (train or ctx.needs_input_grad[4] or (bkgd is not None and ctx.needs_input_grad[3])
                  or ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
         R = samples[0].numel() if points == 2 else rays_o.shape[0]
-        desc = _desc(cfg, R if not points else R // n_samples, n_samples, train, bkgd is not None, points)
+        # the rays' own gradient (den_render_ray_grad) follows the backward when they require grad
+        ray_grad = bool(ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
+        desc = _desc(cfg, R if not points else R // n_samples, n_samples, train, bkgd is not None, points, ray_grad)
         ws = torch.empty(render_workspace_bytes(desc), dtype=torch.uint8, device=rays_o.device)
         out_rgb = torch.empty(R, rd, dtype=torch.float32, device=rays_o.device)
         out_op = torch.empty(R, dtype=torch.float32, device=rays_o.device)

@@ -576,19 +576,29 @@ def evaluation_correction(pred_intensity_img, target_intensity_img, gain_exposur
                     converged=(conv["scale"], conv["gamma"], conv["offset"]))
 
 
+def flat_gradient_buffers(grads):
+    """The gradients grouped by dtype for the all-reduce: {dtype: (flat buffer, [gradients])} -- one
+    f32 buffer for the f32 parameters (the MLP / hash table) and one f64 buffer for the f64 ones (the
+    refractory period, event_generation_params.py:196-201), so no f32 gradient travels as f64."""
+    groups = {}
+    for g in grads:
+        groups.setdefault(g.dtype, []).append(g)
+    return {dt: (torch.cat([g.reshape(-1) for g in gs]), gs) for dt, gs in groups.items()}
+
+
 def allreduce_gradients(module):
     """DDP gradient semantics over the ranks of the default process group: the mean of each
-    gradient, as one all-reduce of one flat buffer (RCCL over xGMI on the GPU box)."""
+    gradient, as one all-reduce per dtype of one flat buffer (RCCL over xGMI on the GPU box)."""
     if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
         return
     grads = [p.grad for p in module.parameters() if p.grad is not None]
     if not grads:
         return
-    flat = torch.cat([g.reshape(-1).to(torch.float64 if g.dtype == torch.float64 else torch.float32) for g in grads])
-    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
-    flat.div_(dist.get_world_size())
-    off = 0
-    for g in grads:
-        n = g.numel()
-        g.copy_(flat[off:off + n].view_as(g))
-        off += n
+    for flat, gs in flat_gradient_buffers(grads).values():
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        flat.div_(dist.get_world_size())
+        off = 0
+        for g in gs:
+            n = g.numel()
+            g.copy_(flat[off:off + n].view_as(g))
+            off += n

@@ -67,7 +67,7 @@ extern "C" {
 #endif
 
 #define DEN_VERSION 5  /* 5: den_queue_raw_events / den_max_refractory_period / den_colorize_events /
-                          den_undistort_events;
+                          den_undistort_events; den_render_desc.ray_grad;
                           4: density_activation in den_render_desc / den_ngp_desc; den_sh_encode_* */
 
 enum den_status {
@@ -123,6 +123,9 @@ typedef struct den_render_desc {
   int32_t density_activation; /* models/nerf.py:20-29: 0 shifted_trunc_exp (exp(x - 1), gradient
                               clamped at exp(15), external/ngp.py:45-61), 1 softplus(beta 1,
                               threshold 20), 2 shifted_softplus (softplus(x - 1)) */
+  int32_t ray_grad;        /* 1: den_render_ray_grad follows the backward (the gradient into the rays,
+                              the refractory period's pose path): the BF16 layer-major backward then
+                              keeps dz_g in the workspace for it (otherwise dz_g never leaves the chip) */
 } den_render_desc;
 
 /* Device buffers of one render call. */

@@ -179,9 +179,12 @@ def test_occupancy_grid_sync_broadcasts_rank0_after_updates():
 
 class _FitStub(torch.nn.Module):
     """The attributes DeblurENeRF.fit_step reads, around the product's fit_step / sync_grid /
-    allreduce_gradients: a training_step that updates the occupancy grid on the first micro-batch
-    of each accumulation group with per-rank draws (deblur_e_nerf.py:465; den_occ_update's effect)
-    and records the grid each micro-batch marches with."""
+    allreduce_gradients: a training_step that updates the occupancy grid with per-rank draws whenever
+    global_step % UPDATE_EVERY == 0 -- on EVERY micro-batch of such a group, as the reference's
+    update_occ_grid(step=global_step) does (global_step only advances per optimizer step,
+    deblur_e_nerf.py:465; den_occ_update's effect) -- and records the grid each micro-batch marches
+    with and the global step it ran at."""
+    UPDATE_EVERY = 2
 
     def __init__(self, rank, acc):
         super().__init__()
@@ -197,11 +200,11 @@ class _FitStub(torch.nn.Module):
     def training_step(self, batch, batch_index):
         grid = self.nerf.occupancy_grid
         before = grid.occs.clone()
-        if batch_index % self.trainer.accumulate_grad_batches == 0:
+        if self._global_step % self.UPDATE_EVERY == 0:
             grid.occs.copy_(torch.rand(grid.num_cells, generator=self.g))
             grid._binary.copy_((grid.occs > 0.5).reshape(grid._binary.shape))
             grid._dirty = True
-        self.seen.append((before, grid.occs.clone()))
+        self.seen.append((before, grid.occs.clone(), self._global_step))
         return (self.w * batch).sum()
 
 
@@ -229,26 +232,34 @@ def _fit_worker(rank, world, port, out, acc, n_micro):
 def test_fit_step_grid_broadcast_per_accumulation_group(acc):
     """DDP + PL accumulation (run.py:84-100, 07_ziggy_and_fuzz_hdr.yaml accumulate_grad_batches):
     rank 0's grid is broadcast only before the first micro-batch of a group (the only forward
-    after a synced one), before that micro-batch's rank-local grid update; micro-batches 1..acc-1
-    march with each rank's own updated grid; the averaged gradient is applied once per group and
-    leaves identical parameters on every rank."""
-    n_micro = 2 * acc + 1
+    after a synced one), before that micro-batch's rank-local grid update; every micro-batch of an
+    updating group (global_step % n == 0) updates the grid again, so micro-batches 1..acc-1 march
+    with the rank's own grid after its second, third ... update; the averaged gradient is applied
+    once per group and leaves identical parameters on every rank."""
+    n_micro = 4 * acc + 1
     port = _free_port()
     out = mp.Manager().dict()
     mp.spawn(_fit_worker, args=(WORLD, port, out, acc, n_micro), nprocs=WORLD, join=True)
     (seen0, p0), (seen1, p1) = out[0], out[1]
+    repeated = 0
     for i in range(n_micro):
-        (b0, a0), (b1, a1) = seen0[i], seen1[i]
+        (b0, a0, gs0), (b1, a1, gs1) = seen0[i], seen1[i]
+        assert gs0 == gs1 == i // acc, (i, gs0, gs1)
+        updating = gs0 % _FitStub.UPDATE_EVERY == 0
         if i % acc == 0:
             # the pre-update grid is rank 0's on every rank (the broadcast), then each rank updates its own
             assert torch.equal(b0, b1), i
             if i > 0:  # rank 0's grid of the previous group's last micro-batch
                 assert torch.equal(b1, seen0[i - 1][1]), i
-            assert not torch.equal(a0, a1), i
-        else:  # no broadcast inside a group: each rank keeps its own freshly updated grid
-            assert torch.equal(b0, a0) and torch.equal(b1, a1), i
-            assert not torch.equal(a0, a1), i
-            assert torch.equal(a1, seen1[i - 1][1]), i
+        else:  # no broadcast inside a group: each rank marches with its own grid of the last micro-batch
+            assert torch.equal(b0, seen0[i - 1][1]) and torch.equal(b1, seen1[i - 1][1]), i
+            repeated += updating
+        if updating:  # a fresh per-rank update on every micro-batch of the group
+            assert not torch.equal(a0, b0) and not torch.equal(a1, b1) and not torch.equal(a0, a1), i
+        else:
+            assert torch.equal(a0, b0) and torch.equal(a1, b1), i
+    assert repeated == (acc - 1) * len({i // acc for i in range(n_micro) if (i // acc) % _FitStub.UPDATE_EVERY == 0
+                                        and i % acc})  or acc == 1
     for i in range(n_micro):
         assert torch.equal(p0[i], p1[i]), i
         if (i + 1) % acc == 0:  # SGD lr 1 on the rank-mean of the group's summed (loss / acc) gradients
@@ -258,3 +269,49 @@ def test_fit_step_grid_broadcast_per_accumulation_group(acc):
             assert torch.allclose(p0[i], prev - g * torch.tensor([1.0, 2.0, 3.0])), i
         elif i > 0:
             assert torch.equal(p0[i], p0[i - 1]), i
+
+
+class _MixedGrads(torch.nn.Module):
+    """f32 parameters (the MLP / hash table) beside an f64 one (tau_r, event_generation_params.py:196-201)."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Parameter(torch.zeros(1000))
+        self.tau = torch.nn.Parameter(torch.zeros((), dtype=torch.float64))
+        self.b = torch.nn.Parameter(torch.zeros(3, 7))
+
+
+def _mixed_worker(rank, world, port, out):
+    import sys
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deblur_e_nerf.models.deblur_e_nerf import allreduce_gradients, flat_gradient_buffers
+    m = _MixedGrads()
+    m.a.grad = torch.full((1000,), float(rank + 1))
+    m.tau.grad = torch.tensor(1e-9 * (rank + 1) + 1.0, dtype=torch.float64)
+    m.b.grad = torch.full((3, 7), 3.0 * (rank + 1))
+    bufs = flat_gradient_buffers([p.grad for p in m.parameters()])
+    allreduce_gradients(m)
+    out[rank] = ({str(dt): (b.dtype, b.numel()) for dt, (b, _) in bufs.items()}, m.a.grad.clone(), m.tau.grad.clone(),
+                 m.b.grad.clone())
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_allreduce_gradients_keeps_f32_and_f64_apart():
+    """allreduce_gradients (deblur_e_nerf.py's DDP step): one f32 buffer for the f32 gradients and one
+    f64 buffer for tau_r's -- the f32 gradients never travel promoted to f64 -- and the result is
+    each gradient's rank mean, in its own dtype (the f64 one exact to f64)."""
+    port = _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_mixed_worker, args=(WORLD, port, out), nprocs=WORLD, join=True)
+    for r in range(WORLD):
+        bufs, ga, gt, gb = out[r]
+        assert bufs == {"torch.float32": (torch.float32, 1000 + 21), "torch.float64": (torch.float64, 1)}, bufs
+        assert ga.dtype == torch.float32 and torch.equal(ga, torch.full((1000,), 1.5))
+        assert gb.dtype == torch.float32 and torch.equal(gb, torch.full((3, 7), 4.5))
+        assert gt.dtype == torch.float64 and float(gt) == (1.0 + 1e-9 + 1.0 + 2e-9) / 2
