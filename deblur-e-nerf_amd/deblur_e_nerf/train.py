@@ -286,11 +286,11 @@ class PixbwTrainStep:
     4 S N per step; the pixel-bandwidth filter turns them into log-intensities
     (den_pixbw_*), then the Huber diff + L1 TV losses, backward, all-reduce, Adam.
 
-    Device ops: den_event_prep, den_pixbw_sample_ts, den_pixel_rays,
+    Device ops: den_event_prep, den_pixbw_sample_ts, den_trajectory (the camera pose at every
+    sample timestamp: LinearTrajectory.forward, trajectories.py:30-90), den_pixel_rays,
     den_render_fwd/bwd, den_pixbw_fwd/bwd, den_event_loss_fwd/bwd, den_adam_step,
-    den_pack_weights, chained by torch.autograd.  The camera trajectory
-    (trajectories.py, SURVEY.md 8(f) #2, not built) is replaced by a synthetic
-    constant-velocity pose per event, evaluated elementwise in torch.
+    den_pack_weights, chained by torch.autograd -- the reference step's front end
+    (render_train_pixels: trajectory -> pixel_params_to_ray -> render).
     """
 
     def __init__(self, n_events, it_sample_size=16, n_samples=128, radiance_dim=1, mode="bf16", seed=0,
@@ -327,31 +327,34 @@ class PixbwTrainStep:
         self.loss = torch.zeros(3, device=self.dev)
 
     def load_events(self, num_pos, num_neg, end_ts, start_ts, normalized, interval_gen, position, T_wc_position,
-                    velocity, T_wc_orientation, intrinsics_inverse, jitter, channel=None):
+                    T_wc_orientation, T_wc_timestamp, intrinsics_inverse, jitter, channel=None):
         """Raw events (see synthetic_pixbw_events): interval_gen (S-1, N) f64 is the
-        datamodule's normalized interval-generator sample (datamodule.py:199-211);
-        the pose of event i at time t is T_wc_position[i] + velocity[i] (t - end_ts[i]) 1e-9,
-        orientation T_wc_orientation[i]; jitter (4, S N)."""
+        datamodule's normalized interval-generator sample (datamodule.py:199-211); the camera
+        trajectory is the pose samples T_wc_position (C, 3), T_wc_orientation (C, 4) XYZW,
+        T_wc_timestamp (C) ns (camera_poses.npz), looked up per sample timestamp by the
+        LinearTrajectory mirror (den_trajectory); jitter (4, S N)."""
+        from .data.datasets import CameraPose
+        from .models.trajectories import LinearTrajectory
         d = self.dev
         i64 = lambda t: t.to(d, torch.int64).contiguous()
         f32 = lambda t: t.to(d, torch.float32).contiguous()
         self.ev = dict(num_pos=i64(num_pos), num_neg=i64(num_neg), end_ts=i64(end_ts), start_ts=i64(start_ts))
         self.norm = normalized.to(d, torch.float64).contiguous()
         self.gen = interval_gen.to(d, torch.float64).contiguous()
-        self.position, self.p0, self.vel = f32(position), f32(T_wc_position), f32(velocity)
-        self.rot = f32(T_wc_orientation)[None].expand(self.S, self.N, 3, 3).contiguous()
+        self.position = f32(position)
+        self.traj = LinearTrajectory(CameraPose.from_arrays(f32(T_wc_position), f32(T_wc_orientation),
+                                                            i64(T_wc_timestamp))).to(d)
         self.K_inv = f32(intrinsics_inverse)
         self.jitter = f32(jitter).reshape(4, self.S * self.N)
         self.channel = None if channel is None else i64(channel)
-        self.t_ref = self.ev["end_ts"].to(torch.float64)
 
     def _intensity_fn(self, g, bkgd):
         S, N = self.S, self.N
 
         def fn(ts):  # (S, N) f64 clamped sample timestamps -> intensity (S, N) (render_train_pixels)
-            with torch.no_grad():
-                pos = (self.p0 + self.vel * ((ts - self.t_ref) * 1e-9).float()[..., None]).contiguous()
-                o, dr = nat.pixel_rays(self.K_inv, self.position, pos, self.rot)
+            with torch.no_grad():  # (the pose path carries no gradient here: tau_r is frozen)
+                pos, rot = self.traj(ts)
+                o, dr = nat.pixel_rays(self.K_inv, self.position, pos.contiguous(), rot.contiguous())
             rgb, op, _ = nat.render(o.reshape(-1, 3), dr.reshape(-1, 3), self.jitter[g], bkgd, self.flat,
                                     self.cfg, self.packed, self.n_samples)
             if self.rd > 1:  # bayering (deblur_e_nerf.py:1223-1235)
@@ -399,22 +402,62 @@ class PixbwTrainStep:
         return self.loss
 
 
+def rotmat_to_quat_xyzw(R):
+    """(..., 3, 3) rotation matrices -> (..., 4) unit quaternions in RoMa's XYZW order (Shepperd's
+    method, the largest of the four candidate pivots); synthetic pose data only."""
+    m = R
+    tr = m[..., 0, 0] + m[..., 1, 1] + m[..., 2, 2]
+    cands = torch.stack([tr, m[..., 0, 0], m[..., 1, 1], m[..., 2, 2]], dim=-1)
+    k = cands.argmax(dim=-1)
+    s0 = torch.sqrt((1 + tr).clamp_min(1e-12)) * 2
+    s1 = torch.sqrt((1 + m[..., 0, 0] - m[..., 1, 1] - m[..., 2, 2]).clamp_min(1e-12)) * 2
+    s2 = torch.sqrt((1 + m[..., 1, 1] - m[..., 0, 0] - m[..., 2, 2]).clamp_min(1e-12)) * 2
+    s3 = torch.sqrt((1 + m[..., 2, 2] - m[..., 0, 0] - m[..., 1, 1]).clamp_min(1e-12)) * 2
+    q0 = torch.stack([(m[..., 2, 1] - m[..., 1, 2]) / s0, (m[..., 0, 2] - m[..., 2, 0]) / s0,
+                      (m[..., 1, 0] - m[..., 0, 1]) / s0, s0 / 4], -1)
+    q1 = torch.stack([s1 / 4, (m[..., 0, 1] + m[..., 1, 0]) / s1, (m[..., 0, 2] + m[..., 2, 0]) / s1,
+                      (m[..., 2, 1] - m[..., 1, 2]) / s1], -1)
+    q2 = torch.stack([(m[..., 0, 1] + m[..., 1, 0]) / s2, s2 / 4, (m[..., 1, 2] + m[..., 2, 1]) / s2,
+                      (m[..., 0, 2] - m[..., 2, 0]) / s2], -1)
+    q3 = torch.stack([(m[..., 0, 2] + m[..., 2, 0]) / s3, (m[..., 1, 2] + m[..., 2, 1]) / s3, s3 / 4,
+                      (m[..., 1, 0] - m[..., 0, 1]) / s3], -1)
+    q = torch.where((k == 0)[..., None], q0, torch.where((k == 1)[..., None], q1, torch.where((k == 2)[..., None], q2, q3)))
+    return q / q.norm(dim=-1, keepdim=True)
+
+
+def synthetic_trajectory(speed=5.0, radius=4.03, n_poses=401, t_end=1.2e9, seed=7):
+    """A camera_poses.npz-shaped trajectory: the camera orbits the AABB centre at `radius` with
+    `speed` units/s and a slow elevation swing, looking at the origin (x right, y down); pose
+    samples every t_end / (n_poses - 1) ns -> T_wc_position (C, 3) f32, T_wc_orientation (C, 4)
+    XYZW f32, T_wc_timestamp (C) i64."""
+    g = torch.Generator().manual_seed(seed)
+    phase = float(torch.rand(1, generator=g)) * 2 * math.pi
+    t = torch.linspace(0.0, t_end, n_poses, dtype=torch.float64)
+    theta = phase + speed / radius * t * 1e-9
+    elev = 0.35 + 0.25 * torch.sin(0.37 * t * 1e-9 + phase)
+    c = torch.stack([torch.cos(theta) * torch.cos(elev), torch.sin(theta) * torch.cos(elev), torch.sin(elev)], -1)
+    c = (c * radius).float()
+    rot = _look_at(c, -c)
+    return dict(T_wc_position=c.contiguous(), T_wc_orientation=rotmat_to_quat_xyzw(rot).float().contiguous(),
+                T_wc_timestamp=t.round().long())
+
+
 def synthetic_pixbw_events(n_events, it_sample_size=16, seed=1234, rank=0, world=1, speed=5.0):
-    """synthetic_events plus the pixel-bandwidth inputs: the (S-1, N) interval
-    generator sample (Triangular(0,1) about 0.5, datamodule.py:199-211) and a
-    per-event camera velocity (units/s) for the constant-velocity trajectory;
-    jitter covers the 4 x S x N rays."""
+    """synthetic_events plus the pixel-bandwidth inputs: the (S-1, N) interval generator sample
+    (Triangular(0,1) about 0.5, datamodule.py:199-211) and ONE camera trajectory for all events
+    (synthetic_trajectory: camera_poses.npz's arrays; the pose of each sample timestamp comes from
+    it, as render_train_pixels looks it up); jitter covers the 4 x S x N rays.  Every rank holds the
+    same trajectory and its shard of the events."""
     S = it_sample_size
     b = synthetic_events(n_events, seed=seed, rank=rank, world=world)
     g = torch.Generator().manual_seed(seed + 1)
     Nt = n_events * world
     u = torch.rand(S - 1, Nt, generator=g, dtype=torch.float64)
     gen = torch.where(u < 0.5, torch.sqrt(u / 2), 1 - torch.sqrt((1 - u) / 2))
-    vel = torch.randn(Nt, 3, generator=g) * speed  # units / s
     jit = torch.rand(4, S, Nt, generator=g)
     sl = slice(rank * n_events, (rank + 1) * n_events)
-    b.pop("jitter")
-    b["T_wc_position"] = b["T_wc_position"][0].contiguous()   # the pose at end_ts
-    b["T_wc_orientation"] = b["T_wc_orientation"][0].contiguous()
-    b.update(interval_gen=gen[:, sl].contiguous(), velocity=vel[sl], jitter=jit[:, :, sl].reshape(4, -1).contiguous())
+    for k in ("jitter", "T_wc_position", "T_wc_orientation"):
+        b.pop(k)
+    b.update(interval_gen=gen[:, sl].contiguous(), jitter=jit[:, :, sl].reshape(4, -1).contiguous(),
+             **synthetic_trajectory(speed=speed, seed=seed + 2))
     return b

@@ -72,7 +72,7 @@ def pixbw_step_loss(p, bkgd, raw, it_sample_size, n_samples, prm, min_ts, w=(1.0
                     fn=("huber", "l1"), dt_dtype=torch.float32):
     """The pixel-bandwidth-on step (deblur_e_nerf.train.PixbwTrainStep layout):
     event preparation, then for each supervision timestamp group the S sample
-    timestamps, the constant-velocity poses, rays, renders and the pixel-bandwidth
+    timestamps, the trajectory's poses (oracle/trajectory.py), rays, renders and the pixel-bandwidth
     filter (oracle/pixbw.py, reset on the diff start), then the losses
     (deblur_e_nerf.py:472-549 with render_log_intensity :1137-1151)."""
     from . import events as oev
@@ -86,13 +86,14 @@ def pixbw_step_loss(p, bkgd, raw, it_sample_size, n_samples, prm, min_ts, w=(1.0
     grad = o["lid"] / (raw["end_ts"] - o["start_ts"])
     target = (ts_diff * grad / c).to(torch.float32)
     orc = opb.PixelBandwidthOracle(prm, min_ts, dt_dtype=dt_dtype)
-    t_ref = raw["end_ts"].to(torch.float64)
-    rot = raw["T_wc_orientation"][None].expand(S, N, 3, 3)
+    from . import trajectory as otraj
     jit = raw["jitter"].reshape(4, S * N)
     ys = []
     for g, tg in enumerate((d_s, d_e, s_s, s_e)):
         def intensity(ts, g=g):
-            pos = raw["T_wc_position"] + raw["velocity"] * ((ts - t_ref) * 1e-9).float()[..., None]
+            with torch.no_grad():  # tau_r frozen: no gradient through the poses
+                pos, rot = otraj.linear_trajectory(raw["T_wc_timestamp"], raw["T_wc_position"].float(),
+                                                   raw["T_wc_orientation"].float(), ts.detach())
             ro, rdir = oev.pixel_params_to_ray(raw["intrinsics_inverse"], raw["position"], pos, rot)
             col, _, _, _ = onerf.render_rays(p, ro.reshape(-1, 3).to(bkgd.dtype), rdir.reshape(-1, 3).to(bkgd.dtype),
                                              jit[g].to(bkgd.dtype), n_samples=n_samples, bkgd=bkgd)

@@ -124,13 +124,15 @@ def test_allreduce_mean_equals_full_batch_gradient(raw):
 
 def test_pixbw_event_sharding_partitions_the_global_batch():
     """synthetic_pixbw_events shards whole events, including the interval
-    generators, velocities and the 4 x S x N jitter."""
+    generators and the 4 x S x N jitter; every rank holds the whole camera trajectory."""
     from deblur_e_nerf.train import synthetic_pixbw_events
     S = 4
     full = synthetic_pixbw_events(N_PER_RANK * WORLD, S)
     parts = [synthetic_pixbw_events(N_PER_RANK, S, rank=r, world=WORLD) for r in range(WORLD)]
-    for k in ("num_pos", "end_ts", "start_ts", "position", "T_wc_position", "velocity", "T_wc_orientation"):
+    for k in ("num_pos", "end_ts", "start_ts", "position"):
         assert torch.equal(torch.cat([p[k] for p in parts]), full[k]), k
+    for k in ("T_wc_position", "T_wc_orientation", "T_wc_timestamp"):
+        assert all(torch.equal(p[k], full[k]) for p in parts), k
     for k in ("normalized", "interval_gen"):
         assert torch.equal(torch.cat([p[k] for p in parts], dim=1), full[k]), k
     j = torch.cat([p["jitter"].reshape(4, S, N_PER_RANK) for p in parts], dim=2)
