@@ -474,10 +474,17 @@ def _affine_log_fit(pred_intensity_img, target_intensity_img, gain_exposure_prod
     if target.dim() == 3:  # (B, H, W): grayscale -> a channel dim of 1 (:722-725)
         pred, target = pred.unsqueeze(1), target.unsqueeze(1)
     B, C, H, W = target.shape
-    gep = torch.ones(B, dtype=torch.float64) if gain_exposure_prod is None else \
-        torch.as_tensor(gain_exposure_prod, dtype=torch.float64).reshape(B)
-    nge = gep / gep.mean()
-    log_gep = nge.log().view(B, 1, 1, 1).to(target.dtype)
+    # the gain-exposure normalisation in the product's own dtype (deblur_e_nerf.py:707-711, 737), f64
+    # only where the reference casts (OffsetGammaCorrection's const_scale, :854)
+    if gain_exposure_prod is None:
+        gep = torch.ones(B, dtype=torch.get_default_dtype())
+    else:
+        gep = torch.as_tensor(gain_exposure_prod).detach().cpu().reshape(B)
+        if not gep.is_floating_point():
+            gep = gep.to(torch.get_default_dtype())
+    nge_in = gep / gep.mean()
+    log_gep = nge_in.log().view(B, 1, 1, 1)
+    nge = nge_in.to(torch.float64)
     # logs in the images' dtype, f64 only for the least squares (the reference's order, :729-792)
     plog = pred.log().to(torch.float64)
     tlog = (target.log() - log_gep).to(torch.float64)

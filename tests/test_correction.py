@@ -93,6 +93,30 @@ def _scipy_refine(res_pred, target, nge, x0):
     return least_squares(f, x0, method="lm", xtol=1e-15, ftol=1e-15, gtol=1e-15, max_nfev=10000).x
 
 
+def test_gain_exposure_normalisation_in_its_own_dtype():
+    """deblur_e_nerf.py:707-739 with an f32, non-constant gain-exposure product: normalised and its
+    log taken in f32, subtracted from the f32 target logs, and only then cast to f64 for the least
+    squares -- the corrected image equals that restatement bit for bit (an f64 normalisation
+    differs at ~1e-7 relative)."""
+    g = torch.Generator().manual_seed(11)
+    target = torch.rand(3, 12, 14, generator=g) * 0.8 + 0.1
+    pred = (target * 1.3 + torch.rand(3, 12, 14, generator=g) * 0.05).clamp(0.01, 2)
+    gep = (torch.rand(3, generator=g) * 3 + 0.2).float() * torch.tensor(1 / 3.0)  # f32, not constant
+    corr, gamma, scale = affine_log_intensity_correction(pred, target, gain_exposure_prod=gep)
+    nge = gep.view(-1, 1, 1, 1) / gep.mean()                        # f32 (:709-711)
+    lg = nge.log()                                                  # f32 (:737)
+    plog = pred.unsqueeze(1).log().double()
+    tlog = (target.unsqueeze(1).log() - lg).double()                # f32 subtraction, then f64 (:738-792)
+    A = torch.nn.functional.pad(plog.unsqueeze(-1), (0, 1), value=1.0).transpose(0, 1).flatten(1, 3)
+    sol = torch.linalg.lstsq(A, tlog.unsqueeze(-1).transpose(0, 1).flatten(1, 3)).solution
+    want = ((A @ sol).view(1, 3, 12, 14).transpose(0, 1) + lg).exp()
+    assert torch.equal(corr, want)
+    assert float(gamma[0]) == float(sol[0, 0, 0])
+    # and the f64 normalisation is measurably different (so the test resolves the dtype)
+    lg64 = (gep.double() / gep.double().mean()).log().view(-1, 1, 1, 1)
+    assert not torch.equal(lg64.float(), lg) or not torch.equal((target.unsqueeze(1).log() - lg64).double(), tlog)
+
+
 @pytest.mark.parametrize("algo", ["lm", "gn"])
 def test_black_level_refinement_converges_to_least_squares(algo):
     pred, target, gep = _scene(7)
