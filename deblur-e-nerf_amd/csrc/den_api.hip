@@ -41,10 +41,22 @@ int fail(int code, const std::string& msg) {
     hipError_t e_ = (call);                                                                         \
     if (e_ != hipSuccess) return fail(DEN_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
   } while (0)
-#define DEN_LAUNCHED()                                                                    \
-  do {                                                                                    \
-    hipError_t e_ = hipGetLastError();                                                    \
-    if (e_ != hipSuccess) return fail(DEN_EHIP, std::string("launch: ") + hipGetErrorString(e_)); \
+// DEN_SYNC_CHECK=1 (debugging only; breaks stream capture): every launch is followed by a device
+// synchronisation, so an asynchronous fault is reported at the launch that caused it (source line)
+inline bool sync_check() {
+  static const bool on = [] {
+    const char* e = std::getenv("DEN_SYNC_CHECK");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+#define DEN_LAUNCHED()                                                                                  \
+  do {                                                                                                  \
+    hipError_t e_ = hipGetLastError();                                                                  \
+    if (e_ == hipSuccess && sync_check()) e_ = hipDeviceSynchronize();                                  \
+    if (e_ != hipSuccess)                                                                               \
+      return fail(DEN_EHIP, std::string("launch (den_api.hip:") + std::to_string(__LINE__) + "): " +   \
+                                hipGetErrorString(e_));                                                 \
   } while (0)
 
 // ---- kernel timing (measurement only; bench.py).  When enabled, each render-path launch is

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
   const int64_t b0 = (int64_t)blockIdx.x * P.per_wg;
   const int64_t b1 = b0 + P.per_wg < P.n_blocks ? b0 + P.per_wg : P.n_blocks;
 
-  auto fetch = [&](int64_t blk, char* dst) {
+  auto fetch = [&](int64_t blk, char* dst) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < (PIECES + NW - 1) / NW; ++q) {
       const int pc = __builtin_amdgcn_readfirstlane(q * NW + wave);

@@ -13,9 +13,8 @@
 //     (all 4 row tiles, k = the item's 256 samples): the bottleneck tile (block b, column w) of each
 //     of the item's 8 wave blocks arrives by untracked LDS-DMA in a private double buffer, both
 //     MFMA operands by transposed LDS reads;
-//   * the view encoding is a function of the ray alone (a wave block lies within one ray), so its
-//     B operand is computed in registers -- feature (lane & 31)'s value in all 8 k-slots -- and
-//     waves 0..3 own its four (row tile w, ve) output tiles plus the bias of row tile w;
+//   * each wave computes its block's view-encoding tile (enc_tile, as the forward) into LDS; waves
+//     0..3 own its four (row tile w, ve) output tiles plus the bias of row tile w;
 //   * the accumulators live in registers for the whole launch; each workgroup writes one split-K
 //     partial in den_dwstream.hip's layout [wg][4][10][64][16] (column 9: the bias), reduced in a
 //     fixed order by dw_reduce_kernel -- deterministic.
@@ -26,6 +25,7 @@ namespace den {
 
 constexpr int HD_STAGE = 8 * 4 * HB_TILE;  // dz_g of the item: 8 waves x 4 tiles (also each wave's Lr scratch)
 constexpr int HD_XBUF = 2 * HB_TILE;       // per wave: a double buffer of one bottleneck tile
+constexpr int HD_VE = 8 * HB_TILE;         // the item's view-encoding tiles, one per wave block
 
 // One bottleneck tile (2 KiB, two 1 KiB pieces) into this wave's private LDS buffer, untracked (the
 // waits are explicit); lane p fetches the tile lane whose fragment belongs in LDS slot p (hb_dma)
@@ -53,12 +53,15 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
   using Acc = typename T::Acc;
   constexpr int TM = T::TM, FPT = T::FPT;
   constexpr int WGS = wg_samples(MODE);
-  __shared__ __attribute__((aligned(16))) char lds[2 * LDS_BUF + WGS * 16 + HD_STAGE + 8 * HD_XBUF];
+  constexpr int LDS_BYTES = 2 * LDS_BUF + WGS * 16 + HD_STAGE + 8 * HD_XBUF + HD_VE;
+  static_assert(LDS_BYTES <= 160 * 1024, "the head kernel's LDS exceeds the CU's");
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   float* rec_lds = (float*)(lds + 2 * LDS_BUF);
   char* stage = lds + 2 * LDS_BUF + WGS * 16;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   char* xbuf = stage + HD_STAGE + wave * HD_XBUF;
   char* lscr = stage + wave * (4 * HB_TILE);  // this wave's Lr scratch = its own dz_g staging area
+  char* vet = stage + HD_STAGE + 8 * HD_XBUF;  // ve tiles of the item's 8 wave blocks
 
   // first item's weight chunk 0 (later items: wrapped in by the previous item's last chain step)
   dma_chunk(A0.w, lds, chunk_bytes_K(bwd_K(MODE, 0)));
@@ -138,6 +141,17 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       *(bf16x8*)(lscr + t * HB_TILE + hb_slot(lane, 0) * 16) = xa[t * FPT];
       *(bf16x8*)(lscr + t * HB_TILE + 1024 + hb_slot(lane, 1) * 16) = xa[t * FPT + 1];
     }
+    // this wave block's view-encoding tile (the Lg weight gradient's B operand for the ve columns),
+    // as the forward computes it: lane = sample c, lane group grp (enc_tile), then the DMA'd-tile
+    // layout; read by waves 0..3 after the chain's barriers
+    {
+      const int64_t ray = A.points == 0 ? sample / A.n_samples : A.points == 2 ? (int64_t)A.ray_idx[sample] : sample;
+      float d[3], dv[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) d[a] = A.rays_d[ray * 3 + a];
+      view_input(d, dv);
+      lds_tile_store(vet + wave * HB_TILE, enc_tile<MODE>(dv, 0, grp, 4));
+    }
     // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles; its last step wraps in the next
     // item's chunk 0
     bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true>(A, lds, sample, xa, xb, 0, D_ZB);
@@ -160,19 +174,6 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       asm volatile("" ::: "memory");
       const char* xt = xbuf + (b & 1) * HB_TILE;
       const char* zt = stage + b * (4 * HB_TILE);  // wave b's dz_g tiles = wave block b of the item
-      // the view encoding of block b's ray, feature (stored position) lane & 31, in every k-slot
-      bf16x8 bve;
-      if (wave < 4) {
-        const int64_t ray = (item * WGS + b * TM) / A.n_samples;
-        float d[3], dv[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) d[a] = A.rays_d[ray * 3 + a];
-        view_input(d, dv);
-        const float v = enc_feature<false>(dv, stored_to_row(MODE, lane & 31), 4);
-        const __bf16 vb = (__bf16)v;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bve[e] = vb;
-      }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const bf16x8 bx = hb_tr_frag(xt, kk);
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
           gacc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hb_tr_frag(zt + mt * HB_TILE, kk), bx, gacc[mt], 0, 0, 0);
         if (wave < 4) {
           const bf16x8 a = hb_tr_frag(zt + wave * HB_TILE, kk);
-          gacc[4] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bve, gacc[4], 0, 0, 0);
+          gacc[4] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hb_tr_frag(vet + b * HB_TILE, kk), gacc[4], 0, 0, 0);
 #pragma unroll
           for (int e = 0; e < 8; ++e) gdb += (float)a[e];
         }
