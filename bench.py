@@ -39,7 +39,8 @@ PEAK_HBM_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (default: WORLD_SIZE under a torch.distributed launcher, else 1)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rays", type=int, default=131072)
@@ -53,7 +54,9 @@ def parse():
     ap.add_argument("--it-samples", type=int, default=16)
     ap.add_argument("--cpu-rays", type=int, default=2048,
                     help="rays of the bounded pixel-bandwidth-on CPU-baseline sample (--pixbw)")
-    ap.add_argument("--psnr-steps", type=int, default=1000, help="Adam steps of the converged-PSNR leg (0: skip)")
+    ap.add_argument("--psnr-steps", type=int, default=None,
+                    help="Adam steps of the converged-PSNR leg (default PSNR_LEG's, which the oracle fixtures "
+                         "were trained on; 0: skip)")
     ap.add_argument("--psnr-only", action="store_true", help="run the converged-PSNR leg alone and print it")
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the configs[2] (pixel bandwidth on) and F32-mode legs of the N = 1 line")
@@ -62,7 +65,12 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 collective backend: nccl (= RCCL, one GPU per rank) or gloo (rehearsal of the "
                          "N-rank GPU path with every rank on a shared GPU: rank r on device r mod count)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.gpus is None:
+        a.gpus = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.psnr_steps is None:
+        a.psnr_steps = PSNR_LEG["steps"]
+    return a
 
 
 def launch_ranks(a):
@@ -516,14 +524,18 @@ def aligned_psnr(pred, tgt, nv, view, dev=None):
     return fn(corr.float(), tgt[:, None], rng), fn(pred[:, None], tgt[:, None], rng), float(gamma[0]), float(scale[0])
 
 
-def oracle_fixture_path(seq):
-    return os.path.join(ROOT, "tests", "golden", f"psnr_oracle_s{seq}.npz")
+def oracle_fixture_path(seq, device="cpu"):
+    """The oracle's converged run on batch sequence `seq`: executed by torch on the build container's
+    CPU (tests/golden/psnr_oracle_s<k>.npz), or -- for the seed study's many sequences -- by torch's
+    own GPU kernels (tests/golden/psnr_oracle_gpu/, make_psnr_oracle.py --device cuda; never libden)."""
+    sub = ("golden",) if device == "cpu" else ("golden", "psnr_oracle_gpu")
+    return os.path.join(ROOT, "tests", *sub, f"psnr_oracle_s{seq}.npz")
 
 
-def _load_oracle_fixture(seq, leg, rd):
-    """tests/golden/psnr_oracle_s<seq>.npz when it was trained on exactly this leg, else None."""
+def _load_oracle_fixture(seq, leg, rd, device="cpu"):
+    """The oracle fixture of `seq` when it was trained on exactly this leg, else None."""
     import numpy as np
-    path = oracle_fixture_path(seq)
+    path = oracle_fixture_path(seq, device)
     if not os.path.exists(path):
         return None
     fx = np.load(path)
@@ -540,7 +552,7 @@ def _stats(xs):
     return {"n": len(xs), "mean": round(m, 4), "std": round(sd, 4), "sem": round(sd / math.sqrt(len(xs)), 4)}
 
 
-def psnr_long(rd, dev, steps=None, modes=("f32", "bf16"), sequences=(0, 1, 2), leg=None):
+def psnr_long(rd, dev, steps=None, modes=("f32", "bf16"), sequences=tuple(range(8)), leg=None):
     """BASELINE's "PSNR vs ref" at convergence (PSNR_LEG): for each batch sequence k, the HIP
     TrainStep in F32 (the reference's arithmetic, pinned to the reference at 1e-4 per step by tests/)
     and in BF16 (the benchmark's mode) train from ONE init on a teacher scene for `steps` Adam steps,
@@ -549,7 +561,9 @@ def psnr_long(rd, dev, steps=None, modes=("f32", "bf16"), sequences=(0, 1, 2), l
     reference's multi_step_lr); the held-out views are aligned to the teacher's by the reference's
     affine log-intensity correction (deblur_e_nerf.py:705-833) and scored with its PSNR
     (metric.py:68-72).  The reference side: tests/golden/psnr_oracle_s<k>.npz, the ORACLE trained the
-    same way on the same batch sequence in the build container (tests/golden/make_psnr_oracle.py).
+    same way on the same batch sequence in the build container (tests/golden/make_psnr_oracle.py), and
+    for the sequences without one the same oracle executed by torch on a GPU
+    (tests/golden/psnr_oracle_gpu/; where both exist their difference is reported, oracle_gpu_minus_cpu).
     Reported per sequence and as mean / std / standard error over the sequences: each mode's PSNR,
     each mode - the oracle (paired, same sequence) and BF16 - F32."""
     from deblur_e_nerf import _native as nat
@@ -571,7 +585,8 @@ def psnr_long(rd, dev, steps=None, modes=("f32", "bf16"), sequences=(0, 1, 2), l
         target, _, _ = nat.render(vo, vd, vu, ones, tflat, tcfg, tpacked, n_samples)
     rows = []
     for seq in sequences:
-        fx = _load_oracle_fixture(seq, L, rd)
+        fx_cpu, fx_gpu = _load_oracle_fixture(seq, L, rd, "cpu"), _load_oracle_fixture(seq, L, rd, "cuda")
+        fx = fx_cpu if fx_cpu is not None else fx_gpu
         row = {"seq": seq}
         for mode in modes:
             ts = TrainStep(n_events, n_samples=n_samples, radiance_dim=rd, mode=mode, device=dev,
@@ -605,7 +620,12 @@ def psnr_long(rd, dev, steps=None, modes=("f32", "bf16"), sequences=(0, 1, 2), l
             del ts
             torch.cuda.empty_cache()
         if fx is not None:
-            row["oracle"] = {"psnr_db": round(float(fx["psnr_db"]), 4), "threads": int(fx["threads"])}
+            row["oracle"] = {"psnr_db": round(float(fx["psnr_db"]), 4),
+                             "executed_on": "cpu" if fx_cpu is not None else "gpu (torch)"}
+            if fx_cpu is not None:
+                row["oracle"]["threads"] = int(fx_cpu["threads"])
+            if fx_cpu is not None and fx_gpu is not None:
+                row["oracle_gpu_minus_cpu_db"] = round(float(fx_gpu["psnr_db"]) - float(fx_cpu["psnr_db"]), 4)
         if "f32" in row and "bf16" in row:
             row["bf16_minus_f32_db"] = round(row["bf16"]["psnr_db"] - row["f32"]["psnr_db"], 4)
         rows.append(row)
@@ -616,12 +636,15 @@ def psnr_long(rd, dev, steps=None, modes=("f32", "bf16"), sequences=(0, 1, 2), l
         summary[f"{m}_minus_oracle"] = _stats([r[m]["minus_oracle_db"] for r in rows
                                                if "minus_oracle_db" in r.get(m, {})])
     summary["bf16_minus_f32"] = _stats([r["bf16_minus_f32_db"] for r in rows if "bf16_minus_f32_db" in r])
+    summary["oracle_gpu_minus_cpu"] = _stats([r["oracle_gpu_minus_cpu_db"] for r in rows
+                                              if "oracle_gpu_minus_cpu_db" in r])
     return dict(rows=rows, summary=summary, leg=L,
                 setup=f"teacher scene, {steps} Adam steps from one init (lr {L['lr0']} x{L['lr_gamma']} at "
                       f"{list(L['milestones'])} of the run), each on a fresh batch of {n_events} events = "
                       f"{4 * n_events} rays x {n_samples} samples; {nv} held-out {view}x{view} views, affine "
                       f"log-intensity correction, mean PSNR vs the teacher; per batch sequence, HIP F32 / BF16 "
-                      f"and the oracle trained identically (tests/golden/psnr_oracle_s<k>.npz)")
+                      f"and the oracle trained identically (tests/golden/psnr_oracle_s<k>.npz, executed on "
+                      f"the CPU; tests/golden/psnr_oracle_gpu/ by torch on a GPU)")
 
 
 def cpu_baseline_pixbw(n_rays, n_samples, rd, S, threads):
@@ -678,6 +701,25 @@ def timed_steps(ts, a, world, dev, sync):
     return elapsed
 
 
+def init_ranks(a, world, local, dist_mod=dist, cuda=torch.cuda):
+    """One process per GPU: rank `local` binds device `local` and joins the process group over RCCL
+    (backend "nccl", bound to that device); --dist-backend gloo rehearses N ranks on fewer GPUs
+    (rank r on device r mod count).  -> (world size, this rank's device).  dist_mod / cuda are
+    parameters so tests/test_bench_launcher.py checks the wiring on the CPU."""
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if a.dist_backend == "gloo":
+            # rehearsal: RCCL refuses two ranks on one device, gloo all-reduces the GPU buffers
+            local = local % cuda.device_count()
+            cuda.set_device(local)
+            dist_mod.init_process_group("gloo")
+        else:
+            cuda.set_device(local)
+            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist_mod.get_world_size()
+    return world, torch.device("cuda", local)
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -703,18 +745,7 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        if a.dist_backend == "gloo":
-            # rehearsal: RCCL refuses two ranks on one device, gloo all-reduces the GPU buffers
-            local = local % torch.cuda.device_count()
-            torch.cuda.set_device(local)
-            dist.init_process_group("gloo")
-        else:
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        world = dist.get_world_size()
-    dev = torch.device("cuda", local)
+    world, dev = init_ranks(a, world, local)
     from deblur_e_nerf import _native as nat
     if a.psnr_only:
         print(json.dumps(psnr_long(a.rd, dev, steps=a.psnr_steps or None)), flush=True)

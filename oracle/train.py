@@ -94,7 +94,10 @@ def pixbw_step_loss(p, bkgd, raw, it_sample_size, n_samples, prm, min_ts, w=(1.0
             with torch.no_grad():  # tau_r frozen: no gradient through the poses
                 pos, rot = otraj.linear_trajectory(raw["T_wc_timestamp"], raw["T_wc_position"].float(),
                                                    raw["T_wc_orientation"].float(), ts.detach())
-            ro, rdir = oev.pixel_params_to_ray(raw["intrinsics_inverse"], raw["position"], pos, rot)
+            # the rays in the poses' precision (f32, as the HIP path's den_pixel_rays); the f64 oracle
+            # promotes them below
+            ro, rdir = oev.pixel_params_to_ray(raw["intrinsics_inverse"].to(pos.dtype), raw["position"].to(pos.dtype),
+                                               pos, rot)
             col, _, _, _ = onerf.render_rays(p, ro.reshape(-1, 3).to(bkgd.dtype), rdir.reshape(-1, 3).to(bkgd.dtype),
                                              jit[g].to(bkgd.dtype), n_samples=n_samples, bkgd=bkgd)
             if raw.get("channel") is not None:

@@ -63,7 +63,8 @@ def main():
                     help="where torch executes the oracle: cpu (the build container), or cuda -- torch's own GPU "
                          "kernels (rocBLAS / hipBLASLt GEMMs, elementwise ops), never libden -- for the many "
                          "sequences of the oracle's own seed study")
-    ap.add_argument("--out-dir", default=None, help="fixture directory (default tests/golden)")
+    ap.add_argument("--out-dir", default=None,
+                    help="fixture directory (default tests/golden, tests/golden/psnr_oracle_gpu for --device cuda)")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     if a.device != "cpu":
@@ -137,7 +138,7 @@ def main():
     with torch.device("cpu"):
         ps, ps_raw, gamma, scale = bench.aligned_psnr(pred, target, nv, view)
     print(f"oracle seq {a.seq}: PSNR {ps:.4f} dB (uncorrected {ps_raw:.3f}), gamma {gamma:.4f}, scale {scale:.4f}")
-    out = bench.oracle_fixture_path(a.seq) if a.out_dir is None else \
+    out = bench.oracle_fixture_path(a.seq, a.device) if a.out_dir is None else \
         os.path.join(a.out_dir, os.path.basename(bench.oracle_fixture_path(a.seq)))
     np.savez_compressed(out, psnr_db=np.array(ps), psnr_uncorrected_db=np.array(ps_raw), gamma=np.array(gamma),
                         scale=np.array(scale), pred=pred[:, 0].reshape(nv, view, view).numpy().astype(np.float32),

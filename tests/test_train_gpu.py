@@ -168,7 +168,11 @@ def test_missed_rays_stay_finite_over_training():
 
 @pytest.mark.parametrize("rd", [1, 3])
 # BF16: the TV loss measured 2.4e-2 off (a difference of pixel-bandwidth filtered log intensities
-# 1e-3 apart), gradients 1.4e-2
+# 1e-3 apart).  The BF16 gradient error is set by the forward's BF16 noise against the intensity
+# change over the events' interval: with the camera on the pose trajectory (r05) it measured 13 / 6 /
+# 2.1 / 0.86 % at 5 / 20 / 50 / 200 units/s, the layer-major and sample-major backward identical
+# (profiles/probe_pixbw_bf16.py, gpurun_out r05h / r05i) -- conditioning, not the kernels; the test
+# runs at 200 units/s, where the f32 oracle's own error is smallest too.
 @pytest.mark.parametrize("mode,tol_l,tol_g", [("f32", 1e-4, 1e-4), ("bf16", 3e-2, 3e-2)])
 def test_pixbw_train_step_matches_oracle(rd, mode, tol_l, tol_g):
     """Pixel-bandwidth-on step (BASELINE configs[2] shape, small): PixbwTrainStep
@@ -182,7 +186,7 @@ def test_pixbw_train_step_matches_oracle(rd, mode, tol_l, tol_g):
     from oracle.train import pixbw_flat_grad
     N, S, n_s = 4, 16, 128
     ts = PixbwTrainStep(N, it_sample_size=S, n_samples=n_s, radiance_dim=rd, mode=mode, device=DEV, seed=9)
-    raw = synthetic_pixbw_events(N, it_sample_size=S, seed=13)
+    raw = synthetic_pixbw_events(N, it_sample_size=S, seed=13, speed=200.0)
     if rd == 3:
         raw["channel"] = torch.randint(0, 3, (N,), generator=torch.Generator().manual_seed(13))
     ts.load_events(**raw)
