@@ -164,32 +164,43 @@ def extra_leg(a, dev, pixbw, mode, steps, warmup=2, rays=None):
 
 
 PHASE_REPS = 3
-# Algorithmic work of each render-path kernel class per sample and STEP (BF16 layout, DESIGN.md
-# section 4), rd = 1 (rd = 3 adds 2 x 128 MACs to the forward and to the head backward).
-#   render_fwd : the forward MLP, 2 x 593,152 MAC
-#   render_bwd : compositing adjoint + the head chain Lr^T (rd x 128), Lg^T (128 x 256, bottleneck
-#                part only) + the fused Lr weight gradient (rd x 128)
-#   hidden_bwd : 7 launches (L7..L1), each dX (256 x 256) + dW (256 x 256) MACs
-#   hidden_bwd_lb : 1 launch (Lb), dX (256 x 257) + dW (257 x 256) MACs
-#   dw_gemm    : the weight gradients of L0 (256 x 63), L5's pe columns (256 x 63), Lg (128 x 283)
-# FLOP = 2 x MAC.  Per launch = per step / launches per step.
-def flop_per_sample(rd):
-    return {"render_fwd_kernel": 2.0 * MAC_PER_SAMPLE[rd],
-            "render_bwd_kernel": 2.0 * (2 * rd * 128 + 128 * 256),
-            "hidden_bwd_kernel": 2.0 * 7 * 2 * 256 * 256,
-            "hidden_bwd_lb_kernel": 2.0 * 2 * 257 * 256,
-            "dw_gemm_kernel": 2.0 * (256 * 63 * 2 + 128 * 283)}
+# Algorithmic work of each render-path kernel per sample and STEP; FLOP =
+# 2 x MAC, per launch = per step / launches per step.  The forward: 593,152 MAC (rd = 1; rd = 3 adds
+# 2 x 128).  BF16 (the layer-major backward):
+#   render_head_bwd : compositing adjoint, Lr^T (rd x 128) + the fused Lr weight gradient (rd x 128),
+#                     Lg^T (128 x 256, bottleneck part) + the fused Lg weight gradient (128 x 283)
+#   hidden_bwd      : 7 launches (L7..L1), each dX (256 x 256) + dW (256 x 256)
+#   hidden_bwd_lb   : 1 launch (Lb), dX (256 x 257) + dW (257 x 256)
+#   dwstream        : the weight gradients of L0 (256 x 63) and of L5's pe columns (256 x 63)
+# F32 (the sample-major parity path):
+#   render_bwd      : the whole dX chain, Lr^T, Lg^T, Lb^T (257 x 256), L7^T..L1^T (7 x 256 x 256)
+#   dw_gemm         : every layer's weight gradient (the forward's MACs)
+def flop_per_sample(rd, mode="bf16"):
+    fwd = MAC_PER_SAMPLE[rd]
+    if mode == "bf16":
+        return {"render_fwd_kernel": 2.0 * fwd,
+                "render_head_bwd_kernel": 2.0 * (2 * rd * 128 + 128 * 256 + 128 * 283),
+                "hidden_bwd_kernel": 2.0 * 7 * 2 * 256 * 256,
+                "hidden_bwd_lb_kernel": 2.0 * 2 * 257 * 256,
+                "dwstream_kernel": 2.0 * (256 * 63 * 2)}
+    return {"render_fwd_kernel": 2.0 * fwd,
+            "render_bwd_kernel": 2.0 * (rd * 128 + 128 * 256 + 257 * 256 + 7 * 256 * 256),
+            "dw_gemm_kernel": 2.0 * fwd}
 
 
-# algorithmic HBM bytes per sample and STEP of each kernel class, BF16 layout:
-# hidden_bwd: L7..L1 each read dz_l + a_(l-1) and write dz_(l-1), 256 bf16 each = 1536 B; Lb reads
-# dz_b (257 bf16) + S7 and writes dz_7 = 1538 B; render_fwd: the activations + record it stores for
-# the backward; render_bwd: the record + G read, dz_g and dz_b (256 bottleneck + sigma) written
-# (16 + 256 + 256 + 514 B).
-# dw_gemm_kernel (the streamed weight-gradient kernels, den_dwstream.hip): dz_0 + dz_5 + pe,
-# dz_g + bottleneck + ve = 1152 + 832 B per sample
-BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "hidden_bwd_lb_kernel": 1538, "render_fwd_kernel": 5072,
-                    "render_bwd_kernel": 1042, "dw_gemm_kernel": 1984}
+# the kernels behind den_timing's classes on the BF16 layer-major path
+BF16_KERNEL_NAMES = {"render_bwd_kernel": "render_head_bwd_kernel", "dw_gemm_kernel": "dwstream_kernel"}
+
+# algorithmic HBM bytes per sample and STEP of each BF16 kernel:
+#   hidden_bwd: L7..L1 each read dz_l + a_(l-1) and write dz_(l-1), 256 bf16 each = 1536 B;
+#   hidden_bwd_lb: reads dz_b (257 bf16) + S7, writes dz_7 = 1538 B;
+#   render_fwd: the activations + record it stores for the backward, S0..S7 + bottleneck + G + record
+#     (4096 + 512 + 256 + 16 B; pe / ve are recomputed by the backward, not stored);
+#   render_head_bwd: the record + G + bottleneck read, dz_b (256 bottleneck + sigma) written
+#     (16 + 256 + 512 + 514 B; dz_g stays on chip);
+#   dwstream: dz_0 + dz_5 read (pe recomputed) = 1024 B
+BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "hidden_bwd_lb_kernel": 1538, "render_fwd_kernel": 4880,
+                    "render_head_bwd_kernel": 1298, "dwstream_kernel": 1024}
 
 
 def pmc_traffic(kernel, a):
@@ -770,12 +781,14 @@ def main():
     nat.timing_enable(False)
     kt = nat.timing_collect()
     n_local = ts.R * (ts.n_samples if a.pixbw else ts.S)
-    fps = flop_per_sample(a.rd)
+    fps = flop_per_sample(a.rd, a.mode)
     peak = PEAK_TFLOPS[a.mode]
     kernels = {}
     for k, (tot, cnt) in kt.items():
         if cnt == 0:
             continue
+        if a.mode == "bf16":
+            k = BF16_KERNEL_NAMES.get(k, k)
         avg = tot / cnt
         e = {"launches_per_step": cnt // PHASE_REPS, "avg_ms": round(avg, 4),
              "step_ms": round(tot / PHASE_REPS, 3)}

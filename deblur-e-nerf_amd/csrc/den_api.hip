@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -130,7 +131,11 @@ WsLayout ws_layout(const den_render_desc* d) {
     // sample-major BF16 path writes them itself, enc_store_kernel)
     // dz_g: kept on chip by the BF16 head backward (render_head_bwd_kernel, the fused Lg weight
     // gradient) unless den_render_ray_grad will read it
+#if defined(DEN_DWS_EXP) && DEN_DWS_EXP == 4
+    const bool enc = a == D_ZG && !d->ray_grad;
+#else
     const bool enc = a == A_PE || a == A_VE || (a == D_ZG && !d->ray_grad);
+#endif
     if (d->train && !(enc && use_hidden_path(d))) off += align256((size_t)n * act_width(d->mode, a) * es);
   }
   L.rec = off;
@@ -405,17 +410,19 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   return DEN_OK;
 }
 
-// compute units of the current device (the persistent forward runs one workgroup per CU)
-int device_cu_count() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cached[dev] == 0) {
-    int n = 0;
+// compute units of the device that owns stream `s` (the persistent kernels run one workgroup per
+// CU); cached per device, thread-safe (several host threads may drive several devices)
+int device_cu_count(hipStream_t s) {
+  static std::atomic<int> cached[64];
+  int dev = -1;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev < 0 || dev >= 64) return 256;
+  int n = cached[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cached[dev] = n;
+    cached[dev].store(n, std::memory_order_relaxed);
   }
-  return cached[dev];
+  return n;
 }
 
 template <int MODE>
@@ -427,7 +434,7 @@ int render_fwd_impl(const den_render_desc* d, const den_render_io* io, hipStream
   A.n_items = n / fwd_wg_samples(MODE);
   // persistent: one workgroup per CU (the 143 KB weight ring + records admit one), each walking
   // items blockIdx.x, blockIdx.x + grid, ...
-  const unsigned grid = (unsigned)std::min<int64_t>(A.n_items, device_cu_count());
+  const unsigned grid = (unsigned)std::min<int64_t>(A.n_items, device_cu_count(s));
   {
     DEN_TIMED(T_RENDER_FWD, s);
     if (d->train)
@@ -484,9 +491,14 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
   if (hidden) {
     // streamed, operand-sharing weight gradients (den_dwstream.hip)
     // (pe and ve are recomputed from the samples: the BF16 forward does not store them)
+#if defined(DEN_DWS_EXP) && DEN_DWS_EXP == 4
+    if ((rc = launch_dwstream<8, 16, 2, 2, DWS_NW1, 3, 1, 0>(d, io, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK)
+      return rc;
+#else
     if ((rc = launch_dwstream<8, 16, 2, 2, DWS_NW1, 3, 1, ENC_PE>(d, io, L, ws, D_Z0 + 0, D_Z0 + 5, -1, -1, s)) !=
         DEN_OK)
       return rc;
+#endif
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s)) != DEN_OK) return rc;
     // (Lb's weight gradient comes from its hidden launch, Lr's and Lg's from render_head_bwd_kernel)

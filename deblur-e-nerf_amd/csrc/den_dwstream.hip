@@ -77,6 +77,21 @@ __device__ __forceinline__ void dws_dma_piece(const char* tile_src, char* dst, i
                : "memory", "m0");
 }
 
+// The fixed-count sampler's encodings (points == 0) are pipelined: the block's ray (o, d, jitter;
+// one ray per 32-sample block) arrives by one untracked dword LDS-DMA of wave 0 a ring step ahead of
+// the block's tiles, and waves [0, T_ENC) compute the block's encoding tiles from it one iteration
+// before its MFMAs -- no global-memory latency on the critical path (r05: computed synchronously
+// from global memory inside the fetch, the {L0 + L5 pe} launch took 5.5 ms against 2.9 ms with pe
+// stored).  Given points / packed samples (points 1 / 2) keep the synchronous fetch-time path.
+__device__ __forceinline__ void dws_dma_ray(const float* src, char* dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)dst);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" : : "v"(src), "s"(m0) : "memory", "m0");
+}
+constexpr int DWS_RAY_BYTES = 256;
+#ifndef DEN_DWS_EXP
+#define DEN_DWS_EXP 0  // experiment builds only (profiles/exp_variants.sh): 1 no encoding, 2 no sampler
+#endif  // per ring slot: 64 lanes x 4 B of the ray DMA (lanes 0..6 used)
+
 // U: wave blocks per ring slot (one barrier per U blocks); P.n_blocks / P.per_wg count U-block steps
 template <int MA, int MT, int NB, int NT, int NW, int DEPTH, int U = 1, int ENC = 0>
 __attribute__((aligned(4096)))  // page-aligned code (r04y A/B)
@@ -92,14 +107,93 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
   static_assert(!(ENC & ENC_VE) || !(ENC & ENC_PE), "one encoding per launch");
   constexpr int T_DMA = TILES - T_PE - T_VE;        // stored tiles, fetched by LDS-DMA
   constexpr int T_ENC = T_PE + T_VE;
+  static_assert(T_ENC == 0 || U == 1, "the encoding launches step one wave block at a time");
+  static_assert(T_ENC <= NW, "one wave per encoding tile");
   constexpr int PIECES = 2 * T_DMA * U;             // 1 KiB DMA pieces per step
   constexpr int TPW = (MT * NT + NW - 1) / NW;      // output tiles per wave
-  static_assert(RING * SLOT <= 160 * 1024, "ring exceeds the LDS");
-  __shared__ __attribute__((aligned(16))) char lds[RING * SLOT];
+  constexpr int RAY_LDS = T_ENC > 0 ? RING * DWS_RAY_BYTES : 0;
+  static_assert(RING * SLOT + RAY_LDS <= 160 * 1024, "ring exceeds the LDS");
+  __shared__ __attribute__((aligned(16))) char lds[RING * SLOT + RAY_LDS];
+  char* ray_lds = lds + RING * SLOT;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR) for the DMA operands
+  // readfirstlane hides the range of threadIdx.x >> 6: without it the compiler cannot prove the
+  // output-tile guards (t < MT * NT) true, branches around every MFMA and copies the accumulators
+  // through each branch (r05: 5.7 ms -> measured below with the range restored)
+  __builtin_assume(wave >= 0 && wave < NW);
   const int64_t b0 = (int64_t)blockIdx.x * P.per_wg;
   const int64_t b1 = b0 + P.per_wg < P.n_blocks ? b0 + P.per_wg : P.n_blocks;
+  const bool pipe = T_ENC > 0 && P.points == 0 && DEN_DWS_EXP != 3 && DEN_DWS_EXP != 5;  // kernel argument: uniform
+
+  // the encoding tiles of wave block `blk` into ring slot `dst` (waves [0, T_ENC): tile = wave), lane
+  // = sample (l & 31), lane group l >> 5, the forward's sampler and enc_tile -- bit-identical to the
+  // tiles it would store.  `ray`: the pipelined path's ray in LDS (o, d, jitter), else null (the
+  // sampler reads global memory).
+  auto encode = [&](int64_t blk, char* dst, const float* ray) __attribute__((always_inline)) {
+    if constexpr (T_ENC > 0 && DEN_DWS_EXP != 1 && DEN_DWS_EXP != 5) {
+      const int te = wave;
+      if (te < T_ENC) {
+        // lane-derived values from an opaque copy of the thread index: loop-invariant, the
+        // encoding's per-lane-group constants were hoisted out of the block loop and spilled
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int ln = tid & 63;
+        const int64_t s = blk * 32 + (ln & 31);
+        // the sampler's arguments read here, from the kernarg segment through an opaque pointer:
+        // preloaded, the dozen extra argument words stay live in scalar registers across the loop
+        typedef __attribute__((address_space(4))) const DwStreamArgs KArgs;
+        KArgs* Pp = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // P is the kernel's only argument
+        asm volatile("" : "+s"(Pp));
+        float aabb[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) aabb[q] = Pp->aabb[q];
+        float xc[3], dir[3], sel;
+        if (ray) {
+          // the fixed-count sampler of sample_point with the block's one ray (n_samples is 64, 128
+          // or 256: a 32-sample wave block lies within one ray)
+          const int64_t s0 = blk * 32;
+          const int64_t r = s0 / Pp->n_samples;
+          const int k = (int)(s0 - r * Pp->n_samples) + (ln & 31);
+          float o[3];
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            o[a] = ray[a];
+            dir[a] = ray[3 + a];
+          }
+#if DEN_DWS_EXP == 2
+          for (int a = 0; a < 3; ++a) xc[a] = o[a] + dir[a] * (float)k;
+#else
+          const RayGeom g = ray_geom(o, dir, aabb, Pp->near_p, Pp->far_p);
+          float t0, t1;
+          sample_interval(g, k, ray[6], Pp->n_samples, &t0, &t1);
+          contract(o, dir, t0, t1, aabb, xc, &sel);
+#endif
+        } else {
+          sample_point(*Pp, aabb, s, xc, dir, &sel);
+        }
+        f32x16 v;
+        float dv[3];
+        view_input(dir, dv);
+        // the tile index as a compile-time constant (wave-uniform branches): enc_tile's feature
+        // indices then fold, with no per-lane coordinate choice
+#pragma unroll
+        for (int tt = 0; tt < T_ENC; ++tt)
+          if (te == tt) v = T_PE ? enc_tile<1>(xc, tt, ln >> 5, 10) : enc_tile<1>(dv, tt, ln >> 5, 4);
+        lds_tile_store(dst + (MT + (T_PE ? 0 : NB) + te) * HB_TILE, v);
+      }
+    }
+  };
+
+  // wave 0 (pipelined path): block blk's ray into its ray slot; issued every iteration (the address
+  // clamped to the range) so that wave 0's DMA count per iteration stays uniform
+  auto ray_dma = [&](int64_t blk) __attribute__((always_inline)) {
+    const int64_t bc = blk < b1 ? blk : b1 - 1;
+    const int64_t r = bc * 32 / P.n_samples;
+    const float* src = lane < 3 ? P.rays_o + r * 3 + lane
+                     : lane < 6 ? P.rays_d + r * 3 + (lane - 3)
+                     : lane == 6 ? P.jitter + r : P.rays_o + r * 3;
+    dws_dma_ray(src, ray_lds + (int)((blk - b0) % RING) * DWS_RAY_BYTES);
+  };
 
   auto fetch = [&](int64_t blk, char* dst) __attribute__((always_inline)) {
 #pragma unroll
@@ -118,68 +212,20 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
         dws_dma_piece(src, dst + ub * BLK + t * 2048 + f * 1024, f);
       }
     }
-    if constexpr (T_ENC > 0) {
-      // the encoding tiles: one wave per (wave block, tile), lane = sample (l & 31), lane group
-      // l >> 5, the forward's sampler and enc_tile -- bit-identical to the tiles it would store
-#pragma unroll
-      for (int e0 = 0; e0 < T_ENC * U; e0 += NW) {
-        const int e = e0 + wave;
-        if (e < T_ENC * U) {
-          const int ub = e / T_ENC, te = e % T_ENC;
-          // lane-derived values from an opaque copy of the thread index: loop-invariant, the
-          // encoding's per-lane-group constants were hoisted out of the block loop and spilled
-          int tid = threadIdx.x;
-          asm volatile("" : "+v"(tid));
-          const int ln = tid & 63;
-          const int64_t s = (blk * U + ub) * 32 + (ln & 31);
-          // the sampler's arguments read here, from the kernarg segment through an opaque pointer:
-          // preloaded, the dozen extra argument words stay live in scalar registers across the loop
-          typedef __attribute__((address_space(4))) const DwStreamArgs KArgs;
-          KArgs* Pp = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // P is the kernel's only argument
-          asm volatile("" : "+s"(Pp));
-          float aabb[6];
-#pragma unroll
-          for (int q = 0; q < 6; ++q) aabb[q] = Pp->aabb[q];
-          float xc[3], dir[3], sel;
-          if (Pp->points == 0) {
-            // the fixed-count sampler of sample_point, with the ray wave-uniform: a 32-sample wave
-            // block lies within one ray (n_samples is 64, 128 or 256, den_render_desc)
-            const int64_t s0 = (blk * U + ub) * 32;
-            const int64_t ray = s0 / Pp->n_samples;
-            const int k = (int)(s0 - ray * Pp->n_samples) + (ln & 31);
-            float o[3];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-              o[a] = Pp->rays_o[ray * 3 + a];
-              dir[a] = Pp->rays_d[ray * 3 + a];
-            }
-            const RayGeom g = ray_geom(o, dir, aabb, Pp->near_p, Pp->far_p);
-            float t0, t1;
-            sample_interval(g, k, Pp->jitter[ray], Pp->n_samples, &t0, &t1);
-            contract(o, dir, t0, t1, aabb, xc, &sel);
-          } else {
-            sample_point(*Pp, aabb, s, xc, dir, &sel);
-          }
-          f32x16 v;
-          float dv[3];
-          view_input(dir, dv);
-          // the tile index as a compile-time constant (wave-uniform branches): enc_tile's feature
-          // indices then fold, with no per-lane coordinate choice
-#pragma unroll
-          for (int tt = 0; tt < T_ENC; ++tt)
-            if (te == tt) v = T_PE ? enc_tile<1>(xc, tt, ln >> 5, 10) : enc_tile<1>(dv, tt, ln >> 5, 4);
-          lds_tile_store(dst + ub * BLK + (MT + (T_PE ? 0 : NB) + te) * HB_TILE, v);
-        }
-      }
-    }
+    if (!pipe) encode(blk, dst, nullptr);  // synchronous (given points / packed samples)
   };
   // DMA instructions this wave issues per block (pieces pc = q * NW + wave < PIECES)
   const bool extra = wave < PIECES % NW;
   constexpr int OPS_LO = PIECES / NW, OPS_HI = OPS_LO + 1;
+  // ... plus wave 0's ray DMA on the pipelined path
+  const bool ray_wave = pipe && wave == 0;
 
 #pragma unroll
   for (int u = 0; u < DEPTH; ++u)
     if (b0 + u < b1) fetch(b0 + u, lds + u * SLOT);
+  if (ray_wave)
+#pragma unroll
+    for (int u = 0; u <= DEPTH; ++u) ray_dma(b0 + u);
 
   f32x16 acc[TPW];
 #pragma unroll
@@ -193,10 +239,23 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  if (pipe && b0 < b1) {
+    // the first block's encodings (the loop computes block blk + 1's during block blk)
+    encode(b0, lds, (const float*)ray_lds);
+    hb_wait_vm_lgkm0<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
 
   for (int64_t blk = b0; blk < b1; ++blk) {
     const int u = (int)((blk - b0) % RING);
     if (blk + DEPTH < b1) fetch(blk + DEPTH, lds + ((u + DEPTH) % RING) * SLOT);
+    if (ray_wave) ray_dma(blk + DEPTH + 1);
+    if (pipe && blk + 1 < b1) {
+      const int u1 = (u + 1) % RING;
+      encode(blk + 1, lds + u1 * SLOT, (const float*)(ray_lds + u1 * DWS_RAY_BYTES));
+    }
 #pragma unroll
     for (int ub = 0; ub < U; ++ub) {
     const char* cur = lds + u * SLOT + ub * BLK;
@@ -224,8 +283,13 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
     }
     }
     if (blk + DEPTH < b1) {
-      if (extra) hb_wait_vm_lgkm0<(DEPTH - 1) * OPS_HI>();
-      else hb_wait_vm_lgkm0<(DEPTH - 1) * OPS_LO>();
+      if (ray_wave) {
+        if (extra) hb_wait_vm_lgkm0<(DEPTH - 1) * (OPS_HI + 1)>();
+        else hb_wait_vm_lgkm0<(DEPTH - 1) * (OPS_LO + 1)>();
+      } else {
+        if (extra) hb_wait_vm_lgkm0<(DEPTH - 1) * OPS_HI>();
+        else hb_wait_vm_lgkm0<(DEPTH - 1) * OPS_LO>();
+      }
     } else {
       hb_wait_vm_lgkm0<0>();
     }

@@ -59,6 +59,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
   float* rec_lds = (float*)(lds + 2 * LDS_BUF);
   char* stage = lds + 2 * LDS_BUF + WGS * 16;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_assume(wave >= 0 && wave < 8);  // the range readfirstlane hides (see dwstream_kernel)
   char* xbuf = stage + HD_STAGE + wave * HD_XBUF;
   char* lscr = stage + wave * (4 * HB_TILE);  // this wave's Lr scratch = its own dz_g staging area
   char* vet = stage + HD_STAGE + 8 * HD_XBUF;  // ve tiles of the item's 8 wave blocks

@@ -527,7 +527,11 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
     // sample positions -> positional encoding as PE_PAD/TM fake accumulator tiles -> fragments.
     // Kept for the backward in F32 mode only: the BF16 backward recomputes pe / ve where it needs
     // them (den_dwstream.hip: 192 B per sample neither stored nor read back)
+#if defined(DEN_DWS_EXP) && DEN_DWS_EXP == 4
+    constexpr bool STORE_ENC = TRAIN;  // experiment build: the BF16 forward stores pe / ve again
+#else
     constexpr bool STORE_ENC = TRAIN && MODE == 0;
+#endif
     constexpr int PE_T = PE_PAD / TM, PE_S = PE_T * FPT;
     float dir[NB][3], sel[NB];
     Frag pe[NB * PE_S];

@@ -76,6 +76,8 @@ template <int DEG>
 __global__ __launch_bounds__(SH_THREADS) void sh_fwd_kernel(int64_t n, const float* __restrict__ coords,
                                                           float* __restrict__ out, ShCoef cf) {
   constexpr int K = DEG * DEG, P = K + 1;
+  static_assert(SH_THREADS * P * 4 <= 160 * 1024, "the staging tile exceeds gfx950's 160 KiB of LDS per workgroup "
+                                                 "(degree 8 needs 65 KiB: gfx950 only, over gfx90a / gfx942's 64 KiB)");
   __shared__ float tile[SH_THREADS * P];
   const int64_t base = int64_t(blockIdx.x) * SH_THREADS;
   const int t = threadIdx.x;
@@ -96,6 +98,8 @@ __global__ __launch_bounds__(SH_THREADS) void sh_bwd_kernel(int64_t n, const flo
                                                           const float* __restrict__ d_out,
                                                           float* __restrict__ d_coords, ShCoef cf) {
   constexpr int K = DEG * DEG, P = K + 1;
+  static_assert(SH_THREADS * P * 4 <= 160 * 1024, "the staging tile exceeds gfx950's 160 KiB of LDS per workgroup "
+                                                 "(degree 8 needs 65 KiB: gfx950 only, over gfx90a / gfx942's 64 KiB)");
   __shared__ float tile[SH_THREADS * P];
   const int64_t base = int64_t(blockIdx.x) * SH_THREADS;
   const int t = threadIdx.x;

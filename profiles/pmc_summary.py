@@ -15,7 +15,8 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("render_fwd_kernel", "render_bwd_kernel", "hidden_bwd_kernel", "dwstream_kernel", "dw_gemm_kernel",
+KERNELS = ("render_fwd_kernel", "render_head_bwd_kernel", "render_bwd_kernel", "hidden_bwd_kernel", "dwstream_kernel",
+           "dw_gemm_kernel",
            "dw_reduce_kernel", "pack_kernel", "adam_kernel")
 
 
