@@ -127,15 +127,12 @@ WsLayout ws_layout(const den_render_desc* d) {
       continue;
     }
     L.act[a] = off;
-    // pe / ve: kept by the F32 forward only; the BF16 layer-major backward recomputes them (the
-    // sample-major BF16 path writes them itself, enc_store_kernel)
+    // pe: kept by the forward (read once by the streamed L0 / L5-pe weight gradient); ve: kept by the
+    // F32 forward only (the BF16 head backward recomputes its tile in LDS; the sample-major BF16 path
+    // writes it itself, enc_store_kernel)
     // dz_g: kept on chip by the BF16 head backward (render_head_bwd_kernel, the fused Lg weight
     // gradient) unless den_render_ray_grad will read it
-#if defined(DEN_DWS_EXP) && DEN_DWS_EXP == 4
-    const bool enc = a == D_ZG && !d->ray_grad;
-#else
-    const bool enc = a == A_PE || a == A_VE || (a == D_ZG && !d->ray_grad);
-#endif
+    const bool enc = a == A_VE || (a == D_ZG && !d->ray_grad);
     if (d->train && !(enc && use_hidden_path(d))) off += align256((size_t)n * act_width(d->mode, a) * es);
   }
   L.rec = off;
@@ -265,11 +262,10 @@ int launch_dw(const den_render_desc* d, const WsLayout& L, char* ws, int layer, 
   return DEN_OK;
 }
 
-// One streamed weight-gradient launch (den_dwstream.hip) over the whole sample range; ENC: the
-// column tiles it recomputes from the samples (b0 / b1 then unused).
-template <int MA, int MT, int NB, int NT, int NW, int DEPTH, int U = 1, int ENC = 0>
-int launch_dwstream(const den_render_desc* d, const den_render_io* io, const WsLayout& L, char* ws, int a0, int a1,
-                    int b0, int b1, hipStream_t s) {
+// One streamed weight-gradient launch (den_dwstream.hip) over the whole sample range.
+template <int MA, int MT, int NB, int NT, int NW, int DEPTH, int U = 1>
+int launch_dwstream(const den_render_desc* d, const WsLayout& L, char* ws, int a0, int a1, int b0, int b1,
+                    hipStream_t s) {
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
   DwStreamArgs P{};
   P.a[0] = ws + L.act[a0];
@@ -285,22 +281,9 @@ int launch_dwstream(const den_render_desc* d, const den_render_io* io, const WsL
   P.n_blocks = n / 32 / U;
   const int64_t grid = hidden_grid(n);
   P.per_wg = (P.n_blocks + grid - 1) / grid;
-  P.points = d->points;
-  P.n_samples = d->n_samples;
-  P.contraction = d->contraction;
-  for (int i = 0; i < 6; ++i) P.aabb[i] = d->aabb[i];
-  P.near_p = d->near_plane;
-  P.far_p = d->far_plane;
-  P.rays_o = io->rays_o;
-  P.rays_d = io->rays_d;
-  P.jitter = io->jitter;
-  P.ray_idx = io->ray_indices;
-  P.t_start = io->t_starts;
-  P.t_end = io->t_ends;
   {
     DEN_TIMED(T_DW_GEMM, s);
-    hipLaunchKernelGGL((dwstream_kernel<MA, MT, NB, NT, NW, DEPTH, U, ENC>), dim3((unsigned)grid), dim3(64 * NW), 0, s,
-                       P);
+    hipLaunchKernelGGL((dwstream_kernel<MA, MT, NB, NT, NW, DEPTH, U>), dim3((unsigned)grid), dim3(64 * NW), 0, s, P);
   }
   DEN_LAUNCHED();
   return DEN_OK;
@@ -489,16 +472,8 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
   }
   if (!(parts & 2)) return DEN_OK;
   if (hidden) {
-    // streamed, operand-sharing weight gradients (den_dwstream.hip)
-    // (pe and ve are recomputed from the samples: the BF16 forward does not store them)
-#if defined(DEN_DWS_EXP) && DEN_DWS_EXP == 4
-    if ((rc = launch_dwstream<8, 16, 2, 2, DWS_NW1, 3, 1, 0>(d, io, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK)
-      return rc;
-#else
-    if ((rc = launch_dwstream<8, 16, 2, 2, DWS_NW1, 3, 1, ENC_PE>(d, io, L, ws, D_Z0 + 0, D_Z0 + 5, -1, -1, s)) !=
-        DEN_OK)
-      return rc;
-#endif
+    // streamed, operand-sharing weight gradients (den_dwstream.hip): L0 and L5's pe columns
+    if ((rc = launch_dwstream<8, 16, 2, 2, DWS_NW1, 3, 1>(d, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s)) != DEN_OK) return rc;
     if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s)) != DEN_OK) return rc;
     // (Lb's weight gradient comes from its hidden launch, Lr's and Lg's from render_head_bwd_kernel)

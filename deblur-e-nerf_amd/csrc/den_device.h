@@ -382,23 +382,32 @@ __device__ __forceinline__ float enc_arg(const float* v, int f, int n_deg) {
 // constants, so the argument is one select between two constant-index products and ONE sine --
 // not a per-lane choice of the coordinate (v[q % 3] with a lane-dependent q), whose lane masks
 // filled the forward's scalar registers.  The same values as enc_feature, bit for bit.
+// BF16: registers [R0, R0 + R) of enc_tile<1>(v, p, grp, n_deg) into out[0 .. R)
+template <int R0, int R>
+__device__ __forceinline__ void enc_tile_regs(const float* v, int p, int grp, int n_deg, float* out) {
+  const int nd = 3 * n_deg;
+  const bool hi = grp != 0;
+#pragma unroll
+  for (int r = R0; r < R0 + R; ++r) {
+    const int f0 = p * 32 + acc_row(1, 0, r), f1 = f0 + 4;
+    const bool sin0 = f0 >= 3 && f0 < 3 + 2 * nd, sin1 = f1 >= 3 && f1 < 3 + 2 * nd;
+    if (sin0 && sin1) {
+      const float x = hi ? enc_arg(v, f1, n_deg) : enc_arg(v, f0, n_deg);
+      out[r - R0] = __sinf(x);
+    } else {
+      out[r - R0] = hi ? enc_feature<false>(v, f1, n_deg) : enc_feature<false>(v, f0, n_deg);
+    }
+  }
+}
+
 template <int MODE>
 __device__ __forceinline__ typename Tr<MODE>::Acc enc_tile(const float* v, int p, int grp, int n_deg) {
   typename Tr<MODE>::Acc a;
   if constexpr (MODE == 1) {
-    const int nd = 3 * n_deg;
-    const bool hi = grp != 0;
+    float o[16];
+    enc_tile_regs<0, 16>(v, p, grp, n_deg, o);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int f0 = p * 32 + acc_row(1, 0, r), f1 = f0 + 4;
-      const bool sin0 = f0 >= 3 && f0 < 3 + 2 * nd, sin1 = f1 >= 3 && f1 < 3 + 2 * nd;
-      if (sin0 && sin1) {
-        const float x = hi ? enc_arg(v, f1, n_deg) : enc_arg(v, f0, n_deg);
-        a[r] = __sinf(x);
-      } else {
-        a[r] = hi ? enc_feature<false>(v, f1, n_deg) : enc_feature<false>(v, f0, n_deg);
-      }
-    }
+    for (int r = 0; r < 16; ++r) a[r] = o[r];
   } else {
 #pragma unroll
     for (int r = 0; r < Tr<MODE>::REGS; ++r) a[r] = enc_feature<true>(v, p * Tr<MODE>::TM + acc_row(MODE, grp, r), n_deg);

@@ -525,13 +525,9 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
 #endif
 
     // sample positions -> positional encoding as PE_PAD/TM fake accumulator tiles -> fragments.
-    // Kept for the backward in F32 mode only: the BF16 backward recomputes pe / ve where it needs
-    // them (den_dwstream.hip: 192 B per sample neither stored nor read back)
-#if defined(DEN_DWS_EXP) && DEN_DWS_EXP == 4
-    constexpr bool STORE_ENC = TRAIN;  // experiment build: the BF16 forward stores pe / ve again
-#else
-    constexpr bool STORE_ENC = TRAIN && MODE == 0;
-#endif
+    // pe is kept for the backward (the streamed L0 / L5-pe weight gradient reads it: den_dwstream.hip
+    // on recomputing it instead); ve only in F32 mode (the BF16 head backward recomputes its tile)
+    constexpr bool STORE_PE = TRAIN, STORE_VE = TRAIN && MODE == 0;
     constexpr int PE_T = PE_PAD / TM, PE_S = PE_T * FPT;
     float dir[NB][3], sel[NB];
     Frag pe[NB * PE_S];
@@ -570,7 +566,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
 #pragma unroll
       for (int p = 0; p < PE_T; ++p) {
         const Acc a = enc_tile<MODE>(xc, p, grp, 10);
-        if (STORE_ENC) store_tile_vals<MODE>(act_ptr<MODE>(A, A_PE, sample[b], p), a);
+        if (STORE_PE) store_tile_vals<MODE>(act_ptr<MODE>(A, A_PE, sample[b], p), a);
         acc_to_frags<MODE>(a, pe + b * PE_S + p * FPT);
       }
     }
@@ -583,7 +579,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
     // inference forward did, 52 SGPRs + 27 VGPRs, before r05)
 #pragma unroll
     for (int q = 0; q < NB * PE_S; ++q) asm volatile("" : "+v"(pe[q]));
-    constexpr int PE_ST = STORE_ENC ? NB * PE_T * (MODE == 1 ? 2 : 1) : 0;
+    constexpr int PE_ST = STORE_PE ? NB * PE_T * (MODE == 1 ? 2 : 1) : 0;
     static_assert(PE_ST < 64, "vmcnt is 6 bits");
     wait_vm_lgkm0<PE_ST>();
     __syncthreads();
@@ -629,7 +625,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
 #pragma unroll
       for (int p = 0; p < VE_T; ++p) {
         const Acc a = enc_tile<MODE>(dv, p, grp, 4);
-        if (STORE_ENC) {
+        if (STORE_VE) {
           store_tile_vals<MODE>(act_ptr<MODE>(A, A_VE, sample[b], p), a);
           vm.issued += MODE == 1 ? 2 : 1;
         }
