@@ -531,6 +531,14 @@ int den_debug_fwd_prof(uint64_t* out) {
 }
 #endif
 
+#ifdef DEN_HEAD_PROF
+// experiment builds only: per-wave phase cycles of the last render_head_bwd launch (256 WGs x 8 waves x 8)
+int den_debug_head_prof(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(den_head_prof), sizeof(uint64_t) * 256 * 8 * 8) == hipSuccess ? DEN_OK
+                                                                                                          : DEN_EHIP;
+}
+#endif
+
 int32_t den_render_tile_samples(int32_t mode) {
   return (mode == 0 || mode == 1) ? std::max(wg_samples(mode), fwd_wg_samples(mode)) : -1;
 }

@@ -23,6 +23,15 @@
 
 namespace den {
 
+#ifdef DEN_HEAD_PROF
+// experiment builds only: per-wave cycles of the head backward's phases (den_debug_head_prof,
+// profiles/head_prof.py)
+__device__ uint64_t den_head_prof[256 * 8 * 8];
+#define HD_T(q) prof[q] += __builtin_amdgcn_s_memtime() - t_; t_ = __builtin_amdgcn_s_memtime()
+#else
+#define HD_T(q)
+#endif
+
 constexpr int HD_STAGE = 8 * 4 * HB_TILE;  // dz_g of the item: 8 waves x 4 tiles (also each wave's Lr scratch)
 constexpr int HD_XBUF = 2 * HB_TILE;       // per wave: a double buffer of one bottleneck tile
 constexpr int HD_VE = 8 * HB_TILE;         // the item's view-encoding tiles, one per wave block
@@ -77,6 +86,11 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     for (int r = 0; r < 16; ++r) gacc[q][r] = 0.0f;
   float ldb[3] = {0.f, 0.f, 0.f}, gdb = 0.0f;
   const int64_t n_items = (int64_t)A0.n_rays * A0.n_samples / WGS;
+#ifdef DEN_HEAD_PROF
+  uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
+  uint64_t t_ = t_start;
+#endif
 
   for (int64_t item = blockIdx.x; item < n_items; item += gridDim.x) {
     // the arguments re-read from the kernarg segment per item through an opaque pointer (as the
@@ -91,7 +105,9 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     const int64_t sample = item * WGS + wave * TM + c;
 
     head_adjoint<MODE>(A, rec_lds, item, sample, wave, lane, c, grp);
+    HD_T(0);
     __syncthreads();  // also: every wave is done with the previous item's staged dz_g
+    HD_T(1);
 
     // fake dz tiles from the per-sample raw gradients (render_bwd_kernel<1, 1>)
     const f32x4 g4 = *(const f32x4*)(rec_lds + (wave * TM + c) * 4);
@@ -136,6 +152,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     // j=0 Lr^T: dz_r -> dz_g in registers (xa, 4 tiles; stored only for den_render_ray_grad) + the
     // fused Lr weight gradient
     bwd_layer_run<MODE, 1, 0, FPT, 0, true>(A, lds, sample, fr, xa, A_G, A.keep_dzg ? D_ZG : -1, lr_hook);
+    HD_T(2);
     // dz_g into this wave's staging area (its Lr scratch, done with): 4 tiles, the DMA'd-tile layout
 #pragma unroll
     for (int t = 0; t < WIDTH_COND / TM; ++t) {
@@ -153,12 +170,14 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       view_input(d, dv);
       lds_tile_store(vet + wave * HB_TILE, enc_tile<MODE>(dv, 0, grp, 4));
     }
+    HD_T(3);
     // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles; its last step wraps in the next
     // item's chunk 0
     bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true>(A, lds, sample, xa, xb, 0, D_ZB);
     // sigma's dz: 32 bf16 per wave block in dz_b's ninth tile (hidden_bwd_kernel<true>)
     if (grp == 0) *(__bf16*)(act_ptr<MODE>(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)g4[0];
     // (the chain's steps end in barriers: every wave's dz_g is staged)
+    HD_T(4);
 
     // ---- Lg weight gradient over the item: wave w = bottleneck column tile w (x 4 row tiles), and
     // for w < 4 the (row tile w, ve) tile + row tile w's bias
@@ -189,10 +208,19 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
         }
       }
     }
+    HD_T(5);
   }
   // drain (nothing of ours in flight past here but the wrapped chunk DMA of a non-existent item)
   __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8));
   __syncthreads();
+#ifdef DEN_HEAD_PROF
+  prof[6] = __builtin_amdgcn_s_memtime() - t_start;
+  prof[7] = (n_items - blockIdx.x + gridDim.x - 1) / gridDim.x;
+  if (blockIdx.x < 256 && (threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) den_head_prof[(blockIdx.x * 8 + wave) * 8 + q] = prof[q];
+  }
+#endif
 
   const int lane = threadIdx.x & 63;
   // ---- Lr partial (as render_bwd_kernel<1, 1>), through the weight ring
