@@ -6,6 +6,14 @@
 
 #include "den_geom.h"
 
+// Every hot kernel's code starts on a 4 KiB boundary (r04y A/B); -DDEN_NO_CODE_ALIGN
+// builds the default placement for the instruction-fetch comparison (profiles/gpu_r05pl.sh)
+#ifdef DEN_NO_CODE_ALIGN
+#define DEN_CODE_ALIGN
+#else
+#define DEN_CODE_ALIGN __attribute__((aligned(4096)))
+#endif
+
 namespace den {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

@@ -68,7 +68,7 @@ __device__ __forceinline__ void dws_dma_piece(const char* tile_src, char* dst, i
 
 // U: wave blocks per ring slot (one barrier per U blocks); P.n_blocks / P.per_wg count U-block steps
 template <int MA, int MT, int NB, int NT, int NW, int DEPTH, int U = 1>
-__attribute__((aligned(4096)))  // page-aligned code (r04y A/B)
+DEN_CODE_ALIGN  // page-aligned code (r04y A/B)
 __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
   constexpr int TILES = MT + NT;
   constexpr int BLK = TILES * HB_TILE;              // one wave block's tiles

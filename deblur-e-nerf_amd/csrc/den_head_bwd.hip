@@ -54,7 +54,7 @@ __device__ __forceinline__ void hd_dma_tile(const char* src, char* dst) {
   hd_dma_piece(src + 1024, dst + 1024, 1);
 }
 
-__attribute__((aligned(4096)))  // page-aligned code (r04y A/B)
+DEN_CODE_ALIGN  // page-aligned code (r04y A/B)
 __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A0, float* lg_partial) {
   constexpr int MODE = 1;
   using T = Tr<MODE>;

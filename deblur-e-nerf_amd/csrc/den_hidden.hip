@@ -236,7 +236,7 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
 }
 
 template <bool LB>
-__attribute__((aligned(4096)))  // page-aligned code (r04y A/B)
+DEN_CODE_ALIGN  // page-aligned code (r04y A/B)
 __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P) {
   // HB_RING LDS slots of [dz_l block | S'_{l-1} block]; HB_DEPTH blocks in flight ahead of the one
   // being computed.  Each wave waits for its own part of block b+1 at the end of block b (vmcnt; the

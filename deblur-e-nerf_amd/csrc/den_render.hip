@@ -458,7 +458,7 @@ __device__ __forceinline__ void fwd_layer(const AT& A, char* lds, int slot0, int
 
 // ------------------------------------------------------------------ forward kernel
 template <int MODE, bool TRAIN>
-__attribute__((aligned(4096)))  // page-aligned code (r04y A/B)
+DEN_CODE_ALIGN  // page-aligned code (r04y A/B)
 __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render_fwd_kernel(RenderArgs<MODE> A0) {
   using T = Tr<MODE>;
   using Frag = typename T::Frag;
@@ -948,7 +948,7 @@ __device__ __forceinline__ void head_adjoint(const AT& A, float* rec_lds, int64_
 template <int MODE, int LAST_J>
 // Page-aligned code, as every hot kernel here: the same render_bwd instructions ran 0.1-0.3 ms
 // apart at different code addresses (r04u / r04w / r04y same-box A/B, profiles/r04{w,y}_ab.json)
-__attribute__((aligned(4096)))
+DEN_CODE_ALIGN
 __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) {
   using T = Tr<MODE>;
   using Frag = typename T::Frag;
