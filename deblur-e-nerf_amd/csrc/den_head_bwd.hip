@@ -32,6 +32,10 @@ __device__ uint64_t den_head_prof[256 * 8 * 8];
 #define HD_T(q)
 #endif
 
+#ifndef DEN_HEAD_UT
+#define DEN_HEAD_UT 1  // the Lg^T chain's weight DMA untracked (chunk_step_ut)
+#endif
+
 constexpr int HD_STAGE = 8 * 4 * HB_TILE;  // dz_g of the item: 8 waves x 4 tiles (also each wave's Lr scratch)
 constexpr int HD_XBUF = 2 * HB_TILE;       // per wave: a double buffer of one bottleneck tile
 constexpr int HD_VE = 8 * HB_TILE;         // the item's view-encoding tiles, one per wave block
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     HD_T(3);
     // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles; its last step wraps in the next
     // item's chunk 0
-    bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true>(A, lds, sample, xa, xb, 0, D_ZB);
+    bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true, DEN_HEAD_UT>(A, lds, sample, xa, xb, 0, D_ZB);
     // sigma's dz: 32 bf16 per wave block in dz_b's ninth tile (hidden_bwd_kernel<true>)
     if (grp == 0) *(__bf16*)(act_ptr<MODE>(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)g4[0];
     // (the chain's steps end in barriers: every wave's dz_g is staged)

@@ -67,6 +67,31 @@ __device__ __forceinline__ char* act_ptr(const AT& A, int a, int64_t sample, int
   return A.act[a] + (wb * (act_width(MODE, a) / TM) + tile) * (int64_t)(TM * TM * ES);
 }
 
+// The backward ring's LDS-DMA through inline asm (untracked: the compiler then does not make the
+// chunk's first LDS read wait vmcnt(0) -- i.e. for the DMA of the NEXT chunk, issued just before, and
+// every store in flight).  Returns the DMA instructions this wave issued (wave-uniform).
+__device__ __forceinline__ int dma_chunk_ut(const char* g, char* lds_slot, int bytes) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_assume(wave >= 0 && wave < WG_THREADS / 64);
+  const uint32_t loff = (uint32_t)(threadIdx.x & 63) * 16;
+  int n = 0;
+#pragma unroll
+  for (int q = 0; q < (CHUNK_MAX + WG_THREADS * 16 - 1) / (WG_THREADS * 16); ++q) {
+    const int off = q * WG_THREADS * 16 + wave * 1024;  // wave-uniform
+    if (off < bytes) {
+      const uint64_t a64 = (uint64_t)(uintptr_t)(g + off);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a64);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a64 >> 32));
+      const char* base = (const char*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+      const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(lds_slot + off));
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"(loff), "s"(base), "s"(m0)
+                   : "memory", "m0");
+      ++n;
+    }
+  }
+  return n;
+}
+
 // One chunk step of the pipeline: prefetch chunk (t+1), run `body` on chunk t,
 // publish chunk t+1 into the other ring slot, barrier.
 template <typename Body>
@@ -75,6 +100,25 @@ __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, 
   if (next_bytes > 0) dma_chunk(wbase + next_off, lds + ((t + 1) & 1) * LDS_BUF, next_bytes);
   body(lds + (t & 1) * LDS_BUF);
   __syncthreads();
+}
+// The same with the untracked DMA: chunk t+1 is waited for by count -- all but the n_after
+// vector-memory ops the body issues after it (vmcnt is in-order) -- so the DMA overlaps the body and
+// the stores stay in flight.  n_after must never exceed what the body issues (an under-count only
+// waits longer).
+template <typename Body>
+__device__ __forceinline__ void chunk_step_ut(char* lds, const char* wbase, int t, int64_t next_off, int next_bytes,
+                                              int n_after, Body&& body) {
+  if (next_bytes > 0) dma_chunk_ut(wbase + next_off, lds + ((t + 1) & 1) * LDS_BUF, next_bytes);
+  body(lds + (t & 1) * LDS_BUF);
+  asm volatile("" ::: "memory");
+  switch (n_after) {
+    case 0: __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8)); break;
+    case 1: __builtin_amdgcn_s_waitcnt(1 | (7 << 4) | (0 << 8)); break;
+    default: __builtin_amdgcn_s_waitcnt(2 | (7 << 4) | (0 << 8)); break;
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // ---- forward weight ring: FWD_RING slots of FWD_G row tiles each; chunks t+1 .. t+FWD_RING-1 are in
@@ -761,8 +805,9 @@ struct NoTileHook {
   __device__ __forceinline__ void operator()(int, const Acc&) const {}
 };
 // DZ < 0: the dz tiles stay in registers only (xo), nothing is stored.
-template <int MODE, int LAST_J, int J, int KS, int DER, bool WRAP = false, typename AT, typename Frag,
-          typename Hook = NoTileHook>
+// UT (BF16, DER = 1 only: no activation loads in the body): the untracked-DMA chunk step.
+template <int MODE, int LAST_J, int J, int KS, int DER, bool WRAP = false, bool UT = false, typename AT,
+          typename Frag, typename Hook = NoTileHook>
 __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sample, const Frag* x, Frag* xo, int SA,
                                               int DZ, Hook&& hook = Hook{}) {
   using T = Tr<MODE>;
@@ -791,13 +836,20 @@ __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sa
     int nbytes;
     bwd_next<MODE, LAST_J, WRAP>(J, i, &noff, &nbytes);
     if constexpr (DER == 0) s_cur = load_tile_vals<MODE>(act_ptr<MODE>(A, SA, sample, i));
-    chunk_step(lds, A.w, cb + i, noff, nbytes, [&](const char* chunk) {
+    auto body = [&](const char* chunk) {
       if (i >= 2) store(i - 2);
       Acc acc = acc_zero<MODE>();
       mfma_chunk<MODE, KS>(chunk, x, acc);
       if (i > 0) epilogue(prev, s_prev, i - 1);
       prev = acc;
-    });
+    };
+    if constexpr (UT) {
+      static_assert(DER == 1 && MODE == 1, "the untracked step counts the body's stores only");
+      // the body's ops after the DMA: store(i - 2), two 1 KiB stores (store_tile_frags)
+      chunk_step_ut(lds, A.w, cb + i, noff, nbytes, (i >= 2 && DZ >= 0) ? 2 : 0, body);
+    } else {
+      chunk_step(lds, A.w, cb + i, noff, nbytes, body);
+    }
     s_prev = s_cur;
   }
   epilogue(prev, s_prev, NT - 1);
