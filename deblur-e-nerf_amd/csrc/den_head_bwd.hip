@@ -175,27 +175,19 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       lds_tile_store(vet + wave * HB_TILE, enc_tile<MODE>(dv, 0, grp, 4));
     }
     HD_T(3);
-    // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles; its last step wraps in the next
-    // item's chunk 0
-    bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true, DEN_HEAD_UT>(A, lds, sample, xa, xb, 0, D_ZB);
-    // sigma's dz: 32 bf16 per wave block in dz_b's ninth tile (hidden_bwd_kernel<true>)
-    if (grp == 0) *(__bf16*)(act_ptr<MODE>(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)g4[0];
-    // (the chain's steps end in barriers: every wave's dz_g is staged)
-    HD_T(4);
-
-    // ---- Lg weight gradient over the item: wave w = bottleneck column tile w (x 4 row tiles), and
-    // for w < 4 the (row tile w, ve) tile + row tile w's bias
+    // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles, its last step wrapping in the next
+    // item's chunk 0 -- with the Lg weight gradient's blocks interleaved: step i (i >= 1) runs block
+    // i - 1 (every wave's dz_g and ve tile are published by step 0's barrier) and issues the
+    // bottleneck tile of block i + 1 into the slot block i - 1 used; blocks 0 and 1 are issued here,
+    // block 7 runs after the chain.  A block's tile is issued two steps before its use, and each
+    // step's counted wait (the next weight chunk, issued after it) covers it: vmcnt is in-order.
+    // Wave w = bottleneck column tile w (x 4 row tiles), and for w < 4 the (row tile w, ve) tile +
+    // row tile w's bias.
     const int64_t wb0 = item * (WGS / TM);  // the item's first wave block
     auto bt_src = [&](int b) { return A.act[A_BT] + ((wb0 + b) * (WIDTH / TM) + wave) * (int64_t)HB_TILE; };
     hd_dma_tile(bt_src(0), xbuf);
-#pragma unroll 1
-    for (int b = 0; b < 8; ++b) {
-      if (b + 1 < 8) hd_dma_tile(bt_src(b + 1), xbuf + ((b + 1) & 1) * HB_TILE);
-      // block b's two pieces landed (only block b + 1's two may stay in flight; vmcnt is in-order)
-      asm volatile("" ::: "memory");
-      if (b + 1 < 8) __builtin_amdgcn_s_waitcnt((2 & 15) | (7 << 4) | (0 << 8));  // vmcnt(2) lgkmcnt(0)
-      else __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8));                  // vmcnt(0) lgkmcnt(0)
-      asm volatile("" ::: "memory");
+    hd_dma_tile(bt_src(1), xbuf + HB_TILE);
+    auto dw_block = [&](int b) {
       const char* xt = xbuf + (b & 1) * HB_TILE;
       const char* zt = stage + b * (4 * HB_TILE);  // wave b's dz_g tiles = wave block b of the item
 #pragma unroll
@@ -211,7 +203,24 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
           for (int e = 0; e < 8; ++e) gdb += (float)a[e];
         }
       }
-    }
+    };
+    auto lg_step = [&](int i) -> int {
+      if (i < 1) return 0;
+      dw_block(i - 1);
+      if (i + 1 >= 8) return 0;
+      // the slot's previous tile (block i - 1) is consumed: its reads fed the MFMAs above
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt / expcnt untouched
+      asm volatile("" ::: "memory");
+      hd_dma_tile(bt_src(i + 1), xbuf + ((i + 1) & 1) * HB_TILE);
+      return 2;
+    };
+    bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true, true>(A, lds, sample, xa, xb, 0, D_ZB, NoTileHook{},
+                                                                 lg_step);
+    // sigma's dz: 32 bf16 per wave block in dz_b's ninth tile (hidden_bwd_kernel<true>)
+    if (grp == 0) *(__bf16*)(act_ptr<MODE>(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)g4[0];
+    HD_T(4);
+    // block 7 (its tile was issued in step 5; step 7's wait covered it)
+    dw_block(7);
     HD_T(5);
   }
   // drain (nothing of ours in flight past here but the wrapped chunk DMA of a non-existent item)

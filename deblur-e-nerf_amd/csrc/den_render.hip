@@ -105,16 +105,19 @@ __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, 
 // vector-memory ops the body issues after it (vmcnt is in-order) -- so the DMA overlaps the body and
 // the stores stay in flight.  n_after must never exceed what the body issues (an under-count only
 // waits longer).
+// (body returns the vector-memory ops it issued; at most 4 are left in flight.)
 template <typename Body>
 __device__ __forceinline__ void chunk_step_ut(char* lds, const char* wbase, int t, int64_t next_off, int next_bytes,
-                                              int n_after, Body&& body) {
+                                              Body&& body) {
   if (next_bytes > 0) dma_chunk_ut(wbase + next_off, lds + ((t + 1) & 1) * LDS_BUF, next_bytes);
-  body(lds + (t & 1) * LDS_BUF);
+  const int n_after = body(lds + (t & 1) * LDS_BUF);
   asm volatile("" ::: "memory");
   switch (n_after) {
     case 0: __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8)); break;
     case 1: __builtin_amdgcn_s_waitcnt(1 | (7 << 4) | (0 << 8)); break;
-    default: __builtin_amdgcn_s_waitcnt(2 | (7 << 4) | (0 << 8)); break;
+    case 2: __builtin_amdgcn_s_waitcnt(2 | (7 << 4) | (0 << 8)); break;
+    case 3: __builtin_amdgcn_s_waitcnt(3 | (7 << 4) | (0 << 8)); break;
+    default: __builtin_amdgcn_s_waitcnt(4 | (7 << 4) | (0 << 8)); break;
   }
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -804,12 +807,17 @@ struct NoTileHook {
   template <typename Acc>
   __device__ __forceinline__ void operator()(int, const Acc&) const {}
 };
+// UT steps: work of step i run after its MFMAs (returns the vector-memory ops it issued)
+struct NoStepHook {
+  __device__ __forceinline__ int operator()(int) const { return 0; }
+};
 // DZ < 0: the dz tiles stay in registers only (xo), nothing is stored.
-// UT (BF16, DER = 1 only: no activation loads in the body): the untracked-DMA chunk step.
+// UT (BF16, DER = 1 only: no activation loads in the body): the untracked-DMA chunk step, with
+// `shook` run in each step after its MFMAs.
 template <int MODE, int LAST_J, int J, int KS, int DER, bool WRAP = false, bool UT = false, typename AT,
-          typename Frag, typename Hook = NoTileHook>
+          typename Frag, typename Hook = NoTileHook, typename StepHook = NoStepHook>
 __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sample, const Frag* x, Frag* xo, int SA,
-                                              int DZ, Hook&& hook = Hook{}) {
+                                              int DZ, Hook&& hook = Hook{}, StepHook&& shook = StepHook{}) {
   using T = Tr<MODE>;
   using Acc = typename T::Acc;
   constexpr int NT = bwd_tiles(MODE, J);
@@ -845,8 +853,12 @@ __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sa
     };
     if constexpr (UT) {
       static_assert(DER == 1 && MODE == 1, "the untracked step counts the body's stores only");
-      // the body's ops after the DMA: store(i - 2), two 1 KiB stores (store_tile_frags)
-      chunk_step_ut(lds, A.w, cb + i, noff, nbytes, (i >= 2 && DZ >= 0) ? 2 : 0, body);
+      // the body's ops after the DMA: store(i - 2), two 1 KiB stores (store_tile_frags), and the
+      // step hook's
+      chunk_step_ut(lds, A.w, cb + i, noff, nbytes, [&](const char* chunk) -> int {
+        body(chunk);
+        return ((i >= 2 && DZ >= 0) ? 2 : 0) + shook(i);
+      });
     } else {
       chunk_step(lds, A.w, cb + i, noff, nbytes, body);
     }
