@@ -155,7 +155,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     Frag xa[KS + 2 * FPT], xb[KS + 2 * FPT];
     // j=0 Lr^T: dz_r -> dz_g in registers (xa, 4 tiles; stored only for den_render_ray_grad) + the
     // fused Lr weight gradient
-    bwd_layer_run<MODE, 1, 0, FPT, 0, true>(A, lds, sample, fr, xa, A_G, A.keep_dzg ? D_ZG : -1, lr_hook);
+    bwd_layer_run<MODE, 1, 0, FPT, 0, true, true>(A, lds, sample, fr, xa, A_G, A.keep_dzg ? D_ZG : -1, lr_hook);
     HD_T(2);
     // dz_g into this wave's staging area (its Lr scratch, done with): 4 tiles, the DMA'd-tile layout
 #pragma unroll

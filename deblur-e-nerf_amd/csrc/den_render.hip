@@ -812,8 +812,8 @@ struct NoStepHook {
   __device__ __forceinline__ int operator()(int) const { return 0; }
 };
 // DZ < 0: the dz tiles stay in registers only (xo), nothing is stored.
-// UT (BF16, DER = 1 only: no activation loads in the body): the untracked-DMA chunk step, with
-// `shook` run in each step after its MFMAs.
+// UT (BF16): the untracked-DMA chunk step, with `shook` run in each step after its MFMAs (DER = 0:
+// the activations preloaded, PRE below).
 template <int MODE, int LAST_J, int J, int KS, int DER, bool WRAP = false, bool UT = false, typename AT,
           typename Frag, typename Hook = NoTileHook, typename StepHook = NoStepHook>
 __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sample, const Frag* x, Frag* xo, int SA,
@@ -838,21 +838,52 @@ __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sa
   auto store = [&](int i) {
     if (DZ >= 0) store_tile_frags<MODE>(act_ptr<MODE>(A, DZ, sample, i), xo + i * FPT);
   };
+  // UT with DER = 0 (the head's Lr^T chain, 4 tiles): every tile's stored activation is loaded up
+  // front, packed (8 dwords per tile, unpacked at its epilogue), so no activation load sits inside the
+  // untracked steps (their counted waits would not know it) and the four HBM round trips overlap
+  constexpr bool PRE = UT && DER == 0;
+  static_assert(!PRE || (MODE == 1 && NT <= 4), "the preloaded activations: BF16, at most 4 tiles");
+  uint4 sraw[PRE ? NT : 1][2];
+  // (unpacked where its epilogue reads it: the compiler's wait for the load then sits there)
+  auto sval = [&](int i) -> Acc {
+    Acc a;
+    if constexpr (PRE) {
+      const uint32_t w[8] = {sraw[i][0].x, sraw[i][0].y, sraw[i][0].z, sraw[i][0].w,
+                             sraw[i][1].x, sraw[i][1].y, sraw[i][1].z, sraw[i][1].w};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        a[2 * q] = __uint_as_float(w[q] << 16);
+        a[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+      }
+    }
+    return a;
+  };
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const char* p = act_ptr<MODE>(A, SA, sample, i) + (threadIdx.x & 63) * 16;
+      sraw[i][0] = ld_stream((const uint4*)p);
+      sraw[i][1] = ld_stream((const uint4*)(p + 1024));
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     int64_t noff;
     int nbytes;
     bwd_next<MODE, LAST_J, WRAP>(J, i, &noff, &nbytes);
-    if constexpr (DER == 0) s_cur = load_tile_vals<MODE>(act_ptr<MODE>(A, SA, sample, i));
+    if constexpr (DER == 0 && !PRE) s_cur = load_tile_vals<MODE>(act_ptr<MODE>(A, SA, sample, i));
     auto body = [&](const char* chunk) {
       if (i >= 2) store(i - 2);
       Acc acc = acc_zero<MODE>();
       mfma_chunk<MODE, KS>(chunk, x, acc);
-      if (i > 0) epilogue(prev, s_prev, i - 1);
+      if (i > 0) {
+        if constexpr (PRE) epilogue(prev, sval(i - 1), i - 1);
+        else epilogue(prev, s_prev, i - 1);
+      }
       prev = acc;
     };
     if constexpr (UT) {
-      static_assert(DER == 1 && MODE == 1, "the untracked step counts the body's stores only");
+      static_assert(MODE == 1, "the untracked step counts the body's stores only (no loads: PRE)");
       // the body's ops after the DMA: store(i - 2), two 1 KiB stores (store_tile_frags), and the
       // step hook's
       chunk_step_ut(lds, A.w, cb + i, noff, nbytes, [&](const char* chunk) -> int {
@@ -862,9 +893,10 @@ __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sa
     } else {
       chunk_step(lds, A.w, cb + i, noff, nbytes, body);
     }
-    s_prev = s_cur;
+    if constexpr (!PRE) s_prev = s_cur;
   }
-  epilogue(prev, s_prev, NT - 1);
+  if constexpr (PRE) epilogue(prev, sval(NT - 1), NT - 1);
+  else epilogue(prev, s_prev, NT - 1);
   if constexpr (NT >= 2) store(NT - 2);
   store(NT - 1);
 }
