@@ -78,7 +78,8 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
   char* vet = stage + HD_STAGE + 8 * HD_XBUF;  // ve tiles of the item's 8 wave blocks
 
   // first item's weight chunk 0 (later items: wrapped in by the previous item's last chain step)
-  dma_chunk(A0.w, lds, chunk_bytes_K(bwd_K(MODE, 0)));
+  dma_chunk(A0.w, lds, bwd_tiles(MODE, 0) * chunk_bytes_K(bwd_K(MODE, 0)));  // all of Lr^T: one chunk
+  int gc = 0;  // ring index of the item's Lr^T chunk (then Lg^T's 8)
 
   f32x16 lacc;  // dW_r (the fused Lr weight gradient), as render_bwd_kernel<1, 1>
   f32x16 gacc[5];  // dW_g: [0..3] = (row tile mt, column tile wave); [4] = (row tile wave, ve) for waves < 4
@@ -155,7 +156,8 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     Frag xa[KS + 2 * FPT], xb[KS + 2 * FPT];
     // j=0 Lr^T: dz_r -> dz_g in registers (xa, 4 tiles; stored only for den_render_ray_grad) + the
     // fused Lr weight gradient
-    bwd_layer_run<MODE, 1, 0, FPT, 0, true, true>(A, lds, sample, fr, xa, A_G, A.keep_dzg ? D_ZG : -1, lr_hook);
+    bwd_layer_run<MODE, 1, 0, FPT, 0, true, true, true>(A, lds, sample, fr, xa, A_G, A.keep_dzg ? D_ZG : -1, lr_hook,
+                                                         NoStepHook{}, gc);
     HD_T(2);
     // dz_g into this wave's staging area (its Lr scratch, done with): 4 tiles, the DMA'd-tile layout
 #pragma unroll
@@ -214,8 +216,9 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       hd_dma_tile(bt_src(i + 1), xbuf + ((i + 1) & 1) * HB_TILE);
       return 2;
     };
-    bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true, true>(A, lds, sample, xa, xb, 0, D_ZB, NoTileHook{},
-                                                                 lg_step);
+    bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true, true, true>(A, lds, sample, xa, xb, 0, D_ZB, NoTileHook{},
+                                                                       lg_step, gc + 1);
+    gc += 1 + bwd_tiles(MODE, 1);
     // sigma's dz: 32 bf16 per wave block in dz_b's ninth tile (hidden_bwd_kernel<true>)
     if (grp == 0) *(__bf16*)(act_ptr<MODE>(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)g4[0];
     HD_T(4);

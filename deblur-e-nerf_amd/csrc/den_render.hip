@@ -300,7 +300,8 @@ __device__ __forceinline__ int fwd_slot(int slot0, int gc) {
 }
 
 // WRAP (persistent kernels): past the last chunk the stream wraps to chunk 0, the next item's
-template <int MODE, int LAST_J, bool WRAP = false>
+// W0: layer 0's tiles travel as ONE chunk (the head backward's Lr^T, 4 x 2 KiB)
+template <int MODE, int LAST_J, bool WRAP = false, bool W0 = false>
 __device__ __forceinline__ void bwd_next(int j, int i, int64_t* off, int* bytes) {
   int nj = j, ni = i + 1;
   if (ni >= bwd_tiles(MODE, j)) { nj = j + 1; ni = 0; }
@@ -310,6 +311,7 @@ __device__ __forceinline__ void bwd_next(int j, int i, int64_t* off, int* bytes)
   }
   *bytes = chunk_bytes_K(bwd_K(MODE, nj));
   *off = bwd_layer_offset(MODE, nj) + (int64_t)ni * *bytes;
+  if (W0 && nj == 0) *bytes *= bwd_tiles(MODE, 0);
 }
 
 // ------------------------------------------------------------------ forward layer
@@ -814,16 +816,22 @@ struct NoStepHook {
 // DZ < 0: the dz tiles stay in registers only (xo), nothing is stored.
 // UT (BF16): the untracked-DMA chunk step, with `shook` run in each step after its MFMAs (DER = 0:
 // the activations preloaded, PRE below).
-template <int MODE, int LAST_J, int J, int KS, int DER, bool WRAP = false, bool UT = false, typename AT,
-          typename Frag, typename Hook = NoTileHook, typename StepHook = NoStepHook>
+// W0 (with UT): layer 0 travels as one chunk -- J = 0 reads all its tiles from one ring slot with
+// no step in between (one wait + barrier after the last tile, for the next layer's first chunk,
+// issued at tile 0); J > 0 wraps to the whole layer 0.  t0: the ring index of the layer's first
+// chunk (default: its index in a per-item stream of one chunk per tile).
+template <int MODE, int LAST_J, int J, int KS, int DER, bool WRAP = false, bool UT = false, bool W0 = false,
+          typename AT, typename Frag, typename Hook = NoTileHook, typename StepHook = NoStepHook>
 __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sample, const Frag* x, Frag* xo, int SA,
-                                              int DZ, Hook&& hook = Hook{}, StepHook&& shook = StepHook{}) {
+                                              int DZ, Hook&& hook = Hook{}, StepHook&& shook = StepHook{}, int t0 = -1) {
   using T = Tr<MODE>;
   using Acc = typename T::Acc;
   constexpr int NT = bwd_tiles(MODE, J);
   constexpr int FPT = T::FPT;
+  static_assert(!W0 || UT, "the whole-layer-0 chunk runs on the untracked step");
   int cb = 0;
   for (int jj = 0; jj < J; ++jj) cb += bwd_tiles(MODE, jj);
+  if (t0 >= 0) cb = t0;
   Acc prev, s_prev, s_cur;
   // hook(i, stored activation of tile i): run in tile i's epilogue, when the load has landed
   auto epilogue = [&](Acc& acc, const Acc& sv, int i) {
@@ -870,7 +878,13 @@ __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sa
   for (int i = 0; i < NT; ++i) {
     int64_t noff;
     int nbytes;
-    bwd_next<MODE, LAST_J, WRAP>(J, i, &noff, &nbytes);
+    if constexpr (W0 && J == 0) {
+      // the next layer's first chunk, issued with tile 0
+      bwd_next<MODE, LAST_J, WRAP, W0>(J, NT - 1, &noff, &nbytes);
+      if (i != 0) nbytes = 0;
+    } else {
+      bwd_next<MODE, LAST_J, WRAP, W0>(J, i, &noff, &nbytes);
+    }
     if constexpr (DER == 0 && !PRE) s_cur = load_tile_vals<MODE>(act_ptr<MODE>(A, SA, sample, i));
     auto body = [&](const char* chunk) {
       if (i >= 2) store(i - 2);
@@ -882,7 +896,19 @@ __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sa
       }
       prev = acc;
     };
-    if constexpr (UT) {
+    if constexpr (UT && W0 && J == 0) {
+      if (nbytes > 0) dma_chunk_ut(A.w + noff, lds + ((cb + 1) & 1) * LDS_BUF, nbytes);
+      body(lds + (cb & 1) * LDS_BUF + i * chunk_bytes_K(bwd_K(MODE, J)));
+      (void)shook(i);
+      if (i == NT - 1) {
+        // the next layer's first chunk landed (every older op too); the barrier publishes it
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8));
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    } else if constexpr (UT) {
       static_assert(MODE == 1, "the untracked step counts the body's stores only (no loads: PRE)");
       // the body's ops after the DMA: store(i - 2), two 1 KiB stores (store_tile_frags), and the
       // step hook's
