@@ -58,6 +58,149 @@ __device__ __forceinline__ void hd_dma_tile(const char* src, char* dst) {
   hd_dma_piece(src + 1024, dst + 1024, 1);
 }
 
+// The compositing adjoint's inputs one item ahead (fixed-count sampler).  Its first global load
+// waited for every older memory op of the wave -- vmcnt is in-order -- i.e. for the previous item's
+// dz_b stores to drain: 7.6 k cycles per item while six of the eight waves waited (r05 head
+// profile).  The next item's per-sample records (4 KiB, waves 0..3, one 1 KiB LDS-DMA each, into
+// rec_lds where the adjoint writes its results in place) and its rays' data (wave 4, one dword per
+// lane: per ray o, d, jitter, d_rgb, d_opacity, d_depth = 12 floats, then bkgd) are DMA'd during
+// the current item's first Lg^T step; that step's successors' counted waits cover them.
+constexpr int HD_NRAY = 256;
+template <typename AT>
+__device__ __forceinline__ int hd_stage_adjoint(const AT& A, int64_t nx, int wave, char* rec_lds, float* nray) {
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
+  constexpr int WGS = wg_samples(1);
+  if (wave < 4) {
+    // linear: lane l's 16 B (sample nx WGS + 64 wave + l) at rec_lds + 1024 wave + 16 l
+    const uint64_t a64 = (uint64_t)(uintptr_t)((const char*)A.rec + (nx * WGS + wave * 64) * 16);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a64);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a64 >> 32));
+    const char* base = (const char*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(rec_lds + wave * 1024));
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"((uint32_t)lane * 16),
+                 "s"(base), "s"(m0) : "memory", "m0");
+    return 1;
+  }
+  if (wave != 4) return 0;
+  const int rpw = WGS / A.n_samples;
+  const float* dummy = A.rays_o;
+  const float* src = dummy;
+  if (lane < 12 * rpw) {
+    const int q = lane / 12, e = lane - 12 * q;
+    const int64_t r = nx * rpw + q;
+    if (e < 3) src = A.rays_o + r * 3 + e;
+    else if (e < 6) src = A.rays_d + r * 3 + (e - 3);
+    else if (e == 6) src = A.jitter + r;
+    else if (e < 10) src = (e - 7 < A.rd) ? A.d_rgb + r * A.rd + (e - 7) : dummy;
+    else if (e == 10) src = A.d_opacity ? A.d_opacity + r : dummy;
+    else src = A.d_depth ? A.d_depth + r : dummy;
+  } else if (lane >= 48 && lane < 51) {
+    src = (A.has_bkgd && lane - 48 < A.rd) ? A.bkgd + (lane - 48) : dummy;
+  }
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)nray);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" : : "v"(src), "s"(m0) : "memory", "m0");
+  return 1;
+}
+
+// head_adjoint (den_render.hip, points = 0) on the staged inputs: the records from rec_lds (each
+// lane reads its own samples before it overwrites them with the results), the ray data from nray
+template <typename AT>
+__device__ __forceinline__ void head_adjoint_staged(const AT& A, float* rec_lds, const float* nray, int64_t item,
+                                                    int wave, int lane) {
+  constexpr int WGS = wg_samples(1);
+  const int rays_per_wg = WGS / A.n_samples;
+  if (wave >= rays_per_wg) return;
+  const int64_t r = item * rays_per_wg + wave;
+  const float* nr = nray + wave * 12;
+  float ro[3], rdv[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    ro[a] = nr[a];
+    rdv[a] = nr[3 + a];
+  }
+  float aabb[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) aabb[q] = A.aabb[q];
+  RayGeom rg = ray_geom(ro, rdv, aabb, A.near_p, A.far_p);
+  const float ru = nr[6];
+  const int spl = A.n_samples / 64;
+  float dC[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch)
+    if (ch < A.rd) dC[ch] = nr[7 + ch];
+  const float dO = A.d_opacity ? nr[10] : 0.0f;
+  const float dD = A.d_depth ? nr[11] : 0.0f;
+  float bk_dot = 0.0f;
+  if (A.has_bkgd)
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+      if (ch < A.rd) bk_dot += dC[ch] * nray[48 + ch];
+  float tau[4], tmid[4], dlt[4], loc[4], locx[4], sg4[4], rc4[4][3];
+  float run = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= spl) break;
+    const int kk = lane * spl + q;
+    float a0, a1;
+    sample_interval(rg, kk, ru, A.n_samples, &a0, &a1);
+    const f32x4 rv = *(const f32x4*)(rec_lds + (wave * A.n_samples + kk) * 4);
+    sg4[q] = rv[0];
+    rc4[q][0] = rv[1];
+    rc4[q][1] = rv[2];
+    rc4[q][2] = rv[3];
+    dlt[q] = a1 - a0;
+    tau[q] = (a1 > a0) ? rv[0] * dlt[q] : 0.0f;
+    tmid[q] = (a0 + a1) / 2.0f;
+    locx[q] = run;
+    run += tau[q];
+    loc[q] = run;
+  }
+  const float base = wave_excl_scan(run);
+  float w[4], gv[4], op_part = 0.0f, wg_run = 0.0f, wgq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= spl) break;
+    w[q] = expf(-(base + locx[q])) * (1.0f - expf(-tau[q]));
+    op_part += w[q];
+  }
+  const float opacity = wave_sum(op_part);
+  const float dO_eff = dO - bk_dot;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= spl) break;
+    gv[q] = dC[0] * rc4[q][0] + dC[1] * rc4[q][1] + dC[2] * rc4[q][2] + dO_eff + dD * tmid[q];
+    wgq[q] = w[q] * gv[q];
+    wg_run += wgq[q];
+  }
+  const float wg_suf_incl = wave_incl_suffix(wg_run);
+  const float wg_after = __shfl_down(wg_suf_incl, 1, 64);
+  float sfx[4] = {0.f, 0.f, 0.f, 0.f}, later = lane < 63 ? wg_after : 0.0f;
+#pragma unroll
+  for (int q = 3; q >= 0; --q) {
+    if (q >= spl) continue;
+    sfx[q] = later;
+    later += wgq[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= spl) break;
+    const int kk = lane * spl + q;
+    const float Tnext = expf(-(base + loc[q]));
+    const float dtau = Tnext * gv[q] - sfx[q];
+    const float dsig = dtau * dlt[q];
+    const float dsig_raw = dsig * density_dact_from_out(sg4[q], A.density_act);
+    const f32x4 o4 = {dsig_raw, w[q] * dC[0] * (-expm1f(-rc4[q][0])), w[q] * dC[1] * (-expm1f(-rc4[q][1])),
+                      w[q] * dC[2] * (-expm1f(-rc4[q][2]))};
+    *(f32x4*)(rec_lds + (wave * A.n_samples + kk) * 4) = o4;
+  }
+  if (lane == 0 && A.bkgd_partial) {
+    for (int ch = 0; ch < 3; ++ch)
+      A.bkgd_partial[(int64_t)ch * A.n_rays + r] = (ch < A.rd && A.has_bkgd) ? dC[ch] * (1.0f - opacity) : 0.0f;
+  }
+}
+
 DEN_CODE_ALIGN  // page-aligned code (r04y A/B)
 __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A0, float* lg_partial) {
   constexpr int MODE = 1;
@@ -66,7 +209,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
   using Acc = typename T::Acc;
   constexpr int TM = T::TM, FPT = T::FPT;
   constexpr int WGS = wg_samples(MODE);
-  constexpr int LDS_BYTES = 2 * LDS_BUF + WGS * 16 + HD_STAGE + 8 * HD_XBUF + HD_VE;
+  constexpr int LDS_BYTES = 2 * LDS_BUF + WGS * 16 + HD_STAGE + 8 * HD_XBUF + HD_VE + HD_NRAY;
   static_assert(LDS_BYTES <= 160 * 1024, "the head kernel's LDS exceeds the CU's");
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   float* rec_lds = (float*)(lds + 2 * LDS_BUF);
@@ -76,10 +219,17 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
   char* xbuf = stage + HD_STAGE + wave * HD_XBUF;
   char* lscr = stage + wave * (4 * HB_TILE);  // this wave's Lr scratch = its own dz_g staging area
   char* vet = stage + HD_STAGE + 8 * HD_XBUF;  // ve tiles of the item's 8 wave blocks
+  float* nray = (float*)(vet + HD_VE);         // the next item's ray data (hd_stage_adjoint)
 
   // first item's weight chunk 0 (later items: wrapped in by the previous item's last chain step)
   dma_chunk(A0.w, lds, bwd_tiles(MODE, 0) * chunk_bytes_K(bwd_K(MODE, 0)));  // all of Lr^T: one chunk
   int gc = 0;  // ring index of the item's Lr^T chunk (then Lg^T's 8)
+  if (A0.points == 0 && (int64_t)blockIdx.x < (int64_t)A0.n_rays * A0.n_samples / WGS) {
+    // the first item's adjoint inputs (later items': staged by the previous item)
+    hd_stage_adjoint(A0, blockIdx.x, wave, (char*)rec_lds, nray);
+    __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8));  // vmcnt(0) lgkmcnt(0)
+    __syncthreads();
+  }
 
   f32x16 lacc;  // dW_r (the fused Lr weight gradient), as render_bwd_kernel<1, 1>
   f32x16 gacc[5];  // dW_g: [0..3] = (row tile mt, column tile wave); [4] = (row tile wave, ve) for waves < 4
@@ -109,7 +259,8 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     const int lane = tid & 63, c = lane % TM, grp = lane / TM;
     const int64_t sample = item * WGS + wave * TM + c;
 
-    head_adjoint<MODE>(A, rec_lds, item, sample, wave, lane, c, grp);
+    if (A.points == 0) head_adjoint_staged(A, rec_lds, nray, item, wave, lane);
+    else head_adjoint<MODE>(A, rec_lds, item, sample, wave, lane, c, grp);
     HD_T(0);
     __syncthreads();  // also: every wave is done with the previous item's staged dz_g
     HD_T(1);
@@ -207,14 +358,19 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       }
     };
     auto lg_step = [&](int i) -> int {
-      if (i < 1) return 0;
+      if (i < 1) {
+        // the next item's adjoint inputs (rec_lds and nray are free: read before the Lr^T chain)
+        const int64_t nx = item + gridDim.x;
+        return (A.points == 0 && nx < n_items) ? hd_stage_adjoint(A, nx, wave, (char*)rec_lds, nray) : 0;
+      }
       dw_block(i - 1);
-      if (i + 1 >= 8) return 0;
+      int n = 0;
+      if (i + 1 >= 8) return n;
       // the slot's previous tile (block i - 1) is consumed: its reads fed the MFMAs above
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt / expcnt untouched
       asm volatile("" ::: "memory");
       hd_dma_tile(bt_src(i + 1), xbuf + ((i + 1) & 1) * HB_TILE);
-      return 2;
+      return n + 2;
     };
     bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true, true, true>(A, lds, sample, xa, xb, 0, D_ZB, NoTileHook{},
                                                                        lg_step, gc + 1);

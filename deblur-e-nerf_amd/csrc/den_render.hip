@@ -105,7 +105,7 @@ __device__ __forceinline__ void chunk_step(char* lds, const char* wbase, int t, 
 // vector-memory ops the body issues after it (vmcnt is in-order) -- so the DMA overlaps the body and
 // the stores stay in flight.  n_after must never exceed what the body issues (an under-count only
 // waits longer).
-// (body returns the vector-memory ops it issued; at most 4 are left in flight.)
+// (body returns the vector-memory ops it issued; at most 5 are left in flight.)
 template <typename Body>
 __device__ __forceinline__ void chunk_step_ut(char* lds, const char* wbase, int t, int64_t next_off, int next_bytes,
                                               Body&& body) {
@@ -117,7 +117,8 @@ __device__ __forceinline__ void chunk_step_ut(char* lds, const char* wbase, int 
     case 1: __builtin_amdgcn_s_waitcnt(1 | (7 << 4) | (0 << 8)); break;
     case 2: __builtin_amdgcn_s_waitcnt(2 | (7 << 4) | (0 << 8)); break;
     case 3: __builtin_amdgcn_s_waitcnt(3 | (7 << 4) | (0 << 8)); break;
-    default: __builtin_amdgcn_s_waitcnt(4 | (7 << 4) | (0 << 8)); break;
+    case 4: __builtin_amdgcn_s_waitcnt(4 | (7 << 4) | (0 << 8)); break;
+    default: __builtin_amdgcn_s_waitcnt(5 | (7 << 4) | (0 << 8)); break;
   }
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
