@@ -107,8 +107,8 @@ __device__ __forceinline__ int hd_stage_adjoint(const AT& A, int64_t nx, int wav
 // head_adjoint (den_render.hip, points = 0) on the staged inputs: the records from rec_lds (each
 // lane reads its own samples before it overwrites them with the results), the ray data from nray
 template <typename AT>
-__device__ __forceinline__ void head_adjoint_staged(const AT& A, float* rec_lds, const float* nray, int64_t item,
-                                                    int wave, int lane) {
+__device__ __forceinline__ void head_adjoint_staged(const AT& A, float* rec_lds, const float* nray, const float* bk,
+                                                    int64_t item, int wave, int lane) {
   constexpr int WGS = wg_samples(1);
   const int rays_per_wg = WGS / A.n_samples;
   if (wave >= rays_per_wg) return;
@@ -136,7 +136,7 @@ __device__ __forceinline__ void head_adjoint_staged(const AT& A, float* rec_lds,
   if (A.has_bkgd)
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch)
-      if (ch < A.rd) bk_dot += dC[ch] * nray[48 + ch];
+      if (ch < A.rd) bk_dot += dC[ch] * bk[ch];
   float tau[4], tmid[4], dlt[4], loc[4], locx[4], sg4[4], rc4[4][3];
   float run = 0.0f;
 #pragma unroll
@@ -259,10 +259,28 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     const int lane = tid & 63, c = lane % TM, grp = lane / TM;
     const int64_t sample = item * WGS + wave * TM + c;
 
-    if (A.points == 0) head_adjoint_staged(A, rec_lds, nray, item, wave, lane);
+    // the Lr^T chain's stored G tiles, issued before the adjoint (which reads only LDS now, so
+    // nothing waits behind them): their HBM round trip overlaps it
+    // (the background colour read first: the compiler puts a full vmcnt(0) before that LDS read)
+    float bk[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) bk[ch] = nray[48 + ch];
+    uint4 graw[WIDTH_COND / TM][2];
+#pragma unroll
+    for (int t = 0; t < WIDTH_COND / TM; ++t) {
+      const char* p = act_ptr<MODE>(A, A_G, sample, t) + lane * 16;
+      graw[t][0] = ld_stream((const uint4*)p);
+      graw[t][1] = ld_stream((const uint4*)(p + 1024));
+    }
+    if (A.points == 0) head_adjoint_staged(A, rec_lds, nray, bk, item, wave, lane);
     else head_adjoint<MODE>(A, rec_lds, item, sample, wave, lane, c, grp);
     HD_T(0);
-    __syncthreads();  // also: every wave is done with the previous item's staged dz_g
+    // also: every wave is done with the previous item's staged dz_g.  LDS only (__syncthreads'
+    // release fence would wait out the G loads above too)
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     HD_T(1);
 
     // fake dz tiles from the per-sample raw gradients (render_bwd_kernel<1, 1>)
@@ -308,7 +326,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     // j=0 Lr^T: dz_r -> dz_g in registers (xa, 4 tiles; stored only for den_render_ray_grad) + the
     // fused Lr weight gradient
     bwd_layer_run<MODE, 1, 0, FPT, 0, true, true, true>(A, lds, sample, fr, xa, A_G, A.keep_dzg ? D_ZG : -1, lr_hook,
-                                                         NoStepHook{}, gc);
+                                                         NoStepHook{}, gc, graw);
     HD_T(2);
     // dz_g into this wave's staging area (its Lr scratch, done with): 4 tiles, the DMA'd-tile layout
 #pragma unroll

@@ -824,7 +824,8 @@ struct NoStepHook {
 template <int MODE, int LAST_J, int J, int KS, int DER, bool WRAP = false, bool UT = false, bool W0 = false,
           typename AT, typename Frag, typename Hook = NoTileHook, typename StepHook = NoStepHook>
 __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sample, const Frag* x, Frag* xo, int SA,
-                                              int DZ, Hook&& hook = Hook{}, StepHook&& shook = StepHook{}, int t0 = -1) {
+                                              int DZ, Hook&& hook = Hook{}, StepHook&& shook = StepHook{}, int t0 = -1,
+                                              const uint4 (*pre_in)[2] = nullptr) {
   using T = Tr<MODE>;
   using Acc = typename T::Acc;
   constexpr int NT = bwd_tiles(MODE, J);
@@ -852,6 +853,7 @@ __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sa
   // untracked steps (their counted waits would not know it) and the four HBM round trips overlap
   constexpr bool PRE = UT && DER == 0;
   static_assert(!PRE || (MODE == 1 && NT <= 4), "the preloaded activations: BF16, at most 4 tiles");
+  // (pre_in: the caller issued these loads itself, earlier)
   uint4 sraw[PRE ? NT : 1][2];
   // (unpacked where its epilogue reads it: the compiler's wait for the load then sits there)
   auto sval = [&](int i) -> Acc {
@@ -870,9 +872,14 @@ __device__ __forceinline__ void bwd_layer_run(const AT& A, char* lds, int64_t sa
   if constexpr (PRE) {
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-      const char* p = act_ptr<MODE>(A, SA, sample, i) + (threadIdx.x & 63) * 16;
-      sraw[i][0] = ld_stream((const uint4*)p);
-      sraw[i][1] = ld_stream((const uint4*)(p + 1024));
+      if (pre_in) {
+        sraw[i][0] = pre_in[i][0];
+        sraw[i][1] = pre_in[i][1];
+      } else {
+        const char* p = act_ptr<MODE>(A, SA, sample, i) + (threadIdx.x & 63) * 16;
+        sraw[i][0] = ld_stream((const uint4*)p);
+        sraw[i][1] = ld_stream((const uint4*)(p + 1024));
+      }
     }
   }
 #pragma unroll
