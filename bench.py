@@ -194,13 +194,13 @@ BF16_KERNEL_NAMES = {"render_bwd_kernel": "render_head_bwd_kernel", "dw_gemm_ker
 # algorithmic HBM bytes per sample and STEP of each BF16 kernel:
 #   hidden_bwd: L7..L1 each read dz_l + a_(l-1) and write dz_(l-1), 256 bf16 each = 1536 B;
 #   hidden_bwd_lb: reads dz_b (257 bf16) + S7, writes dz_7 = 1538 B;
-#   render_fwd: the activations + record it stores for the backward, S0..S7 + bottleneck + G + record
-#     (4096 + 512 + 256 + 16 B; pe / ve are recomputed by the backward, not stored);
+#   render_fwd: the activations + record it stores for the backward, S0..S7 + bottleneck + G + pe +
+#     record (4096 + 512 + 256 + 128 + 16 B; ve is recomputed by the head backward, not stored);
 #   render_head_bwd: the record + G + bottleneck read, dz_b (256 bottleneck + sigma) written
 #     (16 + 256 + 512 + 514 B; dz_g stays on chip);
-#   dwstream: dz_0 + dz_5 read (pe recomputed) = 1024 B
-BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "hidden_bwd_lb_kernel": 1538, "render_fwd_kernel": 4880,
-                    "render_head_bwd_kernel": 1298, "dwstream_kernel": 1024}
+#   dwstream: dz_0 + dz_5 + pe read = 1152 B
+BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "hidden_bwd_lb_kernel": 1538, "render_fwd_kernel": 5008,
+                    "render_head_bwd_kernel": 1298, "dwstream_kernel": 1152}
 
 
 def pmc_traffic(kernel, a):
