@@ -272,6 +272,18 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       graw[t][0] = ld_stream((const uint4*)p);
       graw[t][1] = ld_stream((const uint4*)(p + 1024));
     }
+    // this wave block's view-encoding tile (the Lg weight gradient's B operand for the ve columns), as
+    // the forward computes it.  Fixed-count sampler: the direction from the staged ray data, and the
+    // waves the adjoint leaves idle compute it now (stored after the barrier below: until then other
+    // waves may still read the previous item's tiles); the rest after the Lr^T chain
+    bf16x8 vef[2];
+    auto ve_frags = [&](const float* d) {
+      float dv[3];
+      view_input(d, dv);
+      acc_to_frags<MODE>(enc_tile<MODE>(dv, 0, grp, 4), vef);
+    };
+    const bool ve_early = A.points == 0 && wave >= WGS / A.n_samples;  // (the adjoint: one wave per ray)
+    if (ve_early) ve_frags(nray + (wave * TM) / A.n_samples * 12 + 3);
     if (A.points == 0) head_adjoint_staged(A, rec_lds, nray, bk, item, wave, lane);
     else head_adjoint<MODE>(A, rec_lds, item, sample, wave, lane, c, grp);
     HD_T(0);
@@ -281,6 +293,10 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (ve_early) {
+      *(bf16x8*)(vet + wave * HB_TILE + hb_slot(lane, 0) * 16) = vef[0];
+      *(bf16x8*)(vet + wave * HB_TILE + 1024 + hb_slot(lane, 1) * 16) = vef[1];
+    }
     HD_T(1);
 
     // fake dz tiles from the per-sample raw gradients (render_bwd_kernel<1, 1>)
@@ -334,16 +350,20 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       *(bf16x8*)(lscr + t * HB_TILE + hb_slot(lane, 0) * 16) = xa[t * FPT];
       *(bf16x8*)(lscr + t * HB_TILE + 1024 + hb_slot(lane, 1) * 16) = xa[t * FPT + 1];
     }
-    // this wave block's view-encoding tile (the Lg weight gradient's B operand for the ve columns),
-    // as the forward computes it: lane = sample c, lane group grp (enc_tile), then the DMA'd-tile
-    // layout; read by waves 0..3 after the chain's barriers
-    {
-      const int64_t ray = A.points == 0 ? sample / A.n_samples : A.points == 2 ? (int64_t)A.ray_idx[sample] : sample;
-      float d[3], dv[3];
+    // the view-encoding tile of the waves that did not compute it during the adjoint (lane = sample c,
+    // lane group grp (enc_tile), the DMA'd-tile layout); read by waves 0..3 after the chain's barriers
+    if (!ve_early) {
+      if (A.points == 0) {
+        ve_frags(nray + (wave * TM) / A.n_samples * 12 + 3);  // nray: restaged only in Lg^T's step 0
+      } else {
+        const int64_t ray = A.points == 2 ? (int64_t)A.ray_idx[sample] : sample;
+        float d[3];
 #pragma unroll
-      for (int a = 0; a < 3; ++a) d[a] = A.rays_d[ray * 3 + a];
-      view_input(d, dv);
-      lds_tile_store(vet + wave * HB_TILE, enc_tile<MODE>(dv, 0, grp, 4));
+        for (int a = 0; a < 3; ++a) d[a] = A.rays_d[ray * 3 + a];
+        ve_frags(d);
+      }
+      *(bf16x8*)(vet + wave * HB_TILE + hb_slot(lane, 0) * 16) = vef[0];
+      *(bf16x8*)(vet + wave * HB_TILE + 1024 + hb_slot(lane, 1) * 16) = vef[1];
     }
     HD_T(3);
     // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles, its last step wrapping in the next
