@@ -424,36 +424,44 @@ __device__ __forceinline__ typename Tr<MODE>::Acc enc_tile(const float* v, int p
 }
 
 // ------------------------------------------------------------------ wave primitives
+// DPP forms (no LDS round trip): a ds_bpermute shuffle costs an LDS latency per step, and the
+// compositing scans chain 20 of them (r05: 39 ds_bpermute in the head backward, all on its adjoint's
+// critical path).  dpp_shift: lane l gets v of the source lane the control names, 0 where there is
+// none (row_shr / row_shl / wave_shr / wave_shl) or where the row is masked off (row_bcast).
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_shift(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, false));
+}
+__device__ __forceinline__ float wave_readlane(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+// inclusive prefix sum over the wave: within rows of 16 (row_shr 1, 2, 4, 8), then row 15's total into
+// rows 1 and 3 (row_bcast:15) and lane 31's into rows 2 and 3 (row_bcast:31)
 __device__ __forceinline__ float wave_incl_scan(float v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    float o = __shfl_up(v, off, 64);
-    if (lane >= off) v += o;
-  }
+  v += dpp_shift<0x111>(v);
+  v += dpp_shift<0x112>(v);
+  v += dpp_shift<0x114>(v);
+  v += dpp_shift<0x118>(v);
+  v += dpp_shift<0x142, 0xa>(v);
+  v += dpp_shift<0x143, 0xc>(v);
   return v;
 }
-// inclusive suffix sum over the wave (lane l gets the sum over lanes >= l)
+// inclusive suffix sum over the wave (lane l gets the sum over lanes >= l): within rows (row_shl 1, 2,
+// 4, 8), then the later rows' totals (lanes 16, 32, 48 after the row pass) added per row -- adds only
 __device__ __forceinline__ float wave_incl_suffix(float v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float o = __shfl_down(v, off, 64);
-    if (lane + off < 64) v += o;
-  }
-  return v;
+  v += dpp_shift<0x101>(v);
+  v += dpp_shift<0x102>(v);
+  v += dpp_shift<0x104>(v);
+  v += dpp_shift<0x108>(v);
+  const float t3 = wave_readlane(v, 48), t2 = wave_readlane(v, 32) + t3, t1 = wave_readlane(v, 16) + t2;
+  const int row = (threadIdx.x & 63) >> 4;
+  return row == 0 ? v + t1 : row == 1 ? v + t2 : row == 2 ? v + t3 : v;
 }
 // exclusive prefix sum over the wave (lane 0 gets 0); adds only, no incl - v subtraction
-__device__ __forceinline__ float wave_excl_scan(float v) {
-  const float incl = wave_incl_scan(v);
-  const float prev = __shfl_up(incl, 1, 64);
-  return (threadIdx.x & 63) == 0 ? 0.0f : prev;
-}
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
+__device__ __forceinline__ float wave_excl_scan(float v) { return dpp_shift<0x138>(wave_incl_scan(v)); }  // wave_shr:1
+// v of lane l + 1 (lane 63: 0)
+__device__ __forceinline__ float wave_next_lane(float v) { return dpp_shift<0x130>(v); }  // wave_shl:1
+__device__ __forceinline__ float wave_sum(float v) { return wave_readlane(wave_incl_scan(v), 63); }
 
 // ------------------------------------------------------------------ weight chunk staging
 // A chunk (one packed TM-row tile of a layer, <= 20 KiB, a multiple of 1 KiB)

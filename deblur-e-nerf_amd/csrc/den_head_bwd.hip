@@ -175,7 +175,7 @@ __device__ __forceinline__ void head_adjoint_staged(const AT& A, float* rec_lds,
     wg_run += wgq[q];
   }
   const float wg_suf_incl = wave_incl_suffix(wg_run);
-  const float wg_after = __shfl_down(wg_suf_incl, 1, 64);
+  const float wg_after = wave_next_lane(wg_suf_incl);
   float sfx[4] = {0.f, 0.f, 0.f, 0.f}, later = lane < 63 ? wg_after : 0.0f;
 #pragma unroll
   for (int q = 3; q >= 0; --q) {

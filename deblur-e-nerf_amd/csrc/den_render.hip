@@ -1041,7 +1041,7 @@ __device__ __forceinline__ void head_adjoint(const AT& A, float* rec_lds, int64_
     // the reference's cumsum): total - prefix cancels to eps * total on the late samples of a
     // saturated ray (den_march.hip composite_bwd_kernel)
     const float wg_suf_incl = wave_incl_suffix(wg_run);            // lanes >= this one
-    const float wg_after = __shfl_down(wg_suf_incl, 1, 64);       // lanes > this one
+    const float wg_after = wave_next_lane(wg_suf_incl);       // lanes > this one
     float sfx[4] = {0.f, 0.f, 0.f, 0.f}, later = lane < 63 ? wg_after : 0.0f;
 #pragma unroll
     for (int q = 3; q >= 0; --q) {
