@@ -272,18 +272,33 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       graw[t][0] = ld_stream((const uint4*)p);
       graw[t][1] = ld_stream((const uint4*)(p + 1024));
     }
-    // this wave block's view-encoding tile (the Lg weight gradient's B operand for the ve columns), as
-    // the forward computes it.  Fixed-count sampler: the direction from the staged ray data, and the
-    // waves the adjoint leaves idle compute it now (stored after the barrier below: until then other
-    // waves may still read the previous item's tiles); the rest after the Lr^T chain
+    // the item's view-encoding tiles (the Lg weight gradient's B operand for the ve columns; lane =
+    // sample c, lane group grp (enc_tile), the DMA'd-tile layout), as the forward computes them.
+    // Fixed-count sampler: the directions from the staged ray data, all eight tiles by the waves the
+    // adjoint leaves idle (one wave per ray), during it -- wave rpw + b also computes tile b of the
+    // adjoint's wave b.  Tiles 0..6 are free here (the previous item's dw_block(b <= 6) ran before its
+    // last chain step's barrier); tile 7 is stored after the barrier below (dw_block(7) follows the
+    // chain).  Otherwise each wave computes its own after the Lr^T chain.
     bf16x8 vef[2];
     auto ve_frags = [&](const float* d) {
       float dv[3];
       view_input(d, dv);
       acc_to_frags<MODE>(enc_tile<MODE>(dv, 0, grp, 4), vef);
     };
-    const bool ve_early = A.points == 0 && wave >= WGS / A.n_samples;  // (the adjoint: one wave per ray)
-    if (ve_early) ve_frags(nray + (wave * TM) / A.n_samples * 12 + 3);
+    auto ve_store = [&](int b) {
+      *(bf16x8*)(vet + b * HB_TILE + hb_slot(lane, 0) * 16) = vef[0];
+      *(bf16x8*)(vet + b * HB_TILE + 1024 + hb_slot(lane, 1) * 16) = vef[1];
+    };
+    const int rpw = WGS / A.n_samples;  // (points == 0) rays per item = the adjoint's waves
+    const bool ve_pre = A.points == 0 && rpw <= 4;
+    if (ve_pre && wave >= rpw) {
+      if (wave - rpw < rpw) {
+        ve_frags(nray + ((wave - rpw) * TM) / A.n_samples * 12 + 3);
+        ve_store(wave - rpw);
+      }
+      ve_frags(nray + (wave * TM) / A.n_samples * 12 + 3);
+      if (wave != 7) ve_store(wave);
+    }
     if (A.points == 0) head_adjoint_staged(A, rec_lds, nray, bk, item, wave, lane);
     else head_adjoint<MODE>(A, rec_lds, item, sample, wave, lane, c, grp);
     HD_T(0);
@@ -293,10 +308,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (ve_early) {
-      *(bf16x8*)(vet + wave * HB_TILE + hb_slot(lane, 0) * 16) = vef[0];
-      *(bf16x8*)(vet + wave * HB_TILE + 1024 + hb_slot(lane, 1) * 16) = vef[1];
-    }
+    if (ve_pre && wave == 7) ve_store(7);
     HD_T(1);
 
     // fake dz tiles from the per-sample raw gradients (render_bwd_kernel<1, 1>)
@@ -350,9 +362,9 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       *(bf16x8*)(lscr + t * HB_TILE + hb_slot(lane, 0) * 16) = xa[t * FPT];
       *(bf16x8*)(lscr + t * HB_TILE + 1024 + hb_slot(lane, 1) * 16) = xa[t * FPT + 1];
     }
-    // the view-encoding tile of the waves that did not compute it during the adjoint (lane = sample c,
-    // lane group grp (enc_tile), the DMA'd-tile layout); read by waves 0..3 after the chain's barriers
-    if (!ve_early) {
+    // the view-encoding tile when it was not computed during the adjoint (read by waves 0..3 after the
+    // chain's barriers)
+    if (!ve_pre) {
       if (A.points == 0) {
         ve_frags(nray + (wave * TM) / A.n_samples * 12 + 3);  // nray: restaged only in Lg^T's step 0
       } else {
@@ -362,8 +374,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
         for (int a = 0; a < 3; ++a) d[a] = A.rays_d[ray * 3 + a];
         ve_frags(d);
       }
-      *(bf16x8*)(vet + wave * HB_TILE + hb_slot(lane, 0) * 16) = vef[0];
-      *(bf16x8*)(vet + wave * HB_TILE + 1024 + hb_slot(lane, 1) * 16) = vef[1];
+      ve_store(wave);
     }
     HD_T(3);
     // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles, its last step wrapping in the next
