@@ -190,6 +190,13 @@ DEN_HD double bias_scale(int mode, int l) {
 constexpr int DZB_W = 288, DZR_W = 32;
 enum ActId { A_PE = 0, A_S0 = 1, /* S0..S7 = 1..8 */ A_BT = 9, A_VE = 10, A_G = 11,
              D_Z0 = 12, /* DZ0..DZ7 = 12..19 */ D_ZB = 20, D_ZG = 21, D_ZR = 22, NACT = 23 };
+// The layer-major BF16 path (render_head_bwd_kernel -> hidden_bwd_kernel<true>) keeps dz_b in D_ZB's
+// allocation as 8 tiles per wave block (the bottleneck's 256; act_ptr's pseudo id D_ZB8), followed by
+// sigma's dz as one bf16 per sample (sigma_dz_offset): the Lb launch then streams dz_b exactly as the
+// other hidden launches stream dz (16 KiB blocks back to back) -- with the 288-wide layout its dz read
+// skipped a 2 KiB sigma tile per block and read 64 B of it.
+constexpr int D_ZB8 = NACT;
+DEN_HD constexpr int64_t sigma_dz_offset(int64_t n_blocks, int64_t wb) { return n_blocks * 16384 + wb * 64; }
 DEN_HD constexpr int act_width(int mode, int a) {
   return a == A_PE ? PE_PAD : a <= 8 ? WIDTH : a == A_BT ? WIDTH : a == A_VE ? VE_PAD : a == A_G ? WIDTH_COND
        : a <= 19 ? WIDTH : a == D_ZB ? DZB_W : a == D_ZG ? WIDTH_COND : DZR_W;

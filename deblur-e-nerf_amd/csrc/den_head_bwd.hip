@@ -421,11 +421,14 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       hd_dma_tile(bt_src(i + 1), xbuf + ((i + 1) & 1) * HB_TILE);
       return n + 2;
     };
-    bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true, true, true>(A, lds, sample, xa, xb, 0, D_ZB, NoTileHook{},
+    bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true, true, true>(A, lds, sample, xa, xb, 0, D_ZB8, NoTileHook{},
                                                                        lg_step, gc + 1);
     gc += 1 + bwd_tiles(MODE, 1);
-    // sigma's dz: 32 bf16 per wave block in dz_b's ninth tile (hidden_bwd_kernel<true>)
-    if (grp == 0) *(__bf16*)(act_ptr<MODE>(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)g4[0];
+    // sigma's dz: one bf16 per sample after dz_b's 8-tile blocks (sigma_dz_offset, den_geom.h)
+    if (grp == 0) {
+      const int64_t wb = __builtin_amdgcn_readfirstlane((int)(sample / TM));
+      *(__bf16*)(A.act[D_ZB] + sigma_dz_offset((int64_t)A.n_rays * A.n_samples / TM, wb) + c * 2) = (__bf16)g4[0];
+    }
     HD_T(4);
     // block 7 (its tile was issued in step 5; step 7's wait covered it)
     dw_block(7);

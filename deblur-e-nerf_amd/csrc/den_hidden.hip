@@ -89,7 +89,7 @@ __device__ __forceinline__ void hb_dma_untracked(const char* src, char* dst) {
   }
 }
 
-// LB: sigma's 32 bf16 dz of a wave block (64 B, render_bwd_kernel<1, 1>) into LDS, by lanes 0..3;
+// LB: sigma's 32 bf16 dz of a wave block (64 B, sigma_dz_offset) into LDS, by lanes 0..3;
 // every wave issues it (the same bytes), so each wave's DMA count per block stays uniform
 __device__ __forceinline__ void hb_dma_sigma(const char* src, char* dst) {
   const int lane = threadIdx.x & 63;
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   // HB_RING LDS slots of [dz_l block | S'_{l-1} block]; HB_DEPTH blocks in flight ahead of the one
   // being computed.  Each wave waits for its own part of block b+1 at the end of block b (vmcnt; the
   // younger prefetches and stores stay in flight), then the workgroup barrier publishes every part.
-  constexpr int DZ_TILES = LB ? 9 : 8;           // dz_in tiles per wave block in HBM (LB: the 9th holds sigma)
+  constexpr int DZ_TILES = 8;                    // dz_in tiles per wave block in HBM (LB: D_ZB8, den_geom.h)
   constexpr int DZ_STAGED = LB ? HB_BLOCK + HB_SIG : HB_BLOCK;  // bytes of them staged
   constexpr int SLOT = DZ_STAGED + HB_BLOCK;
   constexpr int KST = LB ? 17 : 16;              // chain k-steps
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   auto blk = [&](int64_t it) { return b0 + it; };
   auto fetch = [&](int64_t b, char* dst) {
     hb_dma_untracked(P.dz_in + b * DZ_TILES * HB_TILE, dst);
-    if constexpr (LB) hb_dma_sigma(P.dz_in + b * DZ_TILES * HB_TILE + HB_BLOCK, dst + HB_BLOCK);
+    if constexpr (LB) hb_dma_sigma(P.dz_in + sigma_dz_offset(P.n_blocks, b), dst + HB_BLOCK);
     hb_dma_untracked(P.s_in + b * HB_BLOCK, dst + DZ_STAGED);
   };
 #pragma unroll

@@ -64,6 +64,7 @@ template <int MODE, typename AT>
 __device__ __forceinline__ char* act_ptr(const AT& A, int a, int64_t sample, int tile) {
   constexpr int TM = Tr<MODE>::TM, ES = es_of(MODE);
   const int64_t wb = __builtin_amdgcn_readfirstlane((int)(sample / TM));  // uniform across the wave
+  if (a == D_ZB8) return A.act[D_ZB] + (wb * (WIDTH / TM) + tile) * (int64_t)(TM * TM * ES);  // (den_geom.h)
   return A.act[a] + (wb * (act_width(MODE, a) / TM) + tile) * (int64_t)(TM * TM * ES);
 }
 
