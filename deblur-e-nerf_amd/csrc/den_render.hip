@@ -1159,12 +1159,16 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
   // j=0 Lr^T: dz_r -> dG * softplus'(G) -> DZG (128 rows) [+ the fused Lr weight gradient]
   bwd_layer_run<MODE, LAST_J, 0, FPT, 0>(A, lds, sample, fr, xa, A_G, D_ZG, lr_hook);
   // j=1 Lg^T: dz_g (K=128) -> dBott (identity) -> DZB tiles 0..
-  bwd_layer_run<MODE, LAST_J, 1, WIDTH_COND / T::KI, 1>(A, lds, sample, xa, xb, 0, D_ZB);
+  bwd_layer_run<MODE, LAST_J, 1, WIDTH_COND / T::KI, 1>(A, lds, sample, xa, xb, 0,
+                                                       (MODE == 1 && LAST_J == 1) ? D_ZB8 : D_ZB);
   // sigma head row(s) of Lb as extra fake tile(s) appended to the DZB fragments
   if constexpr (MODE == 1 && LAST_J == 1) {
-    // Lb runs layer-major (hidden_bwd_kernel<true>): sigma's dz leaves as 32 bf16 per wave block
-    // in the first 64 B of dz_b's ninth tile (the rest of that tile is not read on this path)
-    if (grp == 0) *(__bf16*)(act_ptr<MODE>(A, D_ZB, sample, WIDTH / TM) + c * 2) = (__bf16)dzs[0];
+    // Lb runs layer-major (hidden_bwd_kernel<true>): dz_b as 8-tile blocks, then sigma's dz as one
+    // bf16 per sample (D_ZB8 / sigma_dz_offset, den_geom.h)
+    if (grp == 0) {
+      const int64_t wb = __builtin_amdgcn_readfirstlane((int)(sample / TM));
+      *(__bf16*)(A.act[D_ZB] + sigma_dz_offset((int64_t)A.n_rays * A.n_samples / TM, wb) + c * 2) = (__bf16)dzs[0];
+    }
   } else {
     constexpr int EXTRA_T = (DZB_W - WIDTH) / TM;  // sigma tile + zero padding
 #pragma unroll
