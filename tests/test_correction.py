@@ -96,8 +96,9 @@ def _scipy_refine(res_pred, target, nge, x0):
 def test_gain_exposure_normalisation_in_its_own_dtype():
     """deblur_e_nerf.py:707-739 with an f32, non-constant gain-exposure product: normalised and its
     log taken in f32, subtracted from the f32 target logs, and only then cast to f64 for the least
-    squares -- the corrected image equals that restatement bit for bit (an f64 normalisation
-    differs at ~1e-7 relative)."""
+    squares -- the corrected image equals that restatement to 1e-12 relative (an f64 normalisation
+    differs at ~1e-7 relative; not bit for bit: the threaded LAPACK least squares is not bitwise
+    reproducible from call to call, which made a torch.equal here flaky in the full suite)."""
     g = torch.Generator().manual_seed(11)
     target = torch.rand(3, 12, 14, generator=g) * 0.8 + 0.1
     pred = (target * 1.3 + torch.rand(3, 12, 14, generator=g) * 0.05).clamp(0.01, 2)
@@ -110,8 +111,8 @@ def test_gain_exposure_normalisation_in_its_own_dtype():
     A = torch.nn.functional.pad(plog.unsqueeze(-1), (0, 1), value=1.0).transpose(0, 1).flatten(1, 3)
     sol = torch.linalg.lstsq(A, tlog.unsqueeze(-1).transpose(0, 1).flatten(1, 3)).solution
     want = ((A @ sol).view(1, 3, 12, 14).transpose(0, 1) + lg).exp()
-    assert torch.equal(corr, want)
-    assert float(gamma[0]) == float(sol[0, 0, 0])
+    torch.testing.assert_close(corr, want, rtol=1e-12, atol=0.0)
+    assert abs(float(gamma[0]) - float(sol[0, 0, 0])) <= 1e-12 * abs(float(sol[0, 0, 0]))
     # and the f64 normalisation is measurably different (so the test resolves the dtype)
     lg64 = (gep.double() / gep.double().mean()).log().view(-1, 1, 1, 1)
     assert not torch.equal(lg64.float(), lg) or not torch.equal((target.unsqueeze(1).log() - lg64).double(), tlog)
