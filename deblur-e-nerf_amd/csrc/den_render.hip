@@ -718,6 +718,9 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
         }
       }
     }
+#ifdef DEN_FWD_PROF
+    prof[7] += __builtin_amdgcn_s_memtime() - q1;  // the tail up to the compositing barrier
+#endif
     if (!A.points) {
       __syncthreads();
       // compositing: one wave per ray (nerfacc render_weight_from_density +
