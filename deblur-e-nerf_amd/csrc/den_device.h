@@ -94,6 +94,14 @@ __device__ __forceinline__ void st_stream(V* p, V v) {
   static_assert(sizeof(V) == 16, "16-byte streams");
   __builtin_nontemporal_store(__builtin_bit_cast(den_u32x4, v), (den_u32x4*)p);
 }
+// A wave-uniform read of kernel-constant data (ray inputs, the background colour) as a SCALAR load
+// (constant address space): it waits on lgkmcnt, not behind every older vector-memory op of the wave
+// (vmcnt is in-order: a vector load here would wait out the wave's stores and LDS-DMAs in flight).
+// The address must be wave-uniform.
+template <typename T>
+__device__ __forceinline__ T ld_uniform(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
 template <typename V>
 __device__ __forceinline__ V ld_stream(const V* p) {
   static_assert(sizeof(V) == 16, "16-byte streams");

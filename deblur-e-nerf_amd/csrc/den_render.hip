@@ -508,6 +508,78 @@ __device__ __forceinline__ void fwd_layer(const AT& A, char* lds, int slot0, int
 }
 
 // ------------------------------------------------------------------ forward kernel
+// Compositing of item `item` (fixed-count sampler): one wave per ray, nerfacc
+// render_weight_from_density + accumulate_along_rays (vol_rendering.py:89-126), from the item's
+// per-sample records in rec_lds.  r05bb: run by waves 0 .. rays_per_wg - 1 in the MIDDLE of the next
+// item (between its L_B and L_G layers; rec_lds is rewritten only at that item's end), where the
+// older waves of each SIMD pair wait at the chunk barriers for their partners anyway -- at the item
+// boundary it sat on the critical path (every wave waited for it at the next item's first barrier).
+// The ray data and background by scalar loads: a vector load here would wait out every store and
+// ring DMA in flight.
+template <int MODE, typename AT>
+__device__ __forceinline__ void fwd_composite(const AT& A, const float* rec_lds, int64_t item, int wave, int lane,
+                                              const float* aabb) {
+  constexpr int WGS = fwd_wg_samples(MODE);
+  const int rays_per_wg = WGS / A.n_samples;
+  const int64_t r = item * rays_per_wg + __builtin_amdgcn_readfirstlane(wave);
+  float ro[3], rdv[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    ro[a] = ld_uniform(A.rays_o + r * 3 + a);
+    rdv[a] = ld_uniform(A.rays_d + r * 3 + a);
+  }
+  RayGeom rg = ray_geom(ro, rdv, aabb, A.near_p, A.far_p);
+  const float ru = ld_uniform(A.jitter + r);
+  const int spl = A.n_samples / 64;  // samples per lane (1, 2 or 4)
+  float tau[4], tmid[4], locx[4];
+  float run = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= spl) break;
+    int kk = lane * spl + q;
+    float a0, a1;
+    sample_interval(rg, kk, ru, A.n_samples, &a0, &a1);
+    float sg = rec_lds[(wave * A.n_samples + kk) * 4];
+    // zero-length samples (missed rays) contribute nothing, also where sigma overflowed
+    tau[q] = (a1 > a0) ? sg * (a1 - a0) : 0.0f;
+    tmid[q] = (a0 + a1) / 2.0f;
+    locx[q] = run;
+    run += tau[q];
+  }
+  // exclusive optical depth as a sum of the preceding terms only (nerfacc's sequential exclusive
+  // cumsum): never incl - tau, which is inf - inf once a sigma overflows
+  float base = wave_excl_scan(run);
+  float cs[3] = {0.f, 0.f, 0.f}, op = 0.f, dp = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= spl) break;
+    int kk = lane * spl + q;
+    float excl = base + locx[q];
+    float w = expf(-excl) * (1.0f - expf(-tau[q]));
+    const float* rc = rec_lds + (wave * A.n_samples + kk) * 4;
+    cs[0] += w * rc[1];
+    cs[1] += w * rc[2];
+    cs[2] += w * rc[3];
+    op += w;
+    dp += w * tmid[q];
+  }
+  op = wave_sum(op);
+  dp = wave_sum(dp);
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) cs[ch] = wave_sum(cs[ch]);
+  if (lane == 0) {
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      if (ch >= A.rd) break;
+      float v = cs[ch];
+      if (A.has_bkgd) v = v + ld_uniform(A.bkgd + ch) * (1.0f - op);
+      A.out_rgb[r * A.rd + ch] = v;
+    }
+    A.out_opacity[r] = op;
+    A.out_depth[r] = dp;
+  }
+}
+
 template <int MODE, bool TRAIN>
 DEN_CODE_ALIGN  // page-aligned code (r04y A/B)
 __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render_fwd_kernel(RenderArgs<MODE> A0) {
@@ -683,6 +755,9 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
         acc_to_frags<MODE>(a, ve + b * VE_S + p * FPT);
       }
     }
+    // the previous item's compositing (fwd_composite)
+    if (!A.points && item >= (int64_t)gridDim.x && wave < WGS / A.n_samples)
+      fwd_composite<MODE>(A, rec_lds, item - gridDim.x, wave, lane, aabb);
     fwd_layer<MODE, TRAIN, L_G, KS, KS, VE_S, VE_S, 0, NB, true, DEN_PST(L_B, 1)>(
         A, lds, slot0, grp, sample, xa, ve, xb, A_G, out, vm, DEN_PEND(L_B, 1, xa, 0), tl);
     fwd_layer<MODE, TRAIN, L_R, WIDTH_COND / T::KI, KS, 0, 0, 2, NB, false, DEN_PST(L_G, 0)>(
@@ -719,77 +794,26 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
       }
     }
 #ifdef DEN_FWD_PROF
-    prof[7] += __builtin_amdgcn_s_memtime() - q1;  // the tail up to the compositing barrier
+    prof[7] += __builtin_amdgcn_s_memtime() - q1;  // the per-sample outputs of the tail
 #endif
-    if (!A.points) {
-      __syncthreads();
-      // compositing: one wave per ray (nerfacc render_weight_from_density +
-      // accumulate_along_rays, vol_rendering.py:89-126); the other waves go on to the next item,
-      // whose rec_lds writes come 40 barriers later
-      const int rays_per_wg = WGS / A.n_samples;
-      if (wave < rays_per_wg) {
-        const int64_t r = item * rays_per_wg + wave;
-        float ro[3], rdv[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          ro[a] = A.rays_o[r * 3 + a];
-          rdv[a] = A.rays_d[r * 3 + a];
-        }
-        RayGeom rg = ray_geom(ro, rdv, aabb, A.near_p, A.far_p);
-        const float ru = A.jitter[r];
-        const int spl = A.n_samples / 64;  // samples per lane (1, 2 or 4)
-        float tau[4], tmid[4], locx[4];
-        float run = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (q >= spl) break;
-          int kk = lane * spl + q;
-          float a0, a1;
-          sample_interval(rg, kk, ru, A.n_samples, &a0, &a1);
-          float sg = rec_lds[(wave * A.n_samples + kk) * 4];
-          // zero-length samples (missed rays) contribute nothing, also where sigma overflowed
-          tau[q] = (a1 > a0) ? sg * (a1 - a0) : 0.0f;
-          tmid[q] = (a0 + a1) / 2.0f;
-          locx[q] = run;
-          run += tau[q];
-        }
-        // exclusive optical depth as a sum of the preceding terms only (nerfacc's sequential
-        // exclusive cumsum): never incl - tau, which is inf - inf once a sigma overflows
-        float base = wave_excl_scan(run);
-        float cs[3] = {0.f, 0.f, 0.f}, op = 0.f, dp = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (q >= spl) break;
-          int kk = lane * spl + q;
-          float excl = base + locx[q];
-          float w = expf(-excl) * (1.0f - expf(-tau[q]));
-          const float* rc = rec_lds + (wave * A.n_samples + kk) * 4;
-          cs[0] += w * rc[1];
-          cs[1] += w * rc[2];
-          cs[2] += w * rc[3];
-          op += w;
-          dp += w * tmid[q];
-        }
-        op = wave_sum(op);
-        dp = wave_sum(dp);
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) cs[ch] = wave_sum(cs[ch]);
-        if (lane == 0) {
-#pragma unroll
-          for (int ch = 0; ch < 3; ++ch) {
-            if (ch >= A.rd) break;
-            float v = cs[ch];
-            if (A.has_bkgd) v = v + A.bkgd[ch] * (1.0f - op);
-            A.out_rgb[r * A.rd + ch] = v;
-          }
-          A.out_opacity[r] = op;
-          A.out_depth[r] = dp;
-        }
-      }
-    }
+    // (points = 0: this item is composited by waves 0 .. rays_per_wg - 1 in the middle of the next
+    // item, or after the loop for the last one -- fwd_composite)
 #ifdef DEN_FWD_PROF
     prof[5] += __builtin_amdgcn_s_memtime() - q1;
 #endif
+  }
+  // the last item's compositing (its records: every wave's, published by this barrier)
+  if (!A0.points && (int64_t)blockIdx.x < A0.n_items) {
+    __syncthreads();
+    if (wave < WGS / A0.n_samples) {
+      const int64_t last = blockIdx.x + (A0.n_items - 1 - blockIdx.x) / gridDim.x * gridDim.x;
+      int tid = threadIdx.x;
+      asm volatile("" : "+v"(tid));
+      float aabb[6];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) aabb[q] = A0.aabb[q];
+      fwd_composite<MODE>(A0, rec_lds, last, wave, tid & 63, aabb);
+    }
   }
   // the last item's steps prefetched chunks of an item that does not exist: let those DMAs land
   // before the workgroup (and its LDS) goes away

@@ -57,9 +57,9 @@ def main():
         print(f"    {name:8s} {v.mean():10.0f} cyc/wave ({v.mean() / tot.mean() * 100:5.1f} %)")
     # by wave index: waves w and w + 4 share SIMD w; waves 0 .. rays_per_wg - 1 composite a ray in each
     # item's tail (den_render.hip)
-    # [7]: the part of the tail before the compositing barrier (per-sample outputs + record stores)
+    # [7]: the per-sample outputs + record stores of the tail (r05bb on: the whole tail)
     v7 = p[:, :, 7][waves]
-    print(f"  tail before the compositing barrier {v7.mean():10.0f} cyc/wave ({v7.mean() / tot.mean() * 100:5.1f} %)")
+    print(f"  tail outputs {v7.mean():10.0f} cyc/wave ({v7.mean() / tot.mean() * 100:5.1f} %)")
     for name, q in (("tails", 5), ("barrier", 2), ("body", 0), ("pre-barrier tail", 7)):
         row = [p[:, w, q][waves[:, w]].mean() / tot.mean() * 100 for w in range(8)]
         print(f"  {name:8s} by wave: " + " ".join(f"{x:5.1f}" for x in row) + " %")
