@@ -13,8 +13,12 @@
 //     (all 4 row tiles, k = the item's 256 samples): the bottleneck tile (block b, column w) of each
 //     of the item's 8 wave blocks arrives by untracked LDS-DMA in a private double buffer, both
 //     MFMA operands by transposed LDS reads;
-//   * each wave computes its block's view-encoding tile (enc_tile, as the forward) into LDS; waves
-//     0..3 own its four (row tile w, ve) output tiles plus the bias of row tile w;
+//   * the item's eight view-encoding tiles (enc_tile, as the forward) go to LDS -- with the
+//     fixed-count sampler computed from the staged ray data by the waves the adjoint leaves idle,
+//     during it (r05ar); waves 0..3 own the four (row tile w, ve) output tiles plus row tile w's bias;
+//   * the adjoint's inputs (records, ray data) are staged in LDS one item ahead (r05ag), the Lr^T G
+//     tiles loaded at the item top (r05ah), and every chain step waits by count for its weight chunk
+//     only (untracked DMA, r05aa-ad), so the dz_b stores stay in flight;
 //   * the accumulators live in registers for the whole launch; each workgroup writes one split-K
 //     partial in den_dwstream.hip's layout [wg][4][10][64][16] (column 9: the bias), reduced in a
 //     fixed order by dw_reduce_kernel -- deterministic.
