@@ -335,6 +335,8 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
         ldb[2] += (float)z2;
       }
     }
+    // the dz_r tile's transposed fragments: the same A operand (masked per G tile) for all four tiles
+    const bf16x8 dzr_tr[2] = {hb_tr_frag(lscr, 0), hb_tr_frag(lscr, 1)};
     auto lr_hook = [&](int i, const Acc& sv) {
       Frag gf[FPT];
       acc_to_frags<MODE>(sv, gf);
@@ -344,9 +346,8 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
       const bool keep = ((lane & 31) >> 3) == i;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 a = hb_tr_frag(lscr, kk);
         const bf16x8 zero = {};
-        a = keep ? a : zero;
+        const bf16x8 a = keep ? dzr_tr[kk] : zero;
         lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hb_tr_frag(gs, kk), lacc, 0, 0, 0);
       }
     };
