@@ -27,6 +27,7 @@
 #include "den_raygrad.hip"
 #include "den_sh.hip"
 #include "den_dataset.hip"
+#include "den_eval.hip"
 
 using namespace den;
 
@@ -528,6 +529,16 @@ int den_version(void) { return DEN_VERSION; }
 int den_debug_fwd_prof(uint64_t* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(den_fwd_prof), sizeof(uint64_t) * 512 * 8 * 8) == hipSuccess ? DEN_OK
                                                                                                         : DEN_EHIP;
+}
+#endif
+
+#ifdef DEN_CLOCK
+// diagnostic builds only: the start / end stamps of every hot kernel's last launch (den_device.h)
+int den_debug_clock(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(den_clock), sizeof(uint64_t) * DEN_CLOCK_KERNELS * DEN_CLOCK_WGS * 4) ==
+                 hipSuccess
+             ? DEN_OK
+             : DEN_EHIP;
 }
 #endif
 
@@ -1808,6 +1819,37 @@ int den_undistort_events(int64_t n, int32_t model, const int64_t* position, cons
   A.out = out;
   hipLaunchKernelGGL(undistort_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
   DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+size_t den_ssim_workspace_bytes(int32_t n_img) { return n_img > 0 ? (size_t)n_img * SSIM_SLICES * sizeof(double) : 0; }
+
+int den_ssim(int32_t n_img, int32_t channels, int32_t height, int32_t width, const float* pred, const float* target,
+             const float* window, float c1, float c2, void* workspace, double* ssim_sum, void* stream) {
+  if (n_img <= 0 || channels <= 0 || height < 2 * SSIM_HALF + 1 || width < 2 * SSIM_HALF + 1 || !pred || !target ||
+      !window || !workspace || !ssim_sum)
+    return fail(DEN_EINVAL, "bad arguments (images must be at least 11 x 11)");
+  SsimArgs A{};
+  A.C = channels;
+  A.H = height;
+  A.W = width;
+  A.c1 = c1;
+  A.c2 = c2;
+  for (int q = 0; q < SSIM_WIN * SSIM_WIN; ++q) A.win[q] = window[q];
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ssim_kernel, dim3(SSIM_SLICES, n_img), dim3(SSIM_BLOCK), 0, st, A, pred, target,
+                     (double*)workspace);
+  DEN_LAUNCHED();
+  hipLaunchKernelGGL(sum_partials_f64_kernel, dim3(n_img), dim3(256), 0, st, n_img, SSIM_SLICES,
+                     (const double*)workspace, ssim_sum);
+  DEN_LAUNCHED();
+  return DEN_OK;
+}
+
+int den_png_unfilter(int64_t height, int64_t row_bytes, int32_t bpp, const uint8_t* filtered, uint8_t* out) {
+  if (height < 0 || row_bytes < 0 || bpp < 1 || bpp > 8 || (height > 0 && row_bytes > 0 && (!filtered || !out)))
+    return fail(DEN_EINVAL, "bad arguments");
+  if (!png_unfilter_host(height, row_bytes, bpp, filtered, out)) return fail(DEN_EINVAL, "unknown PNG filter type");
   return DEN_OK;
 }
 

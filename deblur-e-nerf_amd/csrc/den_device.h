@@ -14,6 +14,37 @@
 #define DEN_CODE_ALIGN __attribute__((aligned(4096)))
 #endif
 
+// Diagnostic build only (-DDEN_CLOCK, MI355X_MICROARCH.md 'DVFS give-back' item 6): each hot kernel
+// stamps s_memtime (shader clock) and s_memrealtime (100 MHz) once at its start and once at its end,
+// workgroup by workgroup, into a buffer of its own that no kernel reads (den_debug_clock copies it
+// out); in-kernel clock = delta memtime / delta realtime x 100 MHz.  Kernel slots: 0 render_fwd,
+// 1 render_head_bwd, 2 hidden_bwd (L7..L1, the last launch wins), 3 hidden_bwd Lb, 4 dwstream.
+#ifdef DEN_CLOCK
+constexpr int DEN_CLOCK_KERNELS = 5, DEN_CLOCK_WGS = 512;
+__device__ uint64_t den_clock[DEN_CLOCK_KERNELS * DEN_CLOCK_WGS * 4];
+#define DEN_CLOCK_BEGIN()                                            \
+  const uint64_t den_clk_t0_ = __builtin_amdgcn_s_memtime();         \
+  const uint64_t den_clk_r0_ = __builtin_amdgcn_s_memrealtime()
+#define DEN_CLOCK_END(k)                                                                       \
+  do {                                                                                         \
+    const uint64_t t1_ = __builtin_amdgcn_s_memtime(), r1_ = __builtin_amdgcn_s_memrealtime(); \
+    if (threadIdx.x == 0 && blockIdx.x < DEN_CLOCK_WGS) {                                      \
+      uint64_t* o_ = den_clock + ((int64_t)(k) * DEN_CLOCK_WGS + blockIdx.x) * 4;              \
+      __builtin_nontemporal_store(den_clk_t0_, o_);                                            \
+      __builtin_nontemporal_store(den_clk_r0_, o_ + 1);                                        \
+      __builtin_nontemporal_store(t1_, o_ + 2);                                                \
+      __builtin_nontemporal_store(r1_, o_ + 3);                                                \
+    }                                                                                          \
+  } while (0)
+#else
+#define DEN_CLOCK_BEGIN() \
+  do {                    \
+  } while (0)
+#define DEN_CLOCK_END(k) \
+  do {                   \
+  } while (0)
+#endif
+
 namespace den {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

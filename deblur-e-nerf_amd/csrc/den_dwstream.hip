@@ -78,6 +78,7 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
   constexpr int TPW = (MT * NT + NW - 1) / NW;      // output tiles per wave
   static_assert(RING * SLOT <= 160 * 1024, "ring exceeds the LDS");
   __shared__ __attribute__((aligned(16))) char lds[RING * SLOT];
+  DEN_CLOCK_BEGIN();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR) for the DMA operands
   // readfirstlane hides the range of threadIdx.x >> 6: without it the compiler cannot prove the
@@ -165,6 +166,7 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
+  DEN_CLOCK_END(4);
   // partial of this workgroup: [mt][nt][lane][16], the bias in the ones-tile slot nt = NT
   float* base = P.partial + (int64_t)blockIdx.x * MT * (NT + 1) * 1024;
 #pragma unroll

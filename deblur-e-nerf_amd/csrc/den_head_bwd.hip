@@ -245,6 +245,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     for (int r = 0; r < 16; ++r) gacc[q][r] = 0.0f;
   float ldb[3] = {0.f, 0.f, 0.f}, gdb = 0.0f;
   const int64_t n_items = (int64_t)A0.n_rays * A0.n_samples / WGS;
+  DEN_CLOCK_BEGIN();
 #ifdef DEN_HEAD_PROF
   uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
@@ -442,6 +443,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
   // drain (nothing of ours in flight past here but the wrapped chunk DMA of a non-existent item)
   __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8));
   __syncthreads();
+  DEN_CLOCK_END(1);
 #ifdef DEN_HEAD_PROF
   prof[6] = __builtin_amdgcn_s_memtime() - t_start;
   prof[7] = (n_items - blockIdx.x + gridDim.x - 1) / gridDim.x;

@@ -254,6 +254,7 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   constexpr int YOUNGER = HB_STORE_OPS + (HB_DEPTH - 1) * (DMA_OPS + HB_STORE_OPS);
   static_assert(HB_RING * SLOT <= 160 * 1024, "hidden ring exceeds the LDS");
   __shared__ __attribute__((aligned(16))) char lds[HB_RING * SLOT];
+  DEN_CLOCK_BEGIN();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // a contiguous range of P.per_wg blocks per workgroup (r03: strided by the grid, so that all
   // workgroups sweep one address window, measured the same)
@@ -304,6 +305,7 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
+  DEN_CLOCK_END(LB ? 3 : 2);
   // split-K partial of this workgroup (dw_gemm_kernel layout: [wg][mt][nt][lane][16]); the bias
   // goes where that layout's ones tile (nt = 8) keeps it: column 0 = lanes 0 and 32, row m in
   // register (m & 3) + 4 (m >> 3) of lane 32 ((m >> 2) & 1)

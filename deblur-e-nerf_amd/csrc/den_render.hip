@@ -598,6 +598,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
   float* rec_lds = bias_lds + NBIAS;
 
   const int wave = threadIdx.x >> 6;
+  DEN_CLOCK_BEGIN();
 #ifdef DEN_FWD_PROF
   uint64_t prof[8] = {0, 0, 0, __builtin_amdgcn_s_memtime(), 0, 0, 0, 0};
 #endif
@@ -818,6 +819,7 @@ __global__ __launch_bounds__(fwd_threads(MODE), fwd_min_waves(MODE)) void render
   // the last item's steps prefetched chunks of an item that does not exist: let those DMAs land
   // before the workgroup (and its LDS) goes away
   wait_vm_lgkm0<0>();
+  if constexpr (MODE == 1 && TRAIN) DEN_CLOCK_END(0);
 #ifdef DEN_FWD_PROF
   prof[6] = __builtin_amdgcn_s_memtime();
   if (blockIdx.x < 512 && (threadIdx.x & 63) == 0) {

@@ -150,10 +150,15 @@ _SIGS = {
     "den_max_refractory_period": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
                                   + [ctypes.c_void_p] * 3 + [ctypes.c_size_t] + [ctypes.c_void_p] * 2),
     "den_undistort_events": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 5),
+    # evaluation views and metrics, den_eval.hip
+    "den_ssim_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "den_ssim": (ctypes.c_int, [ctypes.c_int32] * 4 + [ctypes.c_void_p] * 3 + [ctypes.c_float] * 2
+                 + [ctypes.c_void_p] * 3),
+    "den_png_unfilter": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 2),
 }
 
 
-ABI_VERSION = 5  # include/den_api.h DEN_VERSION
+ABI_VERSION = 6  # include/den_api.h DEN_VERSION
 
 
 def lib():
@@ -962,6 +967,47 @@ def image_error(pred, target):
     ws = torch.empty(lib().den_image_error_workspace_bytes(B) // 8, dtype=torch.float64, device=p.device)
     out = torch.empty(B, 2, dtype=torch.float64, device=p.device)
     _check(lib().den_image_error(B, p.shape[1], _ptr(p), _ptr(t), _ptr(ws), _ptr(out), _stream(p.device)))
+    return out
+
+
+SSIM_WIN, SSIM_SIGMA, SSIM_K1, SSIM_K2 = 11, 1.5, 0.01, 0.03
+
+
+def ssim_window():
+    """torchmetrics 0.6.2's SSIM window (functional/image/ssim.py _gaussian / _gaussian_kernel): the
+    normalised 1-D Gaussian over arange(-5, 6) in f32 and its outer product -> (121,) f32."""
+    dist = torch.arange((1 - SSIM_WIN) / 2, (1 + SSIM_WIN) / 2, 1, dtype=torch.float32)
+    g = torch.exp(-torch.pow(dist / SSIM_SIGMA, 2) / 2)
+    g = (g / g.sum()).unsqueeze(0)
+    return torch.matmul(g.t(), g).reshape(-1).contiguous()
+
+
+def ssim(pred, target, data_range):
+    """den_ssim: (B, C, H, W) image pairs -> (B,) f64 mean SSIM index per image (torchmetrics 0.6.2
+    functional.ssim with data_range; H, W >= 11)."""
+    _require_device(pred, target)
+    assert pred.shape == target.shape and pred.dim() == 4
+    B, C, H, W = pred.shape
+    p = pred.to(torch.float32).contiguous()
+    t = target.to(torch.float32).contiguous()
+    win = ssim_window()
+    c1, c2 = (SSIM_K1 * data_range) ** 2, (SSIM_K2 * data_range) ** 2
+    ws = torch.empty(lib().den_ssim_workspace_bytes(B) // 8, dtype=torch.float64, device=p.device)
+    out = torch.empty(B, dtype=torch.float64, device=p.device)
+    wbuf = (ctypes.c_float * win.numel())(*win.tolist())
+    _check(lib().den_ssim(B, C, H, W, _ptr(p), _ptr(t), wbuf, c1, c2, _ptr(ws), _ptr(out), _stream(p.device)))
+    return out / (C * (H - 2 * (SSIM_WIN // 2)) * (W - 2 * (SSIM_WIN // 2)))
+
+
+def png_unfilter(filtered, height, row_bytes, bpp):
+    """den_png_unfilter (host): the inflated rows of a non-interlaced PNG (numpy uint8, height x
+    (1 + row_bytes)) -> the reconstructed bytes (numpy uint8, height x row_bytes)."""
+    import numpy as np
+    src = np.ascontiguousarray(filtered, dtype=np.uint8)
+    if src.size != height * (row_bytes + 1):
+        raise DenError(f"png_unfilter: {src.size} bytes for {height} rows of {row_bytes}")
+    out = np.empty(height * row_bytes, dtype=np.uint8)
+    _check(lib().den_png_unfilter(height, row_bytes, bpp, src.ctypes.data, out.ctypes.data))
     return out
 
 

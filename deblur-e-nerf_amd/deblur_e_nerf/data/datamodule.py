@@ -12,8 +12,9 @@ changes between steps.
 
 A ``pytorch_lightning.LightningDataModule`` when Lightning is importable; otherwise a plain object
 with the same attributes and loaders (Lightning is absent from this image).  The evaluation
-datasets (``PosedImage``: images read with OpenCV) are outside the hot path: ``setup("fit")``
-leaves ``val_dataset`` None when they are unavailable, ``setup("validate" | "test")`` raises.
+datasets are ``PosedImage`` views (data/datasets.py); a directory without a ``views/`` folder still
+trains (``setup("fit")`` leaves ``val_dataset`` None, where the reference would fail), while
+``setup("validate" | "test")`` raises.
 """
 import torch
 import torch.distributed as dist
@@ -112,15 +113,19 @@ class DataModule(_Base):
         return dataset_utils.IterableMapDataset(ev, self.train_batch_size, self.train_generator)
 
     def _build_eval_dataset(self, stage, required):
-        posed = getattr(datasets, "PosedImage", None)
-        if posed is None:
+        """The evaluation views (:107-119): PosedImage of the training views' images for an
+        ``event_view`` target, else of the stage's own transforms; permuted by
+        ``eval_dataset_perm_seed``, alpha-composited over white when configured, trimmed (:121-139)."""
+        if datasets.PosedImage.posed_img_folder_path(self.dataset_directory) is None:
             if required:
-                raise NotImplementedError("evaluation images (PosedImage) are outside the MI355X hot path")
-            return None
+                raise FileNotFoundError(f"no views/ folder in or above {self.dataset_directory} (PosedImage)")
+            return None  # training-only directory: fit proceeds without a val set
         if set(self.eval_target) == {"event_view"}:
-            ds = posed(self.dataset_directory, "train", self.eval_dataset_perm_seed, self.alpha_over_white_bg)
+            ds = datasets.PosedImage(self.dataset_directory, "train", self.eval_dataset_perm_seed,
+                                     self.alpha_over_white_bg)
         elif set(self.eval_target) == {"novel_view"}:
-            ds = posed(self.dataset_directory, stage, self.eval_dataset_perm_seed, self.alpha_over_white_bg)
+            ds = datasets.PosedImage(self.dataset_directory, stage, self.eval_dataset_perm_seed,
+                                     self.alpha_over_white_bg)
         else:
             raise NotImplementedError(f"eval_target {self.eval_target}")
         return self._subset(ds, stage)

@@ -46,7 +46,7 @@ from ..external import marching
 from ..loss_metric import loss as loss_lib
 from ..loss_metric import metric as metric_lib
 from ..optim import Adam
-from ..utils import modules
+from ..utils import image_io, modules
 from ..utils.easydict import EasyDict
 from . import event_generation_params, nerf as nerf_lib, pixel_bandwidth as pixbw_lib, trajectories
 
@@ -60,17 +60,47 @@ except ImportError:  # pragma: no cover - the image has no pytorch_lightning
 
 
 class _TrainerStub:
-    """What training_step reads of a pytorch_lightning Trainer when there is none."""
+    """What the module's hooks read of a pytorch_lightning Trainer when there is none: training_step's
+    ``accumulate_grad_batches`` / ``datamodule``, evaluation_epoch_end's ``log_dir``,
+    ``is_global_zero`` and ``sanity_checking``."""
 
-    def __init__(self, accumulate_grad_batches=1, datamodule=None):
+    def __init__(self, accumulate_grad_batches=1, datamodule=None, log_dir=None):
         self.accumulate_grad_batches = accumulate_grad_batches
         self.datamodule = datamodule
+        self.log_dir = log_dir
+        self.sanity_checking = False
+
+    @property
+    def is_global_zero(self):
+        return not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+
+
+def _gather_collection(data, device):
+    """pytorch_lightning's LightningModule.all_gather (1.4.9) over the default process group: every
+    tensor of a (nested) list / tuple / dict gathered to a (world, ...) stack; with one process the
+    tensors come back as they are (PL's single-device plugin), scalars as 0-d tensors."""
+    if isinstance(data, dict):
+        return type(data)({k: _gather_collection(v, device) for k, v in data.items()})
+    if isinstance(data, (list, tuple)):
+        return type(data)(_gather_collection(v, device) for v in data)
+    t = torch.as_tensor(data, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        t = t.contiguous()
+        out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(out, t)
+        return torch.stack(out)
+    return t
 
 
 class DeblurENeRF(_Base):
     INTRINSICS_KEY = "intrinsics"
     NUM_DIM = 3
     MAX_NUM_SAMPLES_PER_RAY = 1024
+    CORRECTION_ERRORS_FOLDER_NAME = "correction-errors"
+    CORRECTION_ERRORS_EXTENSION = ".csv"
+    PREDICTIONS_FOLDER_NAME = "predictions"
+    PREDICTION_FILE_EXTENSION = ".png"
+    PREDICTION_BIT_DEPTH = 8
     MODEL_COMPONENTS = ["contrast_threshold", "refractory_period", "nerf"]
     MULTI_PARAM_MODEL_COMPONENTS = ["contrast_threshold"]
 
@@ -99,7 +129,12 @@ class DeblurENeRF(_Base):
         self.register_buffer("train_intrinsics_inv",
                              torch.linalg.inv(torch.from_numpy(np.asarray(cal[self.INTRINSICS_KEY])).float()),
                              persistent=False)
+        self._init_eval_stages(dataset_directory, eval_target)
         self.render_bkgd = "parameter" if alpha_over_white_bg else None
+        # the refinement correction's warm start, carried across evaluations (:171-197)
+        if self.correction.black_level_offset:
+            self.init_correction_scale, self.init_correction_gamma, self.init_correction_offset = \
+                init_correction_params(self.has_bayer_filter, self.correction.per_channel_log_it_scale)
 
         hp = EasyDict(git_head_hash=git_head_hash, min_modeled_intensity=min_modeled_intensity,
                       checkpoint_filepath=checkpoint_filepath, contrast_threshold=contrast_threshold,
@@ -111,6 +146,8 @@ class DeblurENeRF(_Base):
             self._hparams = hp
             self._trainer = _TrainerStub()
             self._global_step = 0
+            self._current_epoch = 0
+            self._logger = None
             self.logged = {}
 
         self.contrast_threshold = event_generation_params.ContrastThreshold(
@@ -151,13 +188,60 @@ class DeblurENeRF(_Base):
         def log(self, name, value, **kwargs):
             self.logged[name] = value.detach() if torch.is_tensor(value) else value
 
-        def all_gather(self, t):
-            t = torch.as_tensor(t, device=self.trajectory.T_wc_position.device)
-            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-                out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
-                dist.all_gather(out, t)
-                return torch.stack(out)
-            return t[None]
+        @property
+        def current_epoch(self):
+            return self._current_epoch
+
+        @property
+        def device(self):
+            return self.train_intrinsics_inv.device
+
+        @property
+        def logger(self):
+            """None (no TensorBoard logger) unless a test or driver sets ``_logger``: an object with
+            ``experiment.add_image(tag, img, global_step=...)``."""
+            return self._logger
+
+        def all_gather(self, data):
+            return _gather_collection(data, self.trajectory.T_wc_position.device)
+
+    # ------------------------------------------------------------------ evaluation stages
+    def _init_eval_stages(self, dataset_directory, eval_target):
+        """deblur_e_nerf.py:96-162: the val views (the training views' images for an ``event_view``
+        target, else ``views/transforms_val.json``) and, when present, the test views give each stage
+        its intrinsics inverse, its (H, W, 2) pixel grid and its value range.  One deviation: the
+        reference cannot be constructed without a ``views/`` folder (PosedImage joins a None path);
+        here the stages are then left empty (None) and only validation / testing raise."""
+        if set(eval_target) == {"event_view"}:
+            val_stage = "train"
+        elif set(eval_target) == {"novel_view"}:
+            val_stage = "val"
+        else:
+            raise NotImplementedError(f"eval_target {eval_target}")
+        for name in ("val", "test"):
+            setattr(self, f"{name}_min_normalized_pixel_value", None)
+            setattr(self, f"{name}_max_normalized_pixel_value", None)
+            self.register_buffer(f"{name}_intrinsics_inv", None, persistent=False)
+            self.register_buffer(f"{name}_img_pixel_pos", None, persistent=False)
+        if datasets.PosedImage.posed_img_folder_path(dataset_directory) is None:
+            return
+        val = datasets.PosedImage(dataset_directory, val_stage, permutation_seed=None)
+        self._set_eval_stage("val", val)
+        try:
+            test = val if val_stage == "train" else datasets.PosedImage(dataset_directory, "test", permutation_seed=None)
+            self._set_eval_stage("test", test)
+        except FileNotFoundError:
+            pass
+
+    def _set_eval_stage(self, name, posed):
+        H, W = posed.posed_imgs.img.shape[-2:]
+        setattr(self, f"{name}_min_normalized_pixel_value", posed.min_normalized_pixel_value)
+        setattr(self, f"{name}_max_normalized_pixel_value", posed.max_normalized_pixel_value)
+        dev = self.train_intrinsics_inv.device
+        setattr(self, f"{name}_intrinsics_inv", posed.posed_imgs.intrinsics.inverse().to(dev))
+        setattr(self, f"{name}_img_pixel_pos",
+                torch.stack(torch.meshgrid(torch.arange(W), torch.arange(H), indexing="xy"), dim=2)
+                .to(torch.get_default_dtype()).to(dev))
 
     # ------------------------------------------------------------------ components
     def _build_nerf(self, camera_poses):
@@ -442,6 +526,177 @@ class DeblurENeRF(_Base):
                 self._global_step += 1
         return loss
 
+    # ------------------------------------------------------------------ evaluation (val / test)
+    def on_train_epoch_start(self):
+        """deblur_e_nerf.py:392-394: release the allocator's unoccupied cached blocks."""
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+
+    def on_train_start(self):
+        """deblur_e_nerf.py:1114-1127: the hyper-parameter metrics a logger tracks."""
+        if self.logger is None or not hasattr(self.logger, "log_hyperparams"):
+            return
+        self.logger.log_hyperparams(self.hparams, {"val/l1": float("inf"), "val/psnr": float("-inf"), "val/ssim": -1,
+                                                   "val/lpips": float("inf")})
+
+    def _stage(self, name, keys):
+        for k in keys:
+            if getattr(self, f"{name}_{k}") is None:
+                raise RuntimeError(f"no {name} views: the dataset directory has no views/ folder with "
+                                   f"transforms_{'val' if name == 'val' else 'test'}.json (PosedImage)")
+        return EasyDict({k: getattr(self, f"{name}_{k}") for k in keys})
+
+    def validation_step(self, batch, batch_index):
+        """deblur_e_nerf.py:588-593."""
+        return self.evaluation_step(batch, batch_index, self._stage("val", ("intrinsics_inv", "img_pixel_pos")))
+
+    def test_step(self, batch, batch_index):
+        """deblur_e_nerf.py:595-600."""
+        return self.evaluation_step(batch, batch_index, self._stage("test", ("intrinsics_inv", "img_pixel_pos")))
+
+    def evaluation_step(self, batch, batch_index, stage):
+        """deblur_e_nerf.py:602-652: one view (batch size 1) rendered at its camera pose over the
+        stage's pixel grid (render_pixels: den_pixel_rays + the NeRF renders, chunked in eval mode)
+        -> sample_id, pred_intensity_img ([3,] H, W), target_intensity_img, exposure_time, gain."""
+        batch = EasyDict(batch)
+        batch.size = len(batch.img)
+        assert batch.size == 1
+        for k, v in batch.items():
+            if k != "size":
+                batch[k] = v.squeeze(dim=0)
+        target = batch.img
+        H, W = target.shape[-2:]
+        assert H == stage.img_pixel_pos.shape[0] and W == stage.img_pixel_pos.shape[1]
+        pos = batch.T_wc_position.view(1, 1, 3).expand(H, W, -1)
+        rot = batch.T_wc_orientation.view(1, 1, 3, 3).expand(H, W, -1, -1)
+        pred, _, _, _, _ = self.render_pixels(stage.intrinsics_inv, stage.img_pixel_pos, pos, rot)
+        if "exposure_time" not in batch.keys():
+            batch.exposure_time = torch.tensor(1, dtype=torch.int64, device=self.device)
+        if "gain" not in batch.keys():
+            batch.gain = torch.tensor(1, dtype=torch.get_default_dtype(), device=self.device)
+        return {"sample_id": batch.sample_id, "pred_intensity_img": pred, "target_intensity_img": target,
+                "exposure_time": batch.exposure_time, "gain": batch.gain}
+
+    def validation_epoch_end(self, outputs):
+        """deblur_e_nerf.py:654-660."""
+        stage = self._stage("val", ("min_normalized_pixel_value", "max_normalized_pixel_value"))
+        stage.name = "val"
+        return self.evaluation_epoch_end(outputs, stage)
+
+    def test_epoch_end(self, outputs):
+        """deblur_e_nerf.py:662-668."""
+        stage = self._stage("test", ("min_normalized_pixel_value", "max_normalized_pixel_value"))
+        stage.name = "test"
+        return self.evaluation_epoch_end(outputs, stage)
+
+    def evaluation_epoch_end(self, outputs, stage):
+        """deblur_e_nerf.py:670-1053: gather the views of every rank; on global rank 0 the intensity
+        correction on the CPU in f64 (``evaluation_correction``: the least-squares affine log-intensity
+        fit, then -- ``correction.black_level_offset`` -- the OffsetGammaCorrection refinement by
+        Gauss-Newton / Levenberg-Marquardt from the warm start of the previous evaluation, which is
+        then carried on unless Lightning is sanity checking), the per-view metrics on the device
+        (``Metric.compute``: den_image_error, den_ssim), their mean logged as ``<stage>/<metric>``, and
+        -- with a logger -- the correction-error log, the first view as an image and, with
+        ``eval_save_pred_intensity_img``, the 8-bit predictions as PNG files."""
+        outputs = self.all_gather(outputs)
+        dim = outputs[0]["sample_id"].dim()
+        merge = torch.stack if dim == 1 else torch.cat
+        sample_id = merge([o["sample_id"] for o in outputs])
+        pred = merge([o["pred_intensity_img"] for o in outputs])
+        target = merge([o["target_intensity_img"] for o in outputs])
+        exposure_time = merge([o["exposure_time"] for o in outputs])
+        gain = merge([o["gain"] for o in outputs])
+        del outputs
+        sample_id = self.unicode_code_pt_tensor_to_str(sample_id)
+        log_dir = self.trainer.log_dir
+        if not self.trainer.is_global_zero:
+            return
+        gain_exposure_prod = (gain * exposure_time).cpu()
+        batch_size = len(target)
+        res = evaluation_correction(pred.cpu(), target.cpu(), gain_exposure_prod, self.has_bayer_filter,
+                                    self.correction,
+                                    init=(self.init_correction_scale, self.init_correction_gamma,
+                                          self.init_correction_offset) if self.correction.black_level_offset else None)
+        pred, target = res.pred, res.target
+        if self.correction.black_level_offset:
+            if not self.trainer.sanity_checking:
+                self.init_correction_scale, self.init_correction_gamma, self.init_correction_offset = res.converged
+            if self.logger is not None:
+                folder = os.path.join(log_dir, self.CORRECTION_ERRORS_FOLDER_NAME)
+                os.makedirs(folder, exist_ok=True)
+                np.savetxt(os.path.join(folder, str(self.current_epoch) + self.CORRECTION_ERRORS_EXTENSION),
+                           res.errors.numpy(), fmt=("%.14f",))
+        self.last_correction = res
+        pred = pred.to(self.device)
+        target = target.to(self.device)
+        pred = pred.to(target.dtype)
+        metric = self.metric.init_batch_metric()
+        for p, t in zip(pred, target):
+            sample = self.metric.compute(p, t, min_target_val=stage.min_normalized_pixel_value,
+                                         max_target_val=stage.max_normalized_pixel_value)
+            for k, v in sample.items():
+                metric[k].append(v)
+        for k, v in metric.items():
+            metric[k] = sum(v) / batch_size
+        self.log(f"{stage.name}/epoch", self.current_epoch, prog_bar=True, logger=False, rank_zero_only=True)
+        for k, v in metric.items():
+            self.log(f"{stage.name}/{k}", v, prog_bar=True, rank_zero_only=True)
+        if self.logger is None:
+            return
+        lo, hi = stage.min_normalized_pixel_value, stage.max_normalized_pixel_value
+        self.logger.experiment.add_image(f"{stage.name}/pred_intensity_img",
+                                         ((pred[0] - lo) / (hi - lo)).clamp(min=0, max=1), global_step=self.global_step)
+        if self.current_epoch == 0:
+            self.logger.experiment.add_image(f"{stage.name}/target_intensity_img", (target[0] - lo) / (hi - lo),
+                                             global_step=self.global_step)
+        del target
+        if not self.eval_save_pred_intensity_img:
+            return
+        max_pixel_value = 2 ** self.PREDICTION_BIT_DEPTH - 1
+        img = (max_pixel_value * ((pred.cpu() - lo) / (hi - lo)).clamp(min=0, max=1)).round()
+        img = img.numpy().astype({8: np.uint8, 16: np.uint16}[self.PREDICTION_BIT_DEPTH])
+        img = img.transpose(0, 2, 3, 1)  # (B, H, W, 1 | 3) grey / RGB
+        if self.has_bayer_filter:
+            img = np.stack([image_io.bgr_to_rgb(x) for x in img], axis=0)  # RGB -> BGR, as cv2.imwrite expects
+        folder = os.path.join(log_dir, self.PREDICTIONS_FOLDER_NAME)
+        os.makedirs(folder, exist_ok=True)
+        for sid, x in zip(sample_id, img):
+            image_io.imwrite(os.path.join(folder, sid + self.PREDICTION_FILE_EXTENSION), x)
+
+    @staticmethod
+    def unicode_code_pt_tensor_to_str(batch_unicode_code_pt_tensor):
+        """deblur_e_nerf.py:1310-1319: code points -> strings, trailing padding stripped."""
+        return ["".join(map(chr, (int(c) for c in sample))).rstrip() for sample in batch_unicode_code_pt_tensor]
+
+    @torch.no_grad()
+    def run_evaluation(self, stage, datamodule):
+        """What pytorch_lightning's ``Trainer.validate`` / ``Trainer.test`` run on this module
+        (scripts/run.py:114-118), for use without Lightning: the stage's loader (sharded over the
+        ranks of the default process group as Lightning's ``replace_sampler_ddp`` does, without
+        shuffling), eval mode and no_grad, ``validation_step`` / ``test_step`` per batch on the
+        module's device, then ``*_epoch_end``.  Returns ``[{"<stage>/<metric>": value}]`` as the
+        Trainer does."""
+        assert stage in ("val", "test")
+        datamodule.setup("validate" if stage == "val" else "test")
+        ds = datamodule.val_dataset if stage == "val" else datamodule.test_dataset
+        bs = datamodule.val_batch_size if stage == "val" else datamodule.test_batch_size
+        sampler = None
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            sampler = torch.utils.data.distributed.DistributedSampler(ds, shuffle=False, drop_last=False)
+        loader = torch.utils.data.DataLoader(ds, batch_size=bs, sampler=sampler, shuffle=False, num_workers=0)
+        step = self.validation_step if stage == "val" else self.test_step
+        end = self.validation_epoch_end if stage == "val" else self.test_epoch_end
+        was = self.training
+        self.eval()
+        try:
+            dev = self.device
+            outputs = [step({k: v.to(dev) for k, v in b.items()}, i) for i, b in enumerate(loader)]
+            end(outputs)
+        finally:
+            self.train(was)
+        logged = getattr(self, "logged", {})
+        return [{k: float(v) for k, v in logged.items() if k.startswith(stage + "/") and k != stage + "/epoch"}]
+
     @torch.no_grad()
     def render_image_eval(self, intrinsics_inverse, T_wc_position, T_wc_orientation, img_height, img_width):
         """evaluation_step's render (deblur_e_nerf.py:602-652): the (H, W) image of one camera
@@ -569,7 +824,11 @@ def evaluation_correction(pred_intensity_img, target_intensity_img, gain_exposur
     with torch.no_grad():
         errors = [float(optimizer.model.loss(input=pred, target=tgt)) / n]
     for _ in range(1, int(o.max_steps) + 1):
-        prev = list(mod.detach_clone_named_parameters(model))
+        # the reference keeps the GENERATOR utils/modules.detach_clone_named_parameters returns
+        # (deblur_e_nerf.py:887) and consumes it only in the check below, i.e. after the step: the
+        # parameter half of its early stop compares the updated parameters with themselves, so the
+        # stop rests on the errors alone.  Kept lazy here so the step count is the reference's.
+        prev = mod.detach_clone_named_parameters(model)
         errors.append(float(optimizer.step(input=pred, target=tgt)) / n)
         if (torch.allclose(torch.tensor(errors[-1], dtype=torch.float64), torch.tensor(errors[-2], dtype=torch.float64))
                 and mod.named_parameters_allclose(model, prev)):
@@ -584,13 +843,16 @@ def evaluation_correction(pred_intensity_img, target_intensity_img, gain_exposur
 
 
 def flat_gradient_buffers(grads):
-    """The gradients grouped by dtype for the all-reduce: {dtype: (flat buffer, [gradients])} -- one
-    f32 buffer for the f32 parameters (the MLP / hash table) and one f64 buffer for the f64 ones (the
-    refractory period, event_generation_params.py:196-201), so no f32 gradient travels as f64."""
-    groups = {}
+    """The gradients grouped for the all-reduce: {dtype: (flat buffer, [gradients])} -- one f64 buffer
+    for the f64 parameters (the refractory period, event_generation_params.py:196-201) and one f32
+    buffer for every other floating dtype (the MLP / hash table; a half-precision gradient is
+    promoted, never summed across ranks in half precision), so no f32 gradient travels as f64.  The
+    groups come in a fixed order (f32, then f64), independent of the order the dtypes first appear,
+    so every rank issues the same collectives."""
+    groups = {torch.float32: [], torch.float64: []}
     for g in grads:
-        groups.setdefault(g.dtype, []).append(g)
-    return {dt: (torch.cat([g.reshape(-1) for g in gs]), gs) for dt, gs in groups.items()}
+        groups[torch.float64 if g.dtype == torch.float64 else torch.float32].append(g)
+    return {dt: (torch.cat([g.reshape(-1).to(dt) for g in gs]), gs) for dt, gs in groups.items() if gs}
 
 
 def allreduce_gradients(module):

@@ -40,6 +40,9 @@
  *   den_event_loss_* <- deblur_e_nerf/loss_metric/loss.py:34-96 Loss.compute
  *   den_event_target
  *   den_image_error  <- deblur_e_nerf/loss_metric/metric.py:28-92 (L1, PSNR)
+ *   den_ssim         <- deblur_e_nerf/loss_metric/metric.py:74-81 (torchmetrics 0.6.2 ssim)
+ *   den_png_unfilter <- the PNG decode inside cv2.imread, deblur_e_nerf/data/datasets.py:504-509
+ *                       (PosedImage.load_posed_imgs; host code)
  *   den_adam_step    <- torch.optim.Adam as configured by
  *                       deblur_e_nerf/models/deblur_e_nerf.py:1055-1112
  *   den_march_* / den_visibility / den_compact / den_pack_info / den_exclusive_scan
@@ -66,7 +69,8 @@
 extern "C" {
 #endif
 
-#define DEN_VERSION 5  /* 5: den_queue_raw_events / den_max_refractory_period / den_colorize_events /
+#define DEN_VERSION 6  /* 6: den_ssim / den_png_unfilter (the evaluation views and metrics);
+                          5: den_queue_raw_events / den_max_refractory_period / den_colorize_events /
                           den_undistort_events; den_render_desc.ray_grad;
                           4: density_activation in den_render_desc / den_ngp_desc; den_sh_encode_* */
 
@@ -570,6 +574,23 @@ int den_max_refractory_period(int64_t n, int32_t img_height, int32_t img_width, 
  * (4 f32) are HOST pointers.  OpenCV is absent from this image: parity unpinned. */
 int den_undistort_events(int64_t n, int32_t model, const int64_t* position, const float* intrinsics,
                          const float* distortion, float* out, void* stream);
+
+/* ---------------------------------------------------------------- evaluation (PosedImage, Metric) */
+/* SSIM of n_img (channels, height, width) f32 image pairs (loss_metric/metric.py:74-81 ->
+ * torchmetrics 0.6.2 functional.ssim: 11 x 11 Gaussian window, sigma 1.5; c1 = (0.01 range)^2,
+ * c2 = (0.03 range)^2 with range = the metric's max_target_val).  torchmetrics crops 5 pixels on
+ * every side after its reflect-padded convolution, so only windows inside the image count:
+ * ssim_sum (n_img) f64 = the sum of the SSIM index over channels x (height - 10) x (width - 10)
+ * (the caller divides).  window: HOST pointer to the 121 f32 weights (torchmetrics' outer product
+ * of the normalised 1-D Gaussian).  height, width >= 11.  workspace: den_ssim_workspace_bytes(n_img). */
+size_t den_ssim_workspace_bytes(int32_t n_img);
+int den_ssim(int32_t n_img, int32_t channels, int32_t height, int32_t width, const float* pred, const float* target,
+             const float* window, float c1, float c2, void* workspace, double* ssim_sum, void* stream);
+/* HOST function: PNG scanline unfiltering (filter types 0-4 per row, bytewise, the left neighbour
+ * bpp bytes back): filtered = height rows of [filter type byte | row_bytes bytes] (the inflated IDAT
+ * stream of a non-interlaced PNG), out = height x row_bytes reconstructed bytes.  Used for the 16-bit
+ * colour views (data/datasets.py:508 reads them with cv2.imread); DEN_EINVAL on an unknown type. */
+int den_png_unfilter(int64_t height, int64_t row_bytes, int32_t bpp, const uint8_t* filtered, uint8_t* out);
 
 #ifdef __cplusplus
 }

@@ -18,9 +18,16 @@ modules the reference imports get stand-ins:
   the trajectory fixture);
 * ``pytorch_lightning``: ``LightningModule`` = ``torch.nn.Module`` (the
   DeblurENeRF fixture binds the reference's methods to a plain module);
-* ``cv2``, ``pypose``, ``tinycudann``, ``lpips``, ``torchmetrics``: import-only (never called on
-  these paths); ``tqdm`` is the real package when importable (the dataset queueing fixture runs
-  datasets.py's loops, which call it), else import-only too.
+* ``pypose``: the CPU restatement of pypose 0.6.7's optimizer base in ``oracle/pypose.py`` (exercised
+  by the evaluation fixtures, whose black-level refinement runs the reference's own
+  external/optimizer.py subclasses on it);
+* ``torchmetrics``: the CPU restatement of torchmetrics 0.6.2's psnr / ssim in ``oracle/metrics.py``;
+* ``lpips``: ``LPIPS`` returns zeros (no pretrained network exists offline; the fixtures record no
+  LPIPS values);
+* ``cv2``: attributes are filled by the fixture that uses them (``make_golden.install_cv2``: imread
+  returns the exact samples the fixture wrote, cvtColor restates OpenCV's conversions); otherwise
+  import-only; ``tinycudann``: import-only; ``tqdm`` is the real package when importable (the dataset
+  queueing fixture runs datasets.py's loops, which call it), else import-only too.
 """
 import importlib
 import os
@@ -61,7 +68,9 @@ def install():
         raise RuntimeError("reference tree not present: golden generation only runs in the build container")
     if REPO_ROOT not in sys.path:
         sys.path.insert(0, REPO_ROOT)
+    from oracle import metrics as ometrics
     from oracle import nerfacc as onerfacc
+    from oracle import pypose as opypose
     from oracle import roma as oroma
     ed = types.ModuleType("easydict")
     ed.EasyDict = _EasyDict
@@ -70,11 +79,25 @@ def install():
         import tqdm  # noqa: F401
     except ImportError:
         pass
-    for name in ("cv2", "pypose", "tqdm", "tinycudann", "lpips", "torchmetrics"):
+    for name in ("cv2", "tqdm", "tinycudann"):
         sys.modules.setdefault(name, types.ModuleType(name))
     sys.modules["roma"] = oroma.as_module()
-    pl = types.ModuleType("pytorch_lightning")
+    sys.modules["pypose"] = opypose.as_module()
+    sys.modules["torchmetrics"] = ometrics.as_module()
+    lp = types.ModuleType("lpips")
     import torch
+
+    class LPIPS(torch.nn.Module):
+        def __init__(self, net=None):
+            super().__init__()
+            self.net = net
+
+        def forward(self, in0, in1):
+            return torch.zeros(in0.shape[0], 1, 1, 1, dtype=in0.dtype)
+
+    lp.LPIPS = LPIPS
+    sys.modules["lpips"] = lp
+    pl = types.ModuleType("pytorch_lightning")
     pl.LightningModule = torch.nn.Module
     sys.modules["pytorch_lightning"] = pl
     nf = types.ModuleType("nerfacc")

@@ -1342,6 +1342,346 @@ def gen_queue():
          max_refractory_period_dtype=np.array(str(mx.dtype)))
 
 
+# ----------------------------------------------------------------------------
+# evaluation views (data/datasets.py:376-712 PosedImage) and the evaluation loop
+# (models/deblur_e_nerf.py:588-1053), run through the reference's own code
+from pngenc import bgr as _bgr, encode_png  # noqa: E402
+
+
+IMREAD_TRUTH = {}
+
+
+def install_cv2():
+    """cv2 stand-in for the reference's PosedImage / evaluation_epoch_end: imread returns the exact
+    samples the fixture wrote to that path in OpenCV's conventions (BGR / BGRA order, grey + alpha
+    expanded to BGRA, the file's sample type); cvtColor restates COLOR_BGR2RGB / COLOR_RGB2BGR (the
+    channel order reversed) and COLOR_BGR2GRAY on float32 as OpenCV 4.5.2's SIMD path computes it,
+    fma(r, 0.299f, fma(g, 0.587f, b * 0.114f)) (evaluated exactly in f64, rounded per operation);
+    imwrite records the arrays it is given."""
+    cv2 = sys.modules["cv2"]
+    cv2.IMREAD_UNCHANGED, cv2.COLOR_BGR2RGB, cv2.COLOR_RGB2BGR, cv2.COLOR_BGR2GRAY = -1, 4, 4, 6
+    cv2.written = {}
+
+    def imread(path, flags):
+        assert flags == -1
+        return IMREAD_TRUTH[os.path.realpath(path)].copy()
+
+    def cvtColor(img, code):
+        if code == 4:
+            assert img.ndim == 3 and img.shape[2] == 3
+            return np.ascontiguousarray(img[..., ::-1])
+        assert code == 6 and img.dtype == np.float32
+        c = [np.float64(np.float32(v)) for v in (0.114, 0.587, 0.299)]
+        b, g, r = (img[..., k].astype(np.float64) for k in range(3))
+        t = (b * c[0]).astype(np.float32).astype(np.float64)
+        t = (g * c[1] + t).astype(np.float32).astype(np.float64)
+        return (r * c[2] + t).astype(np.float32)
+
+    def imwrite(path, img):
+        cv2.written[os.path.basename(path)] = np.array(img)
+        return True
+
+    cv2.imread, cv2.cvtColor, cv2.imwrite = imread, cvtColor, imwrite
+    return cv2
+
+
+def _view_poses(n, seed, radius=4.03):
+    """n camera-to-world matrices in the OpenGL convention (x right, y up, z back) looking at the
+    origin from radius ~4 (the layout of the synthetic chair views)."""
+    g = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        v = g.normal(size=3)
+        c = v / np.linalg.norm(v) * radius
+        z = c / np.linalg.norm(c)           # back = away from the origin
+        x = np.cross([0.0, 0.0, 1.0], z)
+        x /= np.linalg.norm(x)
+        y = np.cross(z, x)
+        T = np.eye(4)
+        T[:3, 0], T[:3, 1], T[:3, 2], T[:3, 3] = x, y, z, c
+        out.append(T)
+    return out
+
+
+POSED_CASES = {
+    # name: bayer, renderer (None | display | linear), sample depth, channels, file kind, intrinsics
+    # source, per-frame exposure / gain, bit_depth key, views folder one level up, runs (stage, perm
+    # seed, alpha over white)
+    "mono_display_rgba8": dict(bayer="", renderer="display", depth=8, C=4, kind="png", fov=True, expo=False,
+                               bit_depth=None, up=False, runs=[("val", None, True), ("val", 9, True),
+                                                               ("test", None, False)]),
+    "rggb_real_rgb8": dict(bayer="RGGB", renderer=None, depth=8, C=3, kind="png", fov=False, expo=True,
+                           bit_depth=None, up=True, runs=[("train", None, False), ("train", 3, False)]),
+    "mono_real_gray16_bd10": dict(bayer="", renderer=None, depth=16, C=1, kind="png", fov=True, expo=True,
+                                  bit_depth=10, up=False, runs=[("val", None, False)]),
+    "rggb_display_rgba16": dict(bayer="BGGR", renderer="display", depth=16, C=4, kind="png", fov=True, expo=False,
+                                bit_depth=None, up=False, runs=[("val", None, True), ("val", None, False)]),
+    "mono_display_ga16": dict(bayer="", renderer="display", depth=16, C=2, kind="png", fov=True, expo=False,
+                              bit_depth=None, up=False, runs=[("val", None, True)]),
+    "mono_real_rgb8": dict(bayer="", renderer=None, depth=8, C=3, kind="pil", fov=True, expo=False,
+                           bit_depth=None, up=False, runs=[("val", 1, False)]),
+    "mono_linear_npy": dict(bayer="", renderer="linear", depth=32, C=4, kind="npy", fov=True, expo=False,
+                            bit_depth=None, up=False, runs=[("val", None, True), ("val", None, False)]),
+    "rggb_linear_npy": dict(bayer="RGGB", renderer="linear", depth=32, C=3, kind="npy", fov=False, expo=False,
+                            bit_depth=None, up=False, runs=[("val", None, False)]),
+}
+
+
+def _case_samples(c, n, H, W, g):
+    """n images of samples for a case: smooth gradients + noise in the file's range."""
+    yy, xx = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing="ij")
+    imgs = []
+    for k in range(n):
+        chans = []
+        for ch in range(c["C"]):
+            base = 0.5 + 0.4 * np.sin(3 * xx + 2 * yy * (ch + 1) + k) + 0.05 * g.normal(size=(H, W))
+            if ch == 3 or (c["C"] == 2 and ch == 1):  # alpha: opaque centre, transparent corners
+                base = np.clip(1.6 - 2.5 * np.hypot(xx - 0.5, yy - 0.5), 0, 1)
+            chans.append(np.clip(base, 0, 1))
+        a = np.stack(chans, -1) if c["C"] > 1 else chans[0]
+        if c["kind"] == "npy":
+            a = a.astype(np.float32)
+            if c["C"] == 4:  # premultiplied alpha (linear renders)
+                a[..., :3] *= a[..., 3:4]
+            imgs.append(a)
+            continue
+        top = (2 ** c["bit_depth"] - 1) if c["bit_depth"] else (2 ** c["depth"] - 1)
+        imgs.append(np.round(a * top).astype(np.uint16 if c["depth"] == 16 else np.uint8))
+    return imgs
+
+
+def write_posed_case(name, c, root, seed=5, H=20, W=24):
+    """A dataset directory for a PosedImage case: camera_calibration.npz, [renderer_params.npz],
+    views/transforms_{stage}.json and the image files (PNG by the encoder above or by PIL, or .npy).
+    Registers what cv2.imread returns for each image.  -> {relative path: file bytes}."""
+    from PIL import Image
+    g = np.random.default_rng(seed)
+    cal = dict(bayer_pattern=np.array(c["bayer"]), intrinsics=np.array([[30.0, 0, 12], [0, 30.0, 10], [0, 0, 1]],
+                                                                      dtype=np.float32),
+               img_height=np.array(H), img_width=np.array(W))
+    np.savez(os.path.join(root, "camera_calibration.npz"), **cal)
+    if c["renderer"] is not None:
+        np.savez(os.path.join(root, "renderer_params.npz"), interm_color_space=np.array(c["renderer"]),
+                 log_eps=np.array(0.001))
+    views = os.path.join(root, "..", "views") if c["up"] else os.path.join(root, "views")
+    os.makedirs(views, exist_ok=True)
+    stages = sorted({r[0] for r in c["runs"]})
+    for si, stage in enumerate(stages):
+        os.makedirs(os.path.join(views, stage), exist_ok=True)
+        n = 3 + si
+        imgs = _case_samples(c, n, H, W, g)
+        frames = []
+        for k, (img, T) in enumerate(zip(imgs, _view_poses(n, seed + 17 * si))):
+            rel = f"./{stage}/r_{k}" if k != 1 else f"./{stage}/view_long_name{k}"
+            path = os.path.join(views, rel[2:]) + {"png": ".png", "pil": ".png", "npy": ".npy"}[c["kind"]]
+            if c["kind"] == "npy":
+                np.save(path, _bgr(img))   # float renders stored as OpenCV hands them over (BGR[A])
+            elif c["kind"] == "pil":
+                Image.fromarray(img).save(path)
+            else:
+                with open(path, "wb") as f:
+                    f.write(encode_png(img, c["depth"]))
+            IMREAD_TRUTH[os.path.realpath(path)] = _bgr(img) if c["kind"] != "npy" else _bgr(img)
+            fr = {"file_path": rel, "transform_matrix": T.tolist()}
+            if c["expo"]:
+                fr["exposure_time"] = int(g.integers(5_000_000, 20_000_000))
+                fr["gain"] = float(g.uniform(0.5, 4.0))
+            frames.append(fr)
+        tf = {"frames": frames}
+        if c["fov"]:
+            tf["camera_angle_x"] = 0.6911112070083618
+        else:
+            tf["intrinsics"] = [[28.0, 0.0, 11.5], [0.0, 29.0, 9.5], [0.0, 0.0, 1.0]]
+        if c["bit_depth"]:
+            tf["bit_depth"] = c["bit_depth"]
+        with open(os.path.join(views, f"transforms_{stage}.json"), "w") as f:
+            json.dump(tf, f, indent=2)
+    files = {}
+    base = os.path.dirname(root) if c["up"] else root
+    for dirpath, _, names in os.walk(base):
+        for nm in names:
+            full = os.path.join(dirpath, nm)
+            with open(full, "rb") as f:
+                files[os.path.relpath(full, base)] = f.read()
+    return files
+
+
+def gen_posed():
+    """posed_<case>.npz -- the reference's PosedImage (data/datasets.py:376-712) run as-is on the
+    synthetic view directories of POSED_CASES (cv2 as install_cv2 states it): every output of each
+    (stage, permutation seed, alpha over white) run.  The directory's files are stored as bytes
+    (``file:<relative path>``) so the tests rebuild it; ``root`` names the dataset directory among them."""
+    ds = _refload.load("data.datasets")
+    install_cv2()
+    for name, c in POSED_CASES.items():
+        top = tempfile.mkdtemp(prefix="den_posed_")
+        root = os.path.join(top, "seq") if c["up"] else top
+        os.makedirs(root, exist_ok=True)
+        files = write_posed_case(name, c, root)
+        out = {f"file:{k}": np.frombuffer(v, dtype=np.uint8) for k, v in files.items()}
+        out["root"] = np.array("seq" if c["up"] else ".")
+        out["n_runs"] = np.array(len(c["runs"]))
+        for i, (stage, perm, alpha) in enumerate(c["runs"]):
+            pi = ds.PosedImage(root, stage, perm, alpha)
+            p = f"run{i}:"
+            out[p + "stage"], out[p + "perm"], out[p + "alpha"] = np.array(stage), np.array(-1 if perm is None else perm), \
+                np.array(alpha)
+            for k, v in pi.posed_imgs.items():
+                out[p + k] = v.numpy()
+                out[p + k + "_dtype"] = np.array(str(v.dtype))
+            out[p + "min_normalized_pixel_value"] = np.array(float(pi.min_normalized_pixel_value))
+            out[p + "max_normalized_pixel_value"] = np.array(float(pi.max_normalized_pixel_value))
+        save(f"posed_{name}.npz", **out)
+
+
+class _ImgLogger:
+    """What evaluation_epoch_end uses of a TensorBoard logger: experiment.add_image."""
+
+    def __init__(self):
+        self.images = {}
+        self.experiment = self
+
+    def add_image(self, tag, img, global_step=None):
+        self.images[tag] = img.detach().cpu().numpy()
+
+
+def gen_eval_epoch(rd=1, seed=6, H=20, W=24, black_level_offset=True, algo="lm", tag=None, sigma_bias_shift=2.0,
+                   rgb_weight_scale=30.0):
+    """eval_epoch_*.npz -- the reference's validation loop: PosedImage views (8-bit PNG: RGB for the
+    monochrome sensor, RGBA alpha-composited over white for the Bayer one), the DataModule's permuted order and batches of one,
+    DeblurENeRF.validation_step (render_pixels over the view's pixel grid at its pose, eval mode)
+    and validation_epoch_end (the gather; the affine log-intensity correction; with
+    ``black_level_offset`` the OffsetGammaCorrection refinement by the reference's own
+    external/optimizer.py on oracle/pypose.py; Metric (l1, psnr, ssim via oracle/metrics.py); the
+    correction-error CSV, the logged images and the saved 8-bit predictions) -- twice, the second
+    evaluation warm-started from the first's converged correction.  The targets are the reference
+    model's own renders under a known gamma / scale / black level, quantised; the radiance output
+    layer's weights are scaled by ``rgb_weight_scale`` so the renders span a wide intensity range (a
+    random-init field renders an almost flat image, on which the correction's scale and gamma
+    columns are collinear and its refinement ill-conditioned)."""
+    cfg = _step_cfg(rd=rd)
+    cal, poses = synthetic_dataset_arrays(rd)
+    d = tempfile.mkdtemp(prefix="den_evalep_")
+    write_dataset(d, cal, poses)
+    m = ref_deblur_step_module(d, seed, cfg)
+    with torch.no_grad():
+        m.nerf.radiance_field.mlp.sigma_layer.output_layer.bias.add_(sigma_bias_shift)
+        m.nerf.radiance_field.mlp.rgb_layer.output_layer.weight.mul_(rgb_weight_scale)
+    torch.manual_seed(300)
+    m.nerf.update_occ_grid(step=0, T_wc_position=m.trajectory.T_wc_position)
+    grid = m.nerf.occupancy_grid
+    m.eval()
+    ds = _refload.load("data.datasets")
+    _refload.load("external.optimizer")  # deblur_e_nerf.py reaches it as external.optimizer (pypose stand-in)
+    install_cv2()
+    ED = sys.modules["easydict"].EasyDict
+    # the views: renders of the reference model at 3 poses, mapped through a gamma / scale / black level,
+    # quantised to 8 bits, RGBA with an opaque alpha (display renders)
+    views = os.path.join(d, "views")
+    os.makedirs(os.path.join(views, "val"))
+    fov = 0.9
+    f = (W / 2) / np.tan(fov / 2)
+    K = torch.tensor([[f, 0, W / 2 - 0.5], [0, f, H / 2 - 0.5], [0, 0, 1]], dtype=torch.float32)
+    pix = torch.stack(torch.meshgrid(torch.arange(W), torch.arange(H), indexing="xy"), dim=2).float()
+    frames = []
+    g = np.random.default_rng(seed)
+    for k, T in enumerate(_view_poses(3, seed + 1)):
+        rot = torch.tensor(T[:3, :3] @ np.diag([1.0, -1.0, -1.0]), dtype=torch.float32)
+        pos = torch.tensor(T[:3, 3], dtype=torch.float32)
+        with torch.no_grad():
+            img, _, _, _, _ = m.render_pixels(torch.linalg.inv(K), pix, pos.view(1, 1, 3).expand(H, W, -1),
+                                              rot.view(1, 1, 3, 3).expand(H, W, -1, -1))
+        lin = img.numpy().astype(np.float64)
+        print(f"[eval_epoch rd={rd}] view {k}: render range {lin.min():.4f}..{lin.max():.4f}")
+        lin = 0.9 * np.power(lin / lin.max(), 0.8) + 0.03 + 0.01 * g.normal(size=lin.shape)
+        q = np.round(np.clip(lin, 0, 1) * 255).astype(np.uint8)
+        # a monochrome sensor gets RGB files (converted to grey; the reference converts only 3-channel
+        # views, datasets.py:639-644), a Bayer sensor RGBA ones alpha-composited over white
+        rgb = np.stack([q] * 3, -1) if rd == 1 else q.transpose(1, 2, 0)
+        if rd == 3:
+            alpha = np.full(rgb.shape[:2] + (1,), 255, np.uint8)
+            alpha[:3, :4] = 128
+            rgb = np.concatenate([rgb, alpha], -1)
+        path = os.path.join(views, "val", f"r_{k}.png")
+        with open(path, "wb") as fh:
+            fh.write(encode_png(rgb, 8))
+        IMREAD_TRUTH[os.path.realpath(path)] = _bgr(rgb)
+        frames.append({"file_path": f"./val/r_{k}", "transform_matrix": T.tolist()})
+    with open(os.path.join(views, "transforms_val.json"), "w") as fh:
+        json.dump({"camera_angle_x": fov, "frames": frames}, fh)
+    np.savez(os.path.join(d, "renderer_params.npz"), interm_color_space=np.array("display"), log_eps=np.array(0.001))
+    # DeblurENeRF.__init__'s evaluation state (deblur_e_nerf.py:96-127, 164-197)
+    vp = ds.PosedImage(d, "val", permutation_seed=None)
+    m.val_min_normalized_pixel_value = vp.min_normalized_pixel_value
+    m.val_max_normalized_pixel_value = vp.max_normalized_pixel_value
+    m.register_buffer("val_intrinsics_inv", vp.posed_imgs.intrinsics.inverse(), persistent=False)
+    m.register_buffer("val_img_pixel_pos", torch.stack(torch.meshgrid(torch.arange(W), torch.arange(H), indexing="xy"),
+                                                       dim=2).to(torch.get_default_dtype()), persistent=False)
+    m.correction = ED(per_channel_log_it_scale=False, black_level_offset=black_level_offset,
+                      optimizer=ED(algo=algo, max_steps=10, lm=ED(radius=1.0e6)))
+    rdim = 3 if m.has_bayer_filter else 1
+    if black_level_offset:
+        m.init_correction_scale = torch.ones((rdim, 1, 1, 1), dtype=torch.float64)
+        m.init_correction_offset = torch.zeros((rdim, 1, 1, 1), dtype=torch.float64)
+        m.init_correction_gamma = torch.ones((rdim if not m.has_bayer_filter else 1, 1, 1, 1), dtype=torch.float64)
+    m.metric = _refload.load("loss_metric.metric").Metric("alex")
+    m.eval_save_pred_intensity_img = True
+    logdir = tempfile.mkdtemp(prefix="den_evallog_")
+    m.trainer = types.SimpleNamespace(log_dir=logdir, is_global_zero=True, sanity_checking=False,
+                                      accumulate_grad_batches=1)
+    m.logger = _ImgLogger()
+    m.device = torch.device("cpu")
+    m.all_gather = lambda t: t  # PL single-device all_gather
+    logged = {}
+    m.log = lambda name, value, **kw: logged.__setitem__(name, value)
+    # the DataModule's val set: PosedImage with the config's permutation seed and alpha over white
+    val = ds.PosedImage(d, "val", 9, rd == 3)
+    out = dict(rd=rd, seed=seed, N=0, S=8, pixbw=False, res=cfg["res"], sigma_bias_shift=sigma_bias_shift,
+               rgb_weight_scale=rgb_weight_scale, occ_u=grid.last_u.numpy(), occs=grid.occs.numpy(), black_level_offset=black_level_offset,
+               algo=np.array(algo), eval_perm_seed=9, alpha_over_white_bg=rd == 3,
+               **{f"cal:{k}": v for k, v in cal.items()}, **{f"pose:{k}": v for k, v in poses.items()})
+    base = d
+    for dirpath, _, names in os.walk(os.path.join(d, "views")):
+        for nm in names:
+            full = os.path.join(dirpath, nm)
+            with open(full, "rb") as fh:
+                out["file:" + os.path.relpath(full, base)] = np.frombuffer(fh.read(), dtype=np.uint8)
+    with open(os.path.join(d, "renderer_params.npz"), "rb") as fh:
+        out["file:renderer_params.npz"] = np.frombuffer(fh.read(), dtype=np.uint8)
+    for ev in range(2):
+        m.current_epoch = ev
+        logged.clear()
+        sys.modules["cv2"].written.clear()
+        m.logger.images.clear()
+        outputs = []
+        with torch.no_grad():
+            for i in range(len(val)):
+                batch = torch.utils.data.default_collate([val[i]])
+                outputs.append(m.validation_step(batch, i))
+        p = f"ev{ev}:"
+        out[p + "pred"] = torch.stack([o["pred_intensity_img"] for o in outputs]).numpy()
+        with torch.no_grad():
+            m.validation_epoch_end(outputs)
+        for k, v in logged.items():
+            out[p + "log:" + k] = np.array(float(v))
+        if black_level_offset:
+            out[p + "init_scale"] = m.init_correction_scale.numpy()
+            out[p + "init_gamma"] = m.init_correction_gamma.numpy()
+            out[p + "init_offset"] = m.init_correction_offset.numpy()
+            out[p + "errors"] = np.loadtxt(os.path.join(logdir, "correction-errors", f"{ev}.csv"), ndmin=1)
+        for k, v in m.logger.images.items():
+            out[p + "image:" + k] = v
+        for k, v in sys.modules["cv2"].written.items():
+            out[p + "saved:" + k] = v
+    save(tag or f"eval_epoch_rd{rd}.npz", **out)
+
+
+def gen_eval_epoch_all():
+    gen_eval_epoch(1, seed=6)
+    gen_eval_epoch(3, seed=8, algo="gn", tag="eval_epoch_rd3_gn.npz")
+    gen_eval_epoch(1, seed=10, black_level_offset=False, tag="eval_epoch_rd1_affine.npz")
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.set_num_threads(8)
     for name in sys.argv[1:]:
@@ -1366,3 +1706,5 @@ elif __name__ == "__main__":
     gen_step(True, 1)
     gen_ngp_all()
     gen_queue()
+    gen_posed()
+    gen_eval_epoch_all()

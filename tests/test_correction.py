@@ -164,3 +164,43 @@ def test_black_level_refinement_bayer_shapes():
     assert [tuple(v.shape) for v in r.converged] == [(3, 1, 1, 1), (1, 1, 1, 1), (3, 1, 1, 1)]
     assert r.scale.shape == (3,) and r.gamma.shape == (1,) and r.offset.shape == (3,)  # (:806-810, :924-928)
     assert float((r.pred - target.double()).abs().max()) < 1e-3
+
+
+@pytest.mark.parametrize("name", ["eval_epoch_rd1", "eval_epoch_rd3_gn", "eval_epoch_rd1_affine"])
+def test_correction_on_reference_eval_renders(name):
+    """evaluation_correction on the renders and views of the reference's validation loop
+    (tests/golden/eval_epoch_*.npz): the refinement's converged parameters -- the warm start the next
+    evaluation starts from -- and its error log match the reference's evaluation_epoch_end
+    (deblur_e_nerf.py:842-949, run on oracle/pypose.py) over two evaluations."""
+    import os
+    from test_posed_image import build_views_dir
+    from deblur_e_nerf.data.datasets import PosedImage
+    from deblur_e_nerf.models.deblur_e_nerf import init_correction_params
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", f"{name}.npz"))
+    files = {k: z[k] for k in z.files}
+    files["root"] = np.array(".")
+
+    class _Z(dict):
+        pass
+    zz = _Z(files)
+    zz.files = list(files)
+    root = build_views_dir(zz)
+    np.savez(os.path.join(root, "camera_calibration.npz"), **{k[4:]: z[k] for k in z.files if k.startswith("cal:")})
+    rd = int(z["rd"])
+    target = PosedImage(root, "val", int(z["eval_perm_seed"]), bool(z["alpha_over_white_bg"])).posed_imgs.img
+    blo = bool(z["black_level_offset"])
+    cfg = EasyDict(per_channel_log_it_scale=False, black_level_offset=blo,
+                   optimizer=EasyDict(algo=str(z["algo"]), max_steps=10, lm=EasyDict(radius=1.0e6)))
+    init = init_correction_params(rd == 3, False) if blo else None
+    for ev in range(2):
+        res = evaluation_correction(torch.from_numpy(z[f"ev{ev}:pred"]), target, None, rd == 3, cfg, init=init)
+        if not blo:
+            assert res.errors is None
+            continue
+        ref = z[f"ev{ev}:errors"]
+        assert res.errors.shape == ref.shape and np.allclose(res.errors.numpy(), ref, rtol=1e-9, atol=0), \
+            (res.errors.numpy(), ref)
+        for got, nm in zip(res.converged, ("scale", "gamma", "offset")):
+            assert got.shape == z[f"ev{ev}:init_{nm}"].shape
+            assert np.allclose(got.numpy(), z[f"ev{ev}:init_{nm}"], rtol=1e-9, atol=1e-12), nm
+        init = res.converged

@@ -46,10 +46,12 @@ def _fx(z, key, default):
     return z[key].item() if key in z.files else default
 
 
-def build_model(z, mode="f32", sampler="occupancy"):
+def build_model(z, mode="f32", sampler="occupancy", correction=None, eval_save=False, return_dir=False):
     """DeblurENeRF with the fixture's configuration (make_golden.gen_step: the chair-like defaults,
     or a step config's arch / contraction / aabb / near / far / cone / TV weight / learnable pixel
-    bandwidth, e.g. configs[3]'s composition in step_ziggy_rd1.npz)."""
+    bandwidth, e.g. configs[3]'s composition in step_ziggy_rd1.npz).  A fixture holding evaluation
+    views (``file:`` entries, make_golden.gen_eval_epoch) has them written into the dataset
+    directory first, so the constructor loads them (deblur_e_nerf.py:96-162)."""
     from deblur_e_nerf.models.deblur_e_nerf import DeblurENeRF
     from deblur_e_nerf.utils.easydict import EasyDict as ED
     d = tempfile.mkdtemp(prefix="den_step_")
@@ -58,6 +60,12 @@ def build_model(z, mode="f32", sampler="occupancy"):
     np.savez(os.path.join(d, "camera_calibration.npz"), **cal)
     np.savez(os.path.join(d, "camera_poses.npz"), **poses)
     torch.save(torch.tensor(1_000_000), os.path.join(d, "max_refractory_period.pt"))
+    for k in z.files:
+        if k.startswith("file:"):
+            path = os.path.join(d, k[len("file:"):])
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            with open(path, "wb") as f:
+                f.write(z[k].tobytes())
     rd, S = int(z["rd"]), int(z["S"])
     aabb = [float(v) for v in z["aabb"]] if "aabb" in z.files else [-1.5, -1.5, -1.5, 1.5, 1.5, 1.5]
     nerf_cfg = ED(aabb=aabb, contraction_type=str(z["contraction"]) if "contraction" in z.files else "aabb",
@@ -72,13 +80,13 @@ def build_model(z, mode="f32", sampler="occupancy"):
     pixbw_free = bool(_fx(z, "pixbw_free", False))
     pb_names = ("tau_mil_it_eff_prod", "A_amp_inv", "A_loop_inv", "tau_out", "tau_sf", "tau_diff")
     m = DeblurENeRF(
-        "test", ["novel_view"], 1, [0], 0.001, False, None,
+        "test", ["novel_view"], 1, [0], 0.001, eval_save, None,
         ED(parameterize_mean_ct=True, load_state_dict=False,
            freeze=ED(p2n_contrast_threshold_ratio=False, mean_contrast_threshold=False, default=False)),
         ED(load_state_dict=False, freeze=False),
         ED(enable=bool(z["pixbw"]), it_sample_size=S, f_c_dominant_min=21, target_cumprob=ED(max_sample_lifetime=0.95),
            load_state_dict=False, freeze=ED(default=not pixbw_free, **{n: not pixbw_free for n in pb_names})),
-        nerf_cfg, ED(per_channel_log_it_scale=False, black_level_offset=True),
+        nerf_cfg, correction if correction is not None else ED(per_channel_log_it_scale=False, black_level_offset=True),
         ED(weight=ED(log_intensity_diff=1.0, log_intensity_tv=float(_fx(z, "tv", 1e-3)), nerf_mlp_weight_decay=1e-6),
            error_fn=ED(log_intensity_diff="huber", log_intensity_tv="l1"),
            normalize=ED(log_intensity_diff=True, log_intensity_tv=True)),
@@ -101,7 +109,9 @@ def build_model(z, mode="f32", sampler="occupancy"):
     m = m.to(DEV)
     with torch.no_grad():
         m.nerf.radiance_field.mlp.sigma_layer.output_layer.bias.add_(float(z["sigma_bias_shift"]))
-    return m
+        if "rgb_weight_scale" in z.files:
+            m.nerf.radiance_field.mlp.rgb_layer.output_layer.weight.mul_(float(z["rgb_weight_scale"]))
+    return (m, d) if return_dir else m
 
 
 def _rel(a, b):

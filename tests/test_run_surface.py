@@ -107,3 +107,74 @@ def test_datamodule_rejects_workers():
     with pytest.raises(ValueError):
         DataModule(0, ["novel_view"], 1, [0], EasyDict(enable=False), "/nonexistent", 1.0, 1.0, 1.0, None, 9, True,
                    256, 131072, 1, 1, 4)
+
+
+@pytest.mark.parametrize("name", ["synthetic.yaml", "07_ziggy_and_fuzz_hdr.yaml"])
+def test_run_py_val_test_surface(name):
+    """run.py val|test (scripts/run.py:114-118): with a views/ folder the DataModule's val / test sets
+    are PosedImage views (event_view: the training views' images; novel_view: transforms_val/test),
+    the model holds each stage's intrinsics inverse, pixel grid and value range
+    (deblur_e_nerf.py:96-162), and the loaders yield the batches validation_step / test_step take.
+    Without views/, validation raises (the reference cannot even be constructed then)."""
+    import deblur_e_nerf as den
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "eval_epoch_rd1.npz"))
+    config = _load(name)
+    d = _dataset_dir(rd=1)
+    for k in z.files:
+        if k.startswith("file:views/"):
+            rel = k[len("file:"):]
+            if config.eval_target == ["event_view"]:
+                rel = rel.replace("transforms_val", "transforms_train")
+            path = os.path.join(d, rel)
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            with open(path, "wb") as f:
+                f.write(z[k].tobytes())
+    config.data.dataset_directory = d
+    config.data.alpha_over_white_bg = False  # the views are RGB (no alpha channel)
+    config.data.val_dataset_ratio = 1.0
+    config.data.test_dataset_ratio = 1.0
+    config.git_head_hash, config.seed = "test", 0
+    datamodule = den.data.datamodule.DataModule(
+        config.seed, config.eval_target, config.trainer.num_nodes, config.trainer.gpus, config.model.pixel_bandwidth,
+        **config.data)
+    model = den.models.deblur_e_nerf.DeblurENeRF(
+        config.git_head_hash, config.eval_target, config.trainer.num_nodes, config.trainer.gpus,
+        config.model.min_modeled_intensity, config.model.eval_save_pred_intensity_img,
+        config.model.checkpoint_filepath, config.model.contrast_threshold, config.model.refractory_period,
+        config.model.pixel_bandwidth, config.model.nerf, config.model.correction, config.loss, config.metric,
+        config.optimizer, config.lr_scheduler, config.data.dataset_directory, config.data.alpha_over_white_bg,
+        config.data.train_eff_ray_sample_batch_size)
+    H, W = 20, 24
+    assert model.val_img_pixel_pos.shape == (H, W, 2) and model.val_intrinsics_inv.shape == (3, 3)
+    assert model.val_min_normalized_pixel_value == 0.5 / 256
+    assert model.val_max_normalized_pixel_value == 1 - 0.5 / 256
+    if config.eval_target == ["event_view"]:  # the test stage reuses the val views
+        assert torch.equal(model.test_intrinsics_inv, model.val_intrinsics_inv)
+    else:  # no transforms_test.json: the test stage stays empty (deblur_e_nerf.py:161-162)
+        assert model.test_intrinsics_inv is None
+    assert model.init_correction_gamma.shape == (1, 1, 1, 1)
+    datamodule.setup("validate")
+    b = next(iter(datamodule.val_dataloader()))
+    assert b["img"].shape == (1, H, W) and b["sample_id"].shape == (1, 16)
+    assert b["T_wc_position"].shape == (1, 3) and b["T_wc_orientation"].shape == (1, 3, 3)
+    assert len(datamodule.val_dataset) == 3
+    if config.eval_target == ["event_view"]:
+        datamodule.setup("test")
+        assert len(datamodule.test_dataset) == 3
+    else:
+        with pytest.raises(FileNotFoundError):
+            datamodule.setup("test")
+    if config.eval_target != ["event_view"]:
+        with pytest.raises(RuntimeError):  # no test views: test_step names what is missing
+            model.test_step(b, 0)
+
+
+def test_val_without_views_raises():
+    from deblur_e_nerf.data.datamodule import DataModule
+    from deblur_e_nerf.utils.easydict import EasyDict
+    dm = DataModule(0, ["novel_view"], 1, [0], EasyDict(enable=False), _dataset_dir(), 1.0, 1.0, 1.0, None, 9, True,
+                    256, 131072, 1, 1, 0)
+    dm.setup("fit")
+    assert dm.val_dataset is None
+    with pytest.raises(FileNotFoundError):
+        dm.setup("validate")
