@@ -450,7 +450,12 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
         // head (compositing adjoint, Lr^T + dW_r, Lg^T + dW_g) sample-major and persistent, then Lb,
         // L7..L1 layer-major.  The Lg partial shares dw_partial with the hidden launches: reduced first.
         const int64_t items = n / wg_samples(MODE);
-        const int head_grid = (int)std::min<int64_t>(items, HB_GRID_MAX);
+        // one persistent workgroup per CU, as the forward; at most what the split-K partial region
+        // holds (4 x 10 tiles per workgroup; ws_layout sizes it for the hidden launches' 256 x 9 x 9,
+        // i.e. >= 518 head workgroups) and the Lr partials (one per item)
+        const int64_t dw_cap = (int64_t)(L.lr_partial - L.dw_partial) / (4 * 10 * 1024 * 4);
+        const int head_grid = (int)std::max<int64_t>(
+            1, std::min<int64_t>({items, (int64_t)device_cu_count(s), dw_cap}));
         {
           DEN_TIMED(T_RENDER_BWD, s);
           hipLaunchKernelGGL(render_head_bwd_kernel, dim3((unsigned)head_grid), dim3(512), 0, s, A,
@@ -537,6 +542,15 @@ int den_debug_fwd_prof(uint64_t* out) {
 int den_debug_clock(uint64_t* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(den_clock), sizeof(uint64_t) * DEN_CLOCK_KERNELS * DEN_CLOCK_WGS * 4) ==
                  hipSuccess
+             ? DEN_OK
+             : DEN_EHIP;
+}
+#endif
+
+#ifdef DEN_HIDDEN_PROF
+// experiment builds only: per-wave phase cycles of the last L7..L1 and Lb launches (2 x 256 WGs x 4 waves x 8)
+int den_debug_hidden_prof(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(den_hidden_prof), sizeof(uint64_t) * 2 * 256 * 4 * 8) == hipSuccess
              ? DEN_OK
              : DEN_EHIP;
 }

@@ -38,6 +38,33 @@ constexpr int HB_STORE_OPS = 4;                          // dz_{l-1} stores per 
 
 typedef short hb_v4i16 __attribute__((ext_vector_type(4)));
 
+// Experiment builds only (-DDEN_HIDDEN_PROF, profiles/hidden_prof.py): per-wave cycle split of a launch
+// by s_memtime marks -- 0 DMA issue, 1 chain (dz fragments + W^T MFMAs, Lb's sigma k-step), 2 epilogue
+// (activation derivative + dz stores), 3 dW / db, 4 Lb's sigma weight-gradient row, 5 vmcnt wait for the
+// next block, 6 barrier, 7 the whole launch; slot 0 = the last L7..L1 launch, slot 1 = Lb.
+struct HbProf {
+#ifdef DEN_HIDDEN_PROF
+  uint64_t p[8];
+  uint64_t t;
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) p[q] = 0;
+    t = __builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void mark(int q) {
+    const uint64_t n = __builtin_amdgcn_s_memtime();
+    p[q] += n - t;
+    t = n;
+  }
+#else
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void mark(int) {}
+#endif
+};
+#ifdef DEN_HIDDEN_PROF
+__device__ uint64_t den_hidden_prof[2 * 256 * 4 * 8];
+#endif
+
 struct HiddenArgs {
   const char* w;      // packed transposed weights of the layer (bwd chunk 0 of layer j, 16 KiB per row tile)
   const char* dz_in;  // dz_l
@@ -131,20 +158,30 @@ __device__ __forceinline__ void hb_wait_vm_lgkm0() {
 }
 
 // One 32-sample block from its LDS slot: the chain (dz_{l-1} stored), then the dW / db accumulation.
-// Sigma's weight-gradient row of one block (LB, see hb_block): S7 tiles 2w, 2w + 1 (transposed
-// reads, k = samples) against sigma's dz as the B operand of a tile whose only nonzero feature is
-// sigma -- in column 0 for tile 2w, column 16 for tile 2w + 1 -- into one accumulator.  Column
-// (lane & 31) of a B operand holds k-slots 8 (lane >> 5) + j = samples 16 kk + 8 (lane >> 5) + j:
-// eight consecutive entries of the block's sigma array.
-__device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, f32x16& sacc) {
+// Sigma's weight-gradient row of one block (LB, see hb_block): dW_sigma[q] = sum_n dz_sigma[n] S7[n][q]
+// for the wave's S7 tiles 2w, 2w + 1 by VALU dot products: the transposed fragment of an S7 tile
+// (hb_tr_frag: lane l holds stored position l & 31 of the tile at samples 16 kk + 8 (l >> 5) + j) times
+// the same eight samples' sigma dz, four v_dot2c_f32_bf16 per fragment, into one f32 per tile and lane
+// (the two lane halves hold the two sample halves; added at the end).  r06: this replaced four
+// dependent 32x32x16 MFMAs into one accumulator per block (tile 2w in column 0, 2w + 1 in column 16 of
+// a 16-register tile) -- 703 cycles per block of the Lb launch's 5.5 k (DEN_HIDDEN_PROF,
+// profiles/r06c_hidden_prof.json), the MFMA chain's latency exposed -- and frees 14 registers.
+__device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, float (&sd)[2]) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   __builtin_amdgcn_sched_barrier(0);  // its operands are not read ahead into the previous phase (registers)
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
-    const bf16x8 sv = *(const bf16x8*)(sig + 32 * kk + 16 * (lane >> 5)), zero = {};
-    const bf16x8 b0 = (lane & 31) == 0 ? sv : zero, b1 = (lane & 31) == 16 ? sv : zero;
-    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hb_tr_frag(sb + (2 * wave) * HB_TILE, kk), b0, sacc, 0, 0, 0);
-    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hb_tr_frag(sb + (2 * wave + 1) * HB_TILE, kk), b1, sacc, 0, 0, 0);
+    const bf16x8 sv = *(const bf16x8*)(sig + 32 * kk + 16 * (lane >> 5));
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const bf16x8 a = hb_tr_frag(sb + (2 * wave + t) * HB_TILE, kk);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bf16x2_t x = {a[2 * q], a[2 * q + 1]}, y = {sv[2 * q], sv[2 * q + 1]};
+        sd[t] = __builtin_amdgcn_fdot2_f32_bf16(x, y, sd[t], false);
+      }
+    }
   }
 }
 
@@ -152,13 +189,12 @@ __device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, f32
 // bottleneck tiles, sigma's dz arrives as 32 bf16 per block (staged after them); the chain takes it as
 // a 17th k-step whose B fragment holds sigma at stored position 0 (W_b^T's sigma column; the rest of
 // that k-step and the 18th are zero padding).  Sigma's weight-gradient row would be a ninth row tile
-// of 8 more accumulator tiles; instead wave w computes S7 tile^T x [sigma as a one-feature tile] for
-// its S7 tiles 2w, 2w + 1 into one shared accumulator, tile 2w in column 0 and 2w + 1 in column 16
-// (hb_sigma_dw).
+// of 8 more accumulator tiles; instead wave w forms the row for its S7 tiles 2w, 2w + 1 by VALU dot
+// products (hb_sigma_dw).
 template <bool LB>
 __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, int64_t b,
                                          const bf16x8 (&wt)[2][LB ? 17 : 16], f32x16 (&dw)[2][8], float (&db)[2],
-                                         f32x16& sacc, float& sdb) {
+                                         float (&sd)[2], float& sdb, HbProf& hp) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int DZ_BYTES = LB ? HB_BLOCK + HB_SIG : HB_BLOCK;
   const char* dzb = cur;
@@ -172,6 +208,14 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) accs[t][r] = 0.0f;
+  // the epilogue's S'_{l-1} fragments (the activation derivative's input), read before the chain so
+  // that their LDS latency hides under its 32 MFMAs instead of opening each tile's epilogue
+  bf16x8 sf[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int f = 0; f < 2; ++f) sf[t][f] = hb_frag(sb + (2 * wave + t) * HB_TILE, f);
+  __builtin_amdgcn_sched_barrier(0);  // (left alone, the compiler sinks these reads back to their use)
   {
     bf16x8 bq[HB_PF];
 #pragma unroll
@@ -192,12 +236,12 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     accs[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[1][16], bs, accs[1], 0, 0, 0);
     sdb += (float)bs[0];
   }
+  hp.mark(1);
   // then the activation derivative
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     f32x16 acc = accs[t];
-    const char* st = sb + (2 * wave + t) * HB_TILE;
-    const bf16x8 s0 = hb_frag(st, 0), s1 = hb_frag(st, 1);
+    const bf16x8 s0 = sf[t][0], s1 = sf[t][1];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float sv = (float)(r < 8 ? s0[r] : s1[r - 8]);
@@ -213,6 +257,7 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     // in 128 VGPRs and dW in all 256 AGPRs for the whole launch)
     __builtin_amdgcn_sched_barrier(0);
   }
+  hp.mark(2);
   // weight / bias gradients over the block's 32 samples (two k-steps of 16)
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
@@ -230,9 +275,13 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
       db[1] += (float)a1[j];
     }
   }
+  hp.mark(3);
   // sigma's weight-gradient row last (placed between the chain and the epilogue or before the dW
   // MFMAs its operands spill registers or it measured slower: r03)
-  if constexpr (LB) hb_sigma_dw(sig, sb, sacc);
+  if constexpr (LB) {
+    hb_sigma_dw(sig, sb, sd);
+    hp.mark(4);
+  }
 }
 
 template <bool LB>
@@ -285,10 +334,13 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dw[t][n][r] = 0.0f;
   float db[2] = {0.0f, 0.0f};  // bias partial: feature (lane & 31) of row tile 2w + t, this lane's samples
-  f32x16 sacc;  // LB: sigma's weight-gradient row, S7 tile 2w in column 0, 2w + 1 in column 16
-#pragma unroll
-  for (int r = 0; r < 16; ++r) sacc[r] = 0.0f;
+  float sd[2] = {0.0f, 0.0f};  // LB: sigma's weight-gradient row, stored position lane & 31 of S7 tile 2w + t
   float sdb = 0.0f;  // LB: sigma's bias gradient (lanes 0..31)
+  HbProf hp;
+  hp.init();
+#ifdef DEN_HIDDEN_PROF
+  const uint64_t hp_start = hp.t;
+#endif
   hb_wait_vm_lgkm0<0>();       // block b0 (and the prologue prefetches) landed
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -296,16 +348,27 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
 
   for (int64_t it = 0; it < n_it; ++it) {
     const int u = (int)(it % HB_RING);
+    hp.mark(6);
     // prefetch block it + HB_DEPTH into the slot block it - 1 used (free since the last barrier)
     if (it + HB_DEPTH < n_it) fetch(blk(it + HB_DEPTH), lds + ((u + HB_DEPTH) % HB_RING) * SLOT);
-    hb_block<LB>(P, lds + u * SLOT, blk(it), wt, dw, db, sacc, sdb);
+    hp.mark(0);
+    hb_block<LB>(P, lds + u * SLOT, blk(it), wt, dw, db, sd, sdb, hp);
     if (it + HB_DEPTH < n_it) hb_wait_vm_lgkm0<YOUNGER>();
     else hb_wait_vm_lgkm0<0>();
+    hp.mark(5);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
+  hp.mark(6);
   DEN_CLOCK_END(LB ? 3 : 2);
+#ifdef DEN_HIDDEN_PROF
+  hp.p[7] = hp.t - hp_start;
+  if (blockIdx.x < 256 && lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) den_hidden_prof[((LB ? 256 : 0) + blockIdx.x) * 32 + wave * 8 + q] = hp.p[q];
+  }
+#endif
   // split-K partial of this workgroup (dw_gemm_kernel layout: [wg][mt][nt][lane][16]); the bias
   // goes where that layout's ones tile (nt = 8) keeps it: column 0 = lanes 0 and 32, row m in
   // register (m & 3) + 4 (m >> 3) of lane 32 ((m >> 2) & 1)
@@ -320,17 +383,11 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   }
   if constexpr (LB) {
     // row tile 8 = [sigma, 31 padding rows]: sigma is accumulator row 0 (lanes 0..31, register 0),
-    // column 32 n + lane; every other element of the tiles written as zero.  S7 feature q of tile
-    // 2w + nn sits in sacc's column 16 nn, row q = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    // column 32 n + lane; every other element of the tiles written as zero.  Stored position q of S7
+    // tile 2w + nn: sd[nn] of lanes q and q + 32 (the two sample halves)
 #pragma unroll
     for (int nn = 0; nn < 2; ++nn) {
-      const int q = lane & 31, rsel = (q & 3) + 4 * (q >> 3), src = 16 * nn + 32 * ((q >> 2) & 1);
-      float v = 0.0f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float x = __shfl(sacc[r], src, 64);
-        v = r == rsel ? x : v;
-      }
+      const float v = sd[nn] + __shfl_xor(sd[nn], 32, 64);
       float* o = P.partial + (((int64_t)blockIdx.x * MTA + 8) * 9 + 2 * wave + nn) * 1024 + lane * 16;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
