@@ -107,6 +107,11 @@ constexpr int64_t DW_BLOCK_MAX = 9LL * 11 * 1024;  // floats per split, bound ov
 // persistent workgroups of the layer-major hidden backward: one per CU, at most one per wave block
 constexpr int LR_G1 = 1024;  // stage-1 rows of the fused Lr weight-gradient reduction (at most)
 inline int64_t hidden_grid(int64_t n_samples) { return std::min<int64_t>(HB_GRID_MAX, std::max<int64_t>(1, n_samples / 32)); }
+// the grid of a persistent launch of this render call: at most desc.max_workgroups when it is set
+inline int64_t cap_grid(const den_render_desc* d, int64_t g) {
+  return d->max_workgroups > 0 ? std::max<int64_t>(1, std::min<int64_t>(g, d->max_workgroups)) : g;
+}
+inline int64_t hidden_grid(const den_render_desc* d) { return cap_grid(d, hidden_grid((int64_t)d->n_rays * d->n_samples)); }
 
 // BF16 backward: layer-major hidden layers (den_hidden.hip) unless the descriptor selects the
 // sample-major chain + split-K GEMMs of the F32 mode (bwd_path = 1, A/B comparisons).
@@ -184,6 +189,7 @@ int check_desc(const den_render_desc* d) {
     return fail(DEN_EUNSUPPORTED, "the fixed-count sampler (points = 0) marches the AABB: contraction must be 0");
   if (d->density_activation < 0 || d->density_activation > 2)
     return fail(DEN_EINVAL, "density_activation must be 0 (shifted_trunc_exp), 1 (softplus) or 2 (shifted_softplus)");
+  if (d->max_workgroups < 0) return fail(DEN_EINVAL, "max_workgroups must be >= 0 (0: one workgroup per CU)");
   return DEN_OK;
 }
 
@@ -280,7 +286,7 @@ int launch_dwstream(const den_render_desc* d, const WsLayout& L, char* ws, int a
   P.partial = (float*)(ws + L.dw_partial);
   static_assert(U == 1 || U == 2 || U == 4 || U == 8, "U divides the wave blocks (n is a multiple of 256)");
   P.n_blocks = n / 32 / U;
-  const int64_t grid = hidden_grid(n);
+  const int64_t grid = hidden_grid(d);
   P.per_wg = (P.n_blocks + grid - 1) / grid;
   {
     DEN_TIMED(T_DW_GEMM, s);
@@ -297,7 +303,7 @@ int launch_dwstream_reduce(const den_render_desc* d, const WsLayout& L, char* ws
                            int splits = -1) {
   DwReduceArgs R{};
   R.partial = (float*)(ws + L.dw_partial);
-  R.splits = splits > 0 ? splits : (int)hidden_grid((int64_t)d->n_rays * d->n_samples);
+  R.splits = splits > 0 ? splits : (int)hidden_grid(d);
   R.MT = MT;
   R.NT = NT_ALL;
   R.m_off = 0;
@@ -361,7 +367,7 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   H.dz_out = ws + L.act[D_Z0 + l - 1];
   H.partial = (float*)(ws + L.dw_partial);
   H.n_blocks = n / 32;
-  const int64_t grid = hidden_grid(n);
+  const int64_t grid = hidden_grid(d);
   H.per_wg = (H.n_blocks + grid - 1) / grid;
   {
     TimedLaunch timed_(lb ? T_HIDDEN_LB : T_HIDDEN_BWD, s);
@@ -418,7 +424,7 @@ int render_fwd_impl(const den_render_desc* d, const den_render_io* io, hipStream
   A.n_items = n / fwd_wg_samples(MODE);
   // persistent: one workgroup per CU (the 143 KB weight ring + records admit one), each walking
   // items blockIdx.x, blockIdx.x + grid, ...
-  const unsigned grid = (unsigned)std::min<int64_t>(A.n_items, device_cu_count(s));
+  const unsigned grid = (unsigned)cap_grid(d, std::min<int64_t>(A.n_items, device_cu_count(s)));
   {
     DEN_TIMED(T_RENDER_FWD, s);
     if (d->train)
@@ -454,8 +460,8 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
         // holds (4 x 10 tiles per workgroup; ws_layout sizes it for the hidden launches' 256 x 9 x 9,
         // i.e. >= 518 head workgroups) and the Lr partials (one per item)
         const int64_t dw_cap = (int64_t)(L.lr_partial - L.dw_partial) / (4 * 10 * 1024 * 4);
-        const int head_grid = (int)std::max<int64_t>(
-            1, std::min<int64_t>({items, (int64_t)device_cu_count(s), dw_cap}));
+        const int head_grid = (int)cap_grid(d, std::max<int64_t>(
+            1, std::min<int64_t>({items, (int64_t)device_cu_count(s), dw_cap})));
         {
           DEN_TIMED(T_RENDER_BWD, s);
           hipLaunchKernelGGL(render_head_bwd_kernel, dim3((unsigned)head_grid), dim3(512), 0, s, A,

@@ -28,7 +28,8 @@ class RenderDesc(ctypes.Structure):
                 ("n_samples", ctypes.c_int32), ("aabb", ctypes.c_float * 6), ("near_plane", ctypes.c_float),
                 ("far_plane", ctypes.c_float), ("train", ctypes.c_int32), ("has_bkgd", ctypes.c_int32),
                 ("points", ctypes.c_int32), ("contraction", ctypes.c_int32), ("bwd_path", ctypes.c_int32),
-                ("density_activation", ctypes.c_int32), ("ray_grad", ctypes.c_int32)]
+                ("density_activation", ctypes.c_int32), ("ray_grad", ctypes.c_int32),
+                ("max_workgroups", ctypes.c_int32)]
 
 
 class RenderIO(ctypes.Structure):
@@ -158,7 +159,7 @@ _SIGS = {
 }
 
 
-ABI_VERSION = 6  # include/den_api.h DEN_VERSION
+ABI_VERSION = 7  # include/den_api.h DEN_VERSION
 
 
 def lib():

@@ -69,7 +69,8 @@
 extern "C" {
 #endif
 
-#define DEN_VERSION 6  /* 6: den_ssim / den_png_unfilter (the evaluation views and metrics);
+#define DEN_VERSION 7  /* 7: den_render_desc.max_workgroups (two render calls sharing the chip);
+                          6: den_ssim / den_png_unfilter (the evaluation views and metrics);
                           5: den_queue_raw_events / den_max_refractory_period / den_colorize_events /
                           den_undistort_events; den_render_desc.ray_grad;
                           4: density_activation in den_render_desc / den_ngp_desc; den_sh_encode_* */
@@ -130,6 +131,12 @@ typedef struct den_render_desc {
   int32_t ray_grad;        /* 1: den_render_ray_grad follows the backward (the gradient into the rays,
                               the refractory period's pose path): the BF16 layer-major backward then
                               keeps dz_g in the workspace for it (otherwise dz_g never leaves the chip) */
+  int32_t max_workgroups;  /* 0: the persistent launches (BF16 forward, head backward, layer-major hidden
+                              layers, streamed weight gradients) run one workgroup per CU; > 0: at most
+                              this many, so that two render calls on two streams can share the chip
+                              (profiles/split_probe.py: one half's forward beside the other half's
+                              backward -- slower than the two in sequence).  No reference
+                              counterpart (a launch-shape knob). */
 } den_render_desc;
 
 /* Device buffers of one render call. */
