@@ -65,6 +65,15 @@ def test_invalid_shapes_fail_with_error_text():
     desc = nat._desc(cfg, 3, 100, True, True)  # 100 samples do not tile a workgroup
     assert L.den_render_workspace_bytes(__import__("ctypes").byref(desc)) == 0
     assert len(L.den_last_error()) > 0
+    # max_workgroups (ABI 7): a launch cap only -- the workspace does not depend on it; negative refused
+    import ctypes
+    desc = nat._desc(cfg, 4096, 128, True, True)
+    ref = L.den_render_workspace_bytes(ctypes.byref(desc))
+    desc.max_workgroups = 96
+    assert ref > 0 and L.den_render_workspace_bytes(ctypes.byref(desc)) == ref
+    desc.max_workgroups = -1
+    assert L.den_render_workspace_bytes(ctypes.byref(desc)) == 0
+    assert b"max_workgroups" in L.den_last_error()
 
 
 def test_no_cpu_fallback():

@@ -282,3 +282,28 @@ def test_full_size_step_properties():
     e_lin = norm_rel(acc, g_full)
     print(f"full-size gradient vs the mean of {K} sub-batch gradients: {e_lin:.2e}")
     assert e_lin <= 2e-4
+
+
+@pytest.mark.parametrize("cap", [1, 37])
+def test_render_max_workgroups_cap(cap):
+    """den_render_desc.max_workgroups (ABI 7) changes only the persistent grids: the BF16 forward's
+    radiance is bit-identical and the gradient equal up to the weight gradients' f32 summation order,
+    with 1 (one workgroup walks everything) and 37 (an odd split of the blocks).  Bound 1e-3: one
+    workgroup sums all 8,192 blocks of a layer in one f32 accumulator chain instead of 256 partials
+    (measured 9.5e-5 for cap 1, r06j), on a gradient that cancels (a difference of log intensities)."""
+    ts, _ = _setup("bf16", 1, N=512)
+    ts.forward()
+    ts.backward()
+    torch.cuda.synchronize()
+    rgb0, g0 = ts.rgb.clone(), ts.grad.clone()
+    ts.desc.max_workgroups = cap
+    try:
+        ts.forward()
+        ts.backward()
+    finally:
+        ts.desc.max_workgroups = 0
+    torch.cuda.synchronize()
+    assert torch.equal(ts.rgb, rgb0)
+    e = float((ts.grad - g0).norm() / g0.norm())
+    print(f"[cap {cap}] gradient vs one workgroup per CU: {e:.2e}")
+    assert e <= 1e-3
