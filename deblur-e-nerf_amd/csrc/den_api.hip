@@ -123,13 +123,14 @@ WsLayout ws_layout(const den_render_desc* d) {
   size_t off = 0;
   const int es = es_of(d->mode);
   for (int a = 0; a < NACT; ++a) {
-    // layer-major BF16 backward: dz_l (l = 0..6) is written in place over S_l, which the hidden
-    // launch of layer l + 1 reads for the last time in the same pass (per 32-sample block, into
-    // LDS before the block's dz_l leaves): 6.4 KB of workspace per sample instead of 10 KB
-    // (r03: separate dz buffers measured 0.1-0.5 ms per step faster, within noise: not worth 3.6 KB
-    // per sample)
+    // layer-major BF16 backward: dz_l (l = 0..6) is written over S_{l+1}, which the hidden launch of
+    // layer l + 2 read for the last time -- never over the S_l the writing launch (layer l + 1) is
+    // reading: 6.4 KB of workspace per sample instead of 10 KB.  r06 (profiles/stream_probe): the
+    // launch's pattern (two 16 KiB reads + one 16 KiB write per block) streams at 5.50 TB/s when the
+    // write lands on the block just read (the earlier dz_l-over-S_l aliasing) and 5.81 TB/s when it
+    // goes elsewhere.  dz_7 keeps a buffer of its own (Lb reads S_7 while writing it).
     if (use_hidden_path(d) && a >= D_Z0 && a <= D_Z0 + 6) {
-      L.act[a] = L.act[A_S0 + (a - D_Z0)];
+      L.act[a] = L.act[A_S0 + (a - D_Z0) + 1];
       continue;
     }
     L.act[a] = off;

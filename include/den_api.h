@@ -121,8 +121,8 @@ typedef struct den_render_desc {
                               (ngp.py:96-106), 2 unbounded sphere (ngp.py:68-93); the
                               fixed-count sampler (points = 0) needs 0 */
   int32_t bwd_path;        /* BF16 backward: 0 layer-major hidden layers + streamed weight
-                              gradients (in place: dz_l overwrites the forward activation S_l of
-                              layers 0..6, so one train forward feeds ONE den_render_bwd);
+                              gradients (in place: dz_l overwrites the forward activation S_{l+1},
+                              l = 0..6, so one train forward feeds ONE den_render_bwd);
                               1 the F32 mode's sample-major chain + split-K GEMMs on the same bf16
                               operands (an A/B reference path).  F32 mode ignores it. */
   int32_t density_activation; /* models/nerf.py:20-29: 0 shifted_trunc_exp (exp(x - 1), gradient
