@@ -19,7 +19,6 @@ namespace {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int BLOCK = 16384;
-constexpr int DEPTH = 3, RING = DEPTH + 1;
 
 __device__ __forceinline__ void dma_block(const char* src, char* dst, int waves) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -32,9 +31,10 @@ __device__ __forceinline__ void dma_block(const char* src, char* dst, int waves)
   }
 }
 
-template <bool SEPARATE>
+template <bool SEPARATE, int DEPTH>
 __global__ __launch_bounds__(256, 1) void lds_stream_kernel(const char* a, char* b, char* c, int64_t n_blocks,
-                                                            int64_t per_wg) {
+                                                            int64_t per_wg, int64_t stride) {
+  constexpr int RING = DEPTH + 1;
   __shared__ __attribute__((aligned(16))) char lds[RING * 2 * BLOCK];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t b0 = (int64_t)blockIdx.x * per_wg;
@@ -42,8 +42,8 @@ __global__ __launch_bounds__(256, 1) void lds_stream_kernel(const char* a, char*
   char* out = SEPARATE ? c : b;
   for (int u = 0; u < DEPTH; ++u)
     if (u < n_it) {
-      dma_block(a + (b0 + u) * BLOCK, lds + u * 2 * BLOCK, 4);
-      dma_block(b + (b0 + u) * BLOCK, lds + u * 2 * BLOCK + BLOCK, 4);
+      dma_block(a + (b0 + u) * stride, lds + u * 2 * BLOCK, 4);
+      dma_block(b + (b0 + u) * stride, lds + u * 2 * BLOCK + BLOCK, 4);
     }
   __builtin_amdgcn_s_waitcnt(7 << 4);  // vmcnt(0) lgkmcnt(0)
   __syncthreads();
@@ -51,8 +51,8 @@ __global__ __launch_bounds__(256, 1) void lds_stream_kernel(const char* a, char*
     const int u = (int)(it % RING);
     if (it + DEPTH < n_it) {
       const int v = (u + DEPTH) % RING;
-      dma_block(a + (b0 + it + DEPTH) * BLOCK, lds + v * 2 * BLOCK, 4);
-      dma_block(b + (b0 + it + DEPTH) * BLOCK, lds + v * 2 * BLOCK + BLOCK, 4);
+      dma_block(a + (b0 + it + DEPTH) * stride, lds + v * 2 * BLOCK, 4);
+      dma_block(b + (b0 + it + DEPTH) * stride, lds + v * 2 * BLOCK + BLOCK, 4);
     }
     // the block's output: wave w writes its 4 KiB quarter (4 x 1 KiB), from both staged reads
     const char* s = lds + u * 2 * BLOCK;
@@ -60,12 +60,12 @@ __global__ __launch_bounds__(256, 1) void lds_stream_kernel(const char* a, char*
     for (int q = 0; q < 4; ++q) {
       const int off = (wave * 4 + q) * 1024 + lane * 16;
       const u32x4 x = *(const u32x4*)(s + off), y = *(const u32x4*)(s + BLOCK + off);
-      __builtin_nontemporal_store(x ^ y, (u32x4*)(out + (b0 + it) * BLOCK + off));
+      __builtin_nontemporal_store(x ^ y, (u32x4*)(out + (b0 + it) * stride + off));
     }
-    // wait for this wave's part of block it + 1: younger than its DMAs (issued two iterations ago) are
-    // stores(it - 2), DMA(it + 2), stores(it - 1), DMA(it + 3), stores(it) = 4 + 8 + 4 + 8 + 4 = 28
-    // vector-memory ops (hidden_bwd_kernel's YOUNGER); lgkmcnt(0) for the LDS reads
-    constexpr int VM = 28;
+    // wait for this wave's part of block it + 1: younger than its DMAs (issued DEPTH - 1 iterations
+    // ago) are its stores and the DEPTH - 1 later (DMA, stores) pairs: 4 + (DEPTH - 1) * (8 + 4)
+    // vector-memory ops (hidden_bwd_kernel's YOUNGER; 28 at DEPTH 3); lgkmcnt(0) for the LDS reads
+    constexpr int VM = 4 + (DEPTH - 1) * 12;
     if (it + DEPTH < n_it) __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | ((VM >> 4) << 14));
     else __builtin_amdgcn_s_waitcnt(7 << 4);
     asm volatile("" ::: "memory");
@@ -107,27 +107,37 @@ __global__ __launch_bounds__(512) void reg_stream_kernel(const u32x4* a, const u
 
 }  // namespace
 
+// stride: bytes from one block of a stream to the next (BLOCK: three separate tensors; larger: the
+// streams interleaved in one buffer); variants 4 / 5: the separate-output LDS kernel at DEPTH 2 / 4
 extern "C" int stream_probe_launch(int variant, int grid, int waves, const void* a, void* b, void* c,
-                                   int64_t n_blocks, void* stream) {
+                                   int64_t n_blocks, int64_t stride, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (grid <= 0 || n_blocks <= 0) return 1;
+  if (grid <= 0 || n_blocks <= 0 || stride < BLOCK) return 1;
   const int64_t per_wg = (n_blocks + grid - 1) / grid;
   switch (variant) {
     case 0:
-      hipLaunchKernelGGL(lds_stream_kernel<false>, dim3(grid), dim3(256), 0, s, (const char*)a, (char*)b, (char*)c,
-                         n_blocks, per_wg);
+      hipLaunchKernelGGL((lds_stream_kernel<false, 3>), dim3(grid), dim3(256), 0, s, (const char*)a, (char*)b,
+                         (char*)c, n_blocks, per_wg, stride);
       break;
     case 1:
-      hipLaunchKernelGGL(lds_stream_kernel<true>, dim3(grid), dim3(256), 0, s, (const char*)a, (char*)b, (char*)c,
-                         n_blocks, per_wg);
+      hipLaunchKernelGGL((lds_stream_kernel<true, 3>), dim3(grid), dim3(256), 0, s, (const char*)a, (char*)b,
+                         (char*)c, n_blocks, per_wg, stride);
+      break;
+    case 4:
+      hipLaunchKernelGGL((lds_stream_kernel<true, 2>), dim3(grid), dim3(256), 0, s, (const char*)a, (char*)b,
+                         (char*)c, n_blocks, per_wg, stride);
+      break;
+    case 5:
+      hipLaunchKernelGGL((lds_stream_kernel<true, 4>), dim3(grid), dim3(256), 0, s, (const char*)a, (char*)b,
+                         (char*)c, n_blocks, per_wg, stride);
       break;
     case 2:
-      if (waves < 1 || waves > 8) return 1;
+      if (waves < 1 || waves > 8 || stride != BLOCK) return 1;
       hipLaunchKernelGGL((reg_stream_kernel<4, true>), dim3(grid), dim3(64 * waves), 0, s, (const u32x4*)a,
                          (const u32x4*)b, (u32x4*)c, n_blocks, per_wg);
       break;
     case 3:
-      if (waves < 1 || waves > 8) return 1;
+      if (waves < 1 || waves > 8 || stride != BLOCK) return 1;
       hipLaunchKernelGGL((reg_stream_kernel<4, false>), dim3(grid), dim3(64 * waves), 0, s, (const u32x4*)a,
                          (const u32x4*)b, (u32x4*)c, n_blocks, per_wg);
       break;

@@ -11,16 +11,19 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 BLOCK = 16384
 
-CONFIGS = [  # (name, variant, grid, waves, in_place)
-    ("lds_dma_inplace_256x4 (hidden_bwd_kernel's)", 0, 256, 4, True),
-    ("lds_dma_separate_256x4", 1, 256, 4, False),
-    ("regs_nt_256x4", 2, 256, 4, False),
-    ("regs_nt_256x8", 2, 256, 8, False),
-    ("regs_nt_512x8", 2, 512, 8, False),
-    ("regs_nt_1024x8", 2, 1024, 8, False),
-    ("regs_nt_512x8_inplace", 2, 512, 8, True),
-    ("regs_cached_512x8", 3, 512, 8, False),
-    ("regs_cached_512x8_inplace", 3, 512, 8, True),
+# (name, variant, grid, waves, layout): layout "sep" three tensors (the product's since r06n), "inplace"
+# output over the second read (the product before r06n), "skew" the three tensors offset by 0 / 8 / 4 KiB
+# + n 16 KiB, "inter48" one buffer with blocks [a | b | c] back to back, "bm128" one buffer of 8-slot
+# block-major rows (a slot 5, b slot 3, c slot 4: the three activations of one layer launch)
+CONFIGS = [
+    ("lds_dma_inplace (before r06n)", 0, 256, 4, "inplace"),
+    ("lds_dma_separate (r06n)", 1, 256, 4, "sep"),
+    ("lds_dma_separate_depth2", 4, 256, 4, "sep"),
+    ("lds_dma_separate_depth4", 5, 256, 4, "sep"),
+    ("lds_dma_skew", 1, 256, 4, "skew"),
+    ("lds_dma_interleaved48", 1, 256, 4, "inter48"),
+    ("lds_dma_blockmajor128", 1, 256, 4, "bm128"),
+    ("regs_nt_256x4", 2, 256, 4, "sep"),
 ]
 
 
@@ -28,22 +31,35 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     lib = ctypes.CDLL(os.path.join(HERE, "libstream_probe.so"))
     lib.stream_probe_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
     dev = torch.device("cuda", 0)
     n_blocks = 1 << 19
-    a = torch.randint(0, 2 ** 31 - 1, (n_blocks * BLOCK // 4,), dtype=torch.int32, device=dev)
-    b = torch.randint(0, 2 ** 31 - 1, (n_blocks * BLOCK // 4,), dtype=torch.int32, device=dev)
-    c = torch.empty_like(a)
+    nb = n_blocks * BLOCK
+    # one pool for every layout: 8 slots per block (bm128 needs them all)
+    pool = torch.randint(0, 2 ** 31 - 1, (8 * nb // 4 + 3 * 8192,), dtype=torch.int32, device=dev)
+    p0 = pool.data_ptr()
+
+    def ptrs(layout):
+        if layout in ("sep", "inplace"):
+            a, b, c = p0, p0 + nb, p0 + 2 * nb
+            return a, b, (b if layout == "inplace" else c), BLOCK
+        if layout == "skew":
+            return p0, p0 + nb + 8192 + 16384, p0 + 2 * nb + 4096 + 32768, BLOCK
+        if layout == "inter48":
+            return p0, p0 + BLOCK, p0 + 2 * BLOCK, 3 * BLOCK
+        if layout == "bm128":
+            return p0 + 5 * BLOCK, p0 + 3 * BLOCK, p0 + 4 * BLOCK, 8 * BLOCK
+        raise ValueError(layout)
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     moved = 3.0 * n_blocks * BLOCK
     out = {"n_blocks": n_blocks, "bytes_per_launch": moved, "rows": []}
     for rnd in range(2):
-        for name, v, grid, waves, inplace in (CONFIGS if rnd == 0 else CONFIGS[::-1]):
-            cp = b if inplace else c
+        for name, v, grid, waves, layout in (CONFIGS if rnd == 0 else CONFIGS[::-1]):
+            a, b, c, stride = ptrs(layout)
 
             def go():
-                rc = lib.stream_probe_launch(v, grid, waves, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
-                                             ctypes.c_void_p(cp.data_ptr()), n_blocks, st)
+                rc = lib.stream_probe_launch(v, grid, waves, ctypes.c_void_p(a), ctypes.c_void_p(b), ctypes.c_void_p(c),
+                                             n_blocks, stride, st)
                 assert rc == 0, (name, rc)
             for _ in range(2):
                 go()
