@@ -97,6 +97,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct WsLayout {
   size_t act[NACT];
+  int64_t srow;  // bytes per wave block of S_0..S_7 / dz_0..dz_7 (den_geom.h SROW_SLOTS)
   size_t rec, bkgd_partial, dw_partial, lr_partial, lr_stage1, total;
   int splits;
   int64_t per_split;
@@ -122,15 +123,28 @@ WsLayout ws_layout(const den_render_desc* d) {
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
   size_t off = 0;
   const int es = es_of(d->mode);
+  const int64_t slot = (int64_t)WIDTH * tm_of(d->mode) * es;  // one 256-wide wave block: 16 KiB in both modes
+  L.srow = slot;
+  const bool rows = use_hidden_path(d) && d->train;
   for (int a = 0; a < NACT; ++a) {
-    // layer-major BF16 backward: dz_l (l = 0..6) is written over S_{l+1}, which the hidden launch of
-    // layer l + 2 read for the last time -- never over the S_l the writing launch (layer l + 1) is
-    // reading: 6.4 KB of workspace per sample instead of 10 KB.  r06 (profiles/stream_probe): the
-    // launch's pattern (two 16 KiB reads + one 16 KiB write per block) streams at 5.50 TB/s when the
-    // write lands on the block just read (the earlier dz_l-over-S_l aliasing) and 5.81 TB/s when it
-    // goes elsewhere.  dz_7 keeps a buffer of its own (Lb reads S_7 while writing it).
-    if (use_hidden_path(d) && a >= D_Z0 && a <= D_Z0 + 6) {
-      L.act[a] = L.act[A_S0 + (a - D_Z0) + 1];
+    // layer-major BF16 backward: S_0..S_7 and dz_0..dz_7 as block-major rows of SROW_SLOTS slots
+    // (den_geom.h): dz_l (l = 0..6) is written over S_{l+1}, which the hidden launch of layer l + 2
+    // read for the last time -- never over the S_l the writing launch (layer l + 1) is reading --
+    // and dz_7 takes slot 8: 6.4 KB of workspace per sample instead of 10 KB.  r06
+    // (profiles/stream_probe, profiles/r06u_ab.jsonl): the launch's pattern (two 16 KiB reads + one
+    // 16 KiB write per block) streams at 5.5 TB/s when the write lands on the block just read (the
+    // earlier dz_l-over-S_l aliasing), at 5.1-5.8 TB/s for three tensors 8 GiB apart -- varying
+    // with how each process's pages map to channels -- and at 6.2 TB/s within one 144 KiB row;
+    // the hidden launches: 4.88 / 4.73-4.98 / 4.64-4.73 ms for the three layouts.
+    if (rows && in_srows(a)) {
+      if (a == A_S0) {
+        for (int l = 0; l < 8; ++l) {
+          L.act[A_S0 + l] = off + (size_t)(l * slot);
+          L.act[D_Z0 + l] = off + (size_t)((l + 1) * slot);
+        }
+        L.srow = SROW_SLOTS * slot;
+        off += align256((size_t)(n / tm_of(d->mode)) * (size_t)L.srow);
+      }
       continue;
     }
     L.act[a] = off;
@@ -169,6 +183,13 @@ WsLayout ws_layout(const den_render_desc* d) {
   }
   L.total = off;
   return L;
+}
+
+// bytes from one wave block of activation `a` to the next
+inline int64_t block_bytes(const WsLayout& L, int mode, int a) {
+  if (in_srows(a)) return L.srow;
+  const int tm = tm_of(mode);
+  return (int64_t)(act_width(mode, a) / tm) * tm * tm * es_of(mode);
 }
 
 int check_desc(const den_render_desc* d) {
@@ -225,6 +246,7 @@ RenderArgs<MODE> make_args(const den_render_desc* d, const den_render_io* io, co
   A.out_depth = io->out_depth;
   A.density_act = d->density_activation;
   A.keep_dzg = d->ray_grad;
+  A.srow = L.srow;
   return A;
 }
 
@@ -277,13 +299,13 @@ int launch_dwstream(const den_render_desc* d, const WsLayout& L, char* ws, int a
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
   DwStreamArgs P{};
   P.a[0] = ws + L.act[a0];
-  P.a_tiles[0] = act_width(DEN_MODE_BF16, a0) / 32;
+  P.a_bs[0] = block_bytes(L, DEN_MODE_BF16, a0);
   P.a[1] = a1 >= 0 ? ws + L.act[a1] : nullptr;
-  P.a_tiles[1] = a1 >= 0 ? act_width(DEN_MODE_BF16, a1) / 32 : 0;
+  P.a_bs[1] = a1 >= 0 ? block_bytes(L, DEN_MODE_BF16, a1) : 0;
   P.b[0] = b0 >= 0 ? ws + L.act[b0] : nullptr;
-  P.b_tiles[0] = b0 >= 0 ? act_width(DEN_MODE_BF16, b0) / 32 : 0;
+  P.b_bs[0] = b0 >= 0 ? block_bytes(L, DEN_MODE_BF16, b0) : 0;
   P.b[1] = b1 >= 0 ? ws + L.act[b1] : nullptr;
-  P.b_tiles[1] = b1 >= 0 ? act_width(DEN_MODE_BF16, b1) / 32 : 0;
+  P.b_bs[1] = b1 >= 0 ? block_bytes(L, DEN_MODE_BF16, b1) : 0;
   P.partial = (float*)(ws + L.dw_partial);
   static_assert(U == 1 || U == 2 || U == 4 || U == 8, "U divides the wave blocks (n is a multiple of 256)");
   P.n_blocks = n / 32 / U;
@@ -368,6 +390,9 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   H.dz_out = ws + L.act[D_Z0 + l - 1];
   H.partial = (float*)(ws + L.dw_partial);
   H.n_blocks = n / 32;
+  H.bs_dz_in = lb ? (int64_t)HB_BLOCK : L.srow;  // Lb: dz_b's 8-tile blocks back to back (D_ZB8)
+  H.bs_s = L.srow;
+  H.bs_dz_out = L.srow;
   const int64_t grid = hidden_grid(d);
   H.per_wg = (H.n_blocks + grid - 1) / grid;
   {
@@ -706,6 +731,7 @@ int den_render_ray_grad(const den_render_desc* d, const den_render_io* io, const
   G.t1 = io->t_ends;
   G.per_sample = (float*)rg_workspace;
   RayGradMlp M{params, ws + L.act[D_Z0 + 0], ws + L.act[D_Z0 + 5], ws + L.act[D_ZG],
+               block_bytes(L, d->mode, D_Z0 + 0), block_bytes(L, d->mode, D_Z0 + 5), block_bytes(L, d->mode, D_ZG),
                d->mode == DEN_MODE_F32 ? 1.0f : (float)KAPPA};
   hipStream_t st = (hipStream_t)stream;
   const unsigned grid = (unsigned)((n + RG_THREADS - 1) / RG_THREADS);

@@ -32,9 +32,9 @@ constexpr int DWS_NW1 = 16;
 
 struct DwStreamArgs {
   const char* a[2];     // dz tensors (wave-block major), row tiles [0, MA) from a[0], [MA, MT) from a[1]
-  int a_tiles[2];       // tiles per wave block of each dz tensor
+  int64_t a_bs[2];      // bytes from one wave block of each dz tensor to the next
   const char* b[2];     // x tensors, column tiles [0, NB) from b[0], [NB, NT) from b[1]
-  int b_tiles[2];
+  int64_t b_bs[2];
   float* partial;       // [gridDim.x][MT][NT + 1][64][16]
   int64_t n_blocks;
   int64_t per_wg;
@@ -98,10 +98,10 @@ __global__ __launch_bounds__(64 * NW, 1) void dwstream_kernel(DwStreamArgs P) {
         const int t = tp >> 1, f = tp & 1;
         const int64_t wb = blk * U + ub;
         const char* src;
-        if (t < MA) src = P.a[0] + (wb * P.a_tiles[0] + t) * HB_TILE;
-        else if (t < MT) src = P.a[1] + (wb * P.a_tiles[1] + (t - MA)) * HB_TILE;
-        else if (t < MT + NB) src = P.b[0] + (wb * P.b_tiles[0] + (t - MT)) * HB_TILE;
-        else src = P.b[1] + (wb * P.b_tiles[1] + (t - MT - NB)) * HB_TILE;
+        if (t < MA) src = P.a[0] + wb * P.a_bs[0] + t * HB_TILE;
+        else if (t < MT) src = P.a[1] + wb * P.a_bs[1] + (t - MA) * HB_TILE;
+        else if (t < MT + NB) src = P.b[0] + wb * P.b_bs[0] + (t - MT) * HB_TILE;
+        else src = P.b[1] + wb * P.b_bs[1] + (t - MT - NB) * HB_TILE;
         dws_dma_piece(src, dst + pc * 1024, f);
       }
     }

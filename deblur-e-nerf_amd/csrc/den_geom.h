@@ -197,6 +197,14 @@ enum ActId { A_PE = 0, A_S0 = 1, /* S0..S7 = 1..8 */ A_BT = 9, A_VE = 10, A_G = 
 // skipped a 2 KiB sigma tile per block and read 64 B of it.
 constexpr int D_ZB8 = NACT;
 DEN_HD constexpr int64_t sigma_dz_offset(int64_t n_blocks, int64_t wb) { return n_blocks * 16384 + wb * 64; }
+// The layer-major BF16 path keeps S_0..S_7 and dz_0..dz_7 as block-major rows (r06): per wave block one
+// row of SROW_SLOTS 16 KiB slots -- S_l in slot l, dz_l (written over S_{l+1}, l <= 6) in slot l + 1,
+// dz_7 in slot 8 -- so a hidden launch's two reads and its write fall within one 144 KiB row
+// (profiles/stream_probe: 6.23 TB/s for that pattern, 5.1-5.8 TB/s for three tensors 8 GiB apart).
+// Elsewhere these tensors are contiguous (block stride 16 KiB: 256 features x TM samples x ES bytes in
+// both modes).  act_ptr / the hidden, streamed-dW and ray-gradient kernels take the row's block stride.
+constexpr int SROW_SLOTS = 9;
+DEN_HD constexpr bool in_srows(int a) { return (a >= A_S0 && a <= A_S0 + 7) || (a >= D_Z0 && a <= D_Z0 + 7); }
 DEN_HD constexpr int act_width(int mode, int a) {
   return a == A_PE ? PE_PAD : a <= 8 ? WIDTH : a == A_BT ? WIDTH : a == A_VE ? VE_PAD : a == A_G ? WIDTH_COND
        : a <= 19 ? WIDTH : a == D_ZB ? DZB_W : a == D_ZG ? WIDTH_COND : DZR_W;

@@ -73,6 +73,7 @@ struct HiddenArgs {
   float* partial;     // [gridDim.x][8][9][64][16]
   int64_t n_blocks;   // 32-sample wave blocks
   int64_t per_wg;     // blocks per workgroup
+  int64_t bs_dz_in, bs_s, bs_dz_out;  // bytes from one wave block to the next (den_geom.h SROW_SLOTS rows)
 };
 
 // 16-byte LDS slot that holds tile lane `lane`'s fragment f inside a 1 KiB piece:
@@ -250,7 +251,7 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     // dz_{l-1} tile: stored now, the weight-gradient MFMAs below cover its write latency
     bf16x8 of[2];
     acc_to_frags<1>(acc, of);
-    char* d = P.dz_out + (b * 8 + 2 * wave + t) * HB_TILE + lane * 16;  // dz_{l-1}: 8 tiles per block
+    char* d = P.dz_out + b * P.bs_dz_out + (2 * wave + t) * HB_TILE + lane * 16;  // dz_{l-1}: 8 tiles per block
     __builtin_nontemporal_store(of[0], (bf16x8*)d);
     __builtin_nontemporal_store(of[1], (bf16x8*)(d + 1024));
     // keep the scheduler from hoisting the next phase's LDS reads here (register pressure: W^T lives
@@ -290,7 +291,6 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   // HB_RING LDS slots of [dz_l block | S'_{l-1} block]; HB_DEPTH blocks in flight ahead of the one
   // being computed.  Each wave waits for its own part of block b+1 at the end of block b (vmcnt; the
   // younger prefetches and stores stay in flight), then the workgroup barrier publishes every part.
-  constexpr int DZ_TILES = 8;                    // dz_in tiles per wave block in HBM (LB: D_ZB8, den_geom.h)
   constexpr int DZ_STAGED = LB ? HB_BLOCK + HB_SIG : HB_BLOCK;  // bytes of them staged
   constexpr int SLOT = DZ_STAGED + HB_BLOCK;
   constexpr int KST = LB ? 17 : 16;              // chain k-steps
@@ -311,9 +311,9 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   const int64_t n_it = b0 < P.n_blocks ? (b0 + P.per_wg < P.n_blocks ? P.per_wg : P.n_blocks - b0) : 0;
   auto blk = [&](int64_t it) { return b0 + it; };
   auto fetch = [&](int64_t b, char* dst) {
-    hb_dma_untracked(P.dz_in + b * DZ_TILES * HB_TILE, dst);
+    hb_dma_untracked(P.dz_in + b * P.bs_dz_in, dst);
     if constexpr (LB) hb_dma_sigma(P.dz_in + sigma_dz_offset(P.n_blocks, b), dst + HB_BLOCK);
-    hb_dma_untracked(P.s_in + b * HB_BLOCK, dst + DZ_STAGED);
+    hb_dma_untracked(P.s_in + b * P.bs_s, dst + DZ_STAGED);
   };
 #pragma unroll
   for (int u = 0; u < HB_DEPTH; ++u)

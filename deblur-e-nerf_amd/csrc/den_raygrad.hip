@@ -87,9 +87,9 @@ __device__ __forceinline__ void enc_backward(const float* v, const float* g, flo
 // 4 consecutive features f .. f+3 (f % 4 == 0) of sample s from an activation / dz tensor of
 // `width` features in the wave-block-major layout (den_geom.h, den_render.hip act_ptr)
 template <int MODE>
-__device__ __forceinline__ void act_load4(const char* act, int width, int64_t s, int f, float* out) {
+__device__ __forceinline__ void act_load4(const char* act, int64_t block_bytes, int64_t s, int f, float* out) {
   constexpr int TM = tm_of(MODE), ES = es_of(MODE);
-  const char* tile = act + ((s / TM) * (width / TM) + f / TM) * (int64_t)(TM * TM * ES);
+  const char* tile = act + (s / TM) * block_bytes + (f / TM) * (int64_t)(TM * TM * ES);
   const int c = (int)(s % TM), row = f % TM;
   if constexpr (MODE == 0) {
     // lane c + 16 (row / 4), registers row % 4
@@ -181,6 +181,7 @@ struct RayGradMlp {
   const char* dz0;      // workspace tensors of the render (mode layout): dz of L0, L5 (256 wide), Lg (128)
   const char* dz5;
   const char* dzg;
+  int64_t bs0, bs5, bsg;  // bytes per wave block of each (den_geom.h SROW_SLOTS rows for dz0 / dz5)
   float scale;          // the mode's input-column scale (den_geom.h col_scale: 1 in F32, KAPPA in BF16)
 };
 
@@ -214,8 +215,8 @@ __global__ __launch_bounds__(RG_THREADS) void raygrad_mlp_kernel(RayGradArgs G, 
 #pragma unroll 1
     for (int oo = 0; oo < RG_OB; oo += 4) {
       float a[4], b[4];
-      act_load4<MODE>(M.dz0, WIDTH, sc, o0 + oo, a);
-      act_load4<MODE>(M.dz5, WIDTH, sc, o0 + oo, b);
+      act_load4<MODE>(M.dz0, M.bs0, sc, o0 + oo, a);
+      act_load4<MODE>(M.dz5, M.bs5, sc, o0 + oo, b);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(RG_THREADS) void raygrad_mlp_kernel(RayGradArgs G, 
 #pragma unroll 1
     for (int oo = 0; oo < RG_OB; oo += 4) {
       float a[4];
-      act_load4<MODE>(M.dzg, WIDTH_COND, sc, o0 + oo, a);
+      act_load4<MODE>(M.dzg, M.bsg, sc, o0 + oo, a);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll

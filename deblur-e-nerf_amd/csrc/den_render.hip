@@ -54,6 +54,7 @@ struct RenderArgs {
   int64_t n_items;        // forward: 256-sample (BF16) / 128-sample (F32) blocks, walked by a persistent grid
   int density_act;        // den_render_desc.density_activation
   int keep_dzg;           // den_render_desc.ray_grad: the BF16 head backward also stores dz_g (D_ZG)
+  int64_t srow;           // bytes per wave block of S_0..S_7 / dz_0..dz_7 (den_geom.h in_srows)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -65,6 +66,7 @@ __device__ __forceinline__ char* act_ptr(const AT& A, int a, int64_t sample, int
   constexpr int TM = Tr<MODE>::TM, ES = es_of(MODE);
   const int64_t wb = __builtin_amdgcn_readfirstlane((int)(sample / TM));  // uniform across the wave
   if (a == D_ZB8) return A.act[D_ZB] + (wb * (WIDTH / TM) + tile) * (int64_t)(TM * TM * ES);  // (den_geom.h)
+  if (in_srows(a)) return A.act[a] + wb * A.srow + tile * (int64_t)(TM * TM * ES);
   return A.act[a] + (wb * (act_width(MODE, a) / TM) + tile) * (int64_t)(TM * TM * ES);
 }
 
