@@ -217,6 +217,10 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
 #pragma unroll
     for (int f = 0; f < 2; ++f) sf[t][f] = hb_frag(sb + (2 * wave + t) * HB_TILE, f);
   __builtin_amdgcn_sched_barrier(0);  // (left alone, the compiler sinks these reads back to their use)
+  // L7..L1: the epilogue's 32 activation-derivative factors 1 - 2^-S', computed in the chain MFMAs'
+  // shadow (r06, profiles/r06v_ab.jsonl: 4.639 -> 4.607 ms per launch in ABBA order; Lb's 17th k-step
+  // leaves no registers for them)
+  float dv[2][16];
   {
     bf16x8 bq[HB_PF];
 #pragma unroll
@@ -227,6 +231,13 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
       if (k + HB_PF < 16) bq[k % HB_PF] = hb_frag(dzb + ((k + HB_PF) >> 1) * HB_TILE, (k + HB_PF) & 1);
       accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[0][k], cur, accs[0], 0, 0, 0);
       accs[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[1][k], cur, accs[1], 0, 0, 0);
+      if constexpr (!LB) {  // two of the derivative factors per k-step
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int t = k >> 3, r = 2 * (k & 7) + e;
+          dv[t][r] = dsoftplus2_scaled_from_out((float)sf[t][r >> 3][r & 7]);
+        }
+      }
     }
   }
   if constexpr (LB) {
@@ -245,8 +256,12 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     const bf16x8 s0 = sf[t][0], s1 = sf[t][1];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float sv = (float)(r < 8 ? s0[r] : s1[r - 8]);
-      acc[r] = acc[r] * dsoftplus2_scaled_from_out(sv);
+      if constexpr (!LB) {
+        acc[r] = acc[r] * dv[t][r];
+      } else {
+        const float sv = (float)(r < 8 ? s0[r] : s1[r - 8]);
+        acc[r] = acc[r] * dsoftplus2_scaled_from_out(sv);
+      }
     }
     // dz_{l-1} tile: stored now, the weight-gradient MFMAs below cover its write latency
     bf16x8 of[2];
