@@ -10,7 +10,7 @@
 //           (k = samples: both operands by ds_read_b64_tr_b16 from the same LDS blocks; the bias from
 //           VALU sums of the dz operand), accumulated in registers over the whole range, written once as a
 //           split-K partial for dw_reduce_kernel (den_dw.hip layout, MT = NT = 8).
-// dz_l and S'_{l-1} (16 KiB per block each) arrive by LDS-DMA HB_DEPTH = 3 blocks ahead (96 KiB in flight per CU).  Per sample and layer
+// dz_l and S'_{l-1} (16 KiB per block each) arrive by LDS-DMA 3 blocks ahead (96 KiB in flight per CU).  Per sample and layer
 // this moves 1.5 KiB of HBM (read dz_l and S'_{l-1}, write dz_{l-1}) where the sample-major chain
 // plus the split-K GEMM (den_render.hip + den_dw.hip; kept for the F32 parity mode) move 3 KiB.
 //
@@ -32,8 +32,12 @@ constexpr int HB_SIG = 256;            // LB: LDS bytes for sigma's bf16[32] dz 
 // (overlapping them, in compiler order or a pinned interleave, was 1-2 ms per step slower).
 constexpr int HB_GRID_MAX = 256;  // persistent workgroups (one per CU)
 constexpr int HB_PF = 4;          // dz_l fragments read ahead of the chain MFMAs
-constexpr int HB_DEPTH = 3;       // blocks in flight ahead of the computed one
-constexpr int HB_RING = HB_DEPTH + 1;                    // LDS slots (32 KiB each, 33 for Lb; <= 4 fit in 160 KiB)
+#ifndef DEN_HB_DEPTH_L
+#define DEN_HB_DEPTH_L 3
+#endif
+constexpr int HB_DEPTH_LB = 3;    // blocks in flight ahead of the computed one (Lb: 33 KiB slots, <= 4 fit)
+constexpr int HB_DEPTH_L = DEN_HB_DEPTH_L;  // L7..L1 (32 KiB slots: up to 4 ahead in 160 KiB; 4 measured
+                                            // no faster with the block-major rows, profiles/r06y_ab.jsonl)
 constexpr int HB_STORE_OPS = 4;                          // dz_{l-1} stores per wave per block
 
 typedef short hb_v4i16 __attribute__((ext_vector_type(4)));
@@ -315,6 +319,8 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   // vector-memory ops a wave issues after its DMA of block b+1 by the end of block b (issue order:
   // stores(b-2), DMA(b+2), stores(b-1), DMA(b+3), stores(b)); the asm DMAs clobber "memory", so the
   // stores keep their program order around them
+  constexpr int HB_DEPTH = LB ? HB_DEPTH_LB : HB_DEPTH_L;
+  constexpr int HB_RING = HB_DEPTH + 1;
   constexpr int YOUNGER = HB_STORE_OPS + (HB_DEPTH - 1) * (DMA_OPS + HB_STORE_OPS);
   static_assert(HB_RING * SLOT <= 160 * 1024, "hidden ring exceeds the LDS");
   __shared__ __attribute__((aligned(16))) char lds[HB_RING * SLOT];
