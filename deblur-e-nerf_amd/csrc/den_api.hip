@@ -97,7 +97,8 @@ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct WsLayout {
   size_t act[NACT];
-  int64_t srow;  // bytes per wave block of S_0..S_7 / dz_0..dz_7 (den_geom.h SROW_SLOTS)
+  int64_t bstride[NACT + 1];  // bytes from one wave block of each activation (and D_ZB8) to the next
+  size_t sigma_dz;            // layer-major BF16: sigma's dz, one bf16 per sample (den_geom.h D_ZB8)
   size_t rec, bkgd_partial, dw_partial, lr_partial, lr_stage1, total;
   int splits;
   int64_t per_split;
@@ -122,31 +123,33 @@ WsLayout ws_layout(const den_render_desc* d) {
   WsLayout L{};
   const int64_t n = (int64_t)d->n_rays * d->n_samples;
   size_t off = 0;
-  const int es = es_of(d->mode);
-  const int64_t slot = (int64_t)WIDTH * tm_of(d->mode) * es;  // one 256-wide wave block: 16 KiB in both modes
-  L.srow = slot;
+  const int tm = tm_of(d->mode), es = es_of(d->mode);
+  const int64_t n_blocks = n / tm;
+  for (int a = 0; a <= NACT; ++a)
+    L.bstride[a] = (int64_t)((a == D_ZB8 ? WIDTH : act_width(d->mode, a)) / tm) * tm * tm * es;
+  // layer-major BF16 training: the activations the hidden launches stream as block-major rows
+  // (den_geom.h SROW_BYTES): S_0..S_7, dz_l over S_{l+1} (l = 0..6) -- read for the last time by the
+  // launch before the one writing it, never by that one -- dz_7 and dz_b's 8 tiles, one row per wave
+  // block: 6.4 KB of workspace per sample for S / dz instead of 10 KB.  r06
+  // (profiles/stream_probe, profiles/r06u_ab.jsonl): a hidden launch's pattern (two 16 KiB reads +
+  // one 16 KiB write per block) streams at 5.5 TB/s when the write lands on the block just read (the
+  // earlier dz_l-over-S_l aliasing), at 5.1-5.8 TB/s for three tensors 8 GiB apart -- varying with
+  // how each process's pages map to channels -- and at 6.2 TB/s within one row; the hidden launches
+  // ran 4.88 / 4.73-4.98 / 4.64-4.73 ms for the three layouts.
   const bool rows = use_hidden_path(d) && d->train;
-  for (int a = 0; a < NACT; ++a) {
-    // layer-major BF16 backward: S_0..S_7 and dz_0..dz_7 as block-major rows of SROW_SLOTS slots
-    // (den_geom.h): dz_l (l = 0..6) is written over S_{l+1}, which the hidden launch of layer l + 2
-    // read for the last time -- never over the S_l the writing launch (layer l + 1) is reading --
-    // and dz_7 takes slot 8: 6.4 KB of workspace per sample instead of 10 KB.  r06
-    // (profiles/stream_probe, profiles/r06u_ab.jsonl): the launch's pattern (two 16 KiB reads + one
-    // 16 KiB write per block) streams at 5.5 TB/s when the write lands on the block just read (the
-    // earlier dz_l-over-S_l aliasing), at 5.1-5.8 TB/s for three tensors 8 GiB apart -- varying
-    // with how each process's pages map to channels -- and at 6.2 TB/s within one 144 KiB row;
-    // the hidden launches: 4.88 / 4.73-4.98 / 4.64-4.73 ms for the three layouts.
-    if (rows && in_srows(a)) {
-      if (a == A_S0) {
-        for (int l = 0; l < 8; ++l) {
-          L.act[A_S0 + l] = off + (size_t)(l * slot);
-          L.act[D_Z0 + l] = off + (size_t)((l + 1) * slot);
-        }
-        L.srow = SROW_SLOTS * slot;
-        off += align256((size_t)(n / tm_of(d->mode)) * (size_t)L.srow);
-      }
-      continue;
+  if (rows) {
+    for (int a = 0; a <= NACT; ++a) {
+      const int64_t o = srow_offset(a);
+      if (o < 0) continue;
+      L.act[a == D_ZB8 ? D_ZB : a] = off + (size_t)o;  // D_ZB's base is the dz_b slot (the 288-wide D_ZB unused)
+      L.bstride[a] = SROW_BYTES;
     }
+    off += align256((size_t)n_blocks * (size_t)SROW_BYTES);
+    L.sigma_dz = off;
+    off += align256((size_t)n * 2);
+  }
+  for (int a = 0; a < NACT; ++a) {
+    if (rows && (srow_offset(a) >= 0 || a == D_ZB)) continue;
     L.act[a] = off;
     // pe: kept by the forward (read once by the streamed L0 / L5-pe weight gradient); ve: kept by the
     // F32 forward only (the BF16 head backward recomputes its tile in LDS; the sample-major BF16 path
@@ -186,11 +189,7 @@ WsLayout ws_layout(const den_render_desc* d) {
 }
 
 // bytes from one wave block of activation `a` to the next
-inline int64_t block_bytes(const WsLayout& L, int mode, int a) {
-  if (in_srows(a)) return L.srow;
-  const int tm = tm_of(mode);
-  return (int64_t)(act_width(mode, a) / tm) * tm * tm * es_of(mode);
-}
+inline int64_t block_bytes(const WsLayout& L, int mode, int a) { return L.bstride[a]; }
 
 int check_desc(const den_render_desc* d) {
   if (!d) return fail(DEN_EINVAL, "null desc");
@@ -246,7 +245,8 @@ RenderArgs<MODE> make_args(const den_render_desc* d, const den_render_io* io, co
   A.out_depth = io->out_depth;
   A.density_act = d->density_activation;
   A.keep_dzg = d->ray_grad;
-  A.srow = L.srow;
+  for (int a = 0; a <= NACT; ++a) A.bstride[a] = L.bstride[a];
+  A.sigma_dz = ws ? ws + L.sigma_dz : nullptr;
   return A;
 }
 
@@ -390,9 +390,10 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   H.dz_out = ws + L.act[D_Z0 + l - 1];
   H.partial = (float*)(ws + L.dw_partial);
   H.n_blocks = n / 32;
-  H.bs_dz_in = lb ? (int64_t)HB_BLOCK : L.srow;  // Lb: dz_b's 8-tile blocks back to back (D_ZB8)
-  H.bs_s = L.srow;
-  H.bs_dz_out = L.srow;
+  H.bs_dz_in = L.bstride[lb ? D_ZB8 : D_Z0 + l];
+  H.bs_s = L.bstride[A_S0 + l - 1];
+  H.bs_dz_out = L.bstride[D_Z0 + l - 1];
+  H.sigma_dz = ws + L.sigma_dz;
   const int64_t grid = hidden_grid(d);
   H.per_wg = (H.n_blocks + grid - 1) / grid;
   {

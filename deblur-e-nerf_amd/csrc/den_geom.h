@@ -190,21 +190,25 @@ DEN_HD double bias_scale(int mode, int l) {
 constexpr int DZB_W = 288, DZR_W = 32;
 enum ActId { A_PE = 0, A_S0 = 1, /* S0..S7 = 1..8 */ A_BT = 9, A_VE = 10, A_G = 11,
              D_Z0 = 12, /* DZ0..DZ7 = 12..19 */ D_ZB = 20, D_ZG = 21, D_ZR = 22, NACT = 23 };
-// The layer-major BF16 path (render_head_bwd_kernel -> hidden_bwd_kernel<true>) keeps dz_b in D_ZB's
-// allocation as 8 tiles per wave block (the bottleneck's 256; act_ptr's pseudo id D_ZB8), followed by
-// sigma's dz as one bf16 per sample (sigma_dz_offset): the Lb launch then streams dz_b exactly as the
-// other hidden launches stream dz (16 KiB blocks back to back) -- with the 288-wide layout its dz read
-// skipped a 2 KiB sigma tile per block and read 64 B of it.
+// The layer-major BF16 path (render_head_bwd_kernel -> hidden_bwd_kernel<true>) keeps dz_b as 8 tiles
+// per wave block (the bottleneck's 256; act_ptr's pseudo id D_ZB8) and sigma's dz as one bf16 per sample
+// in an array of its own: the Lb launch then streams dz_b exactly as the other hidden launches stream
+// dz -- with the 288-wide layout its dz read skipped a 2 KiB sigma tile per block and read 64 B of it.
 constexpr int D_ZB8 = NACT;
-DEN_HD constexpr int64_t sigma_dz_offset(int64_t n_blocks, int64_t wb) { return n_blocks * 16384 + wb * 64; }
-// The layer-major BF16 path keeps S_0..S_7 and dz_0..dz_7 as block-major rows (r06): per wave block one
-// row of SROW_SLOTS 16 KiB slots -- S_l in slot l, dz_l (written over S_{l+1}, l <= 6) in slot l + 1,
-// dz_7 in slot 8 -- so a hidden launch's two reads and its write fall within one 144 KiB row
-// (profiles/stream_probe: 6.23 TB/s for that pattern, 5.1-5.8 TB/s for three tensors 8 GiB apart).
-// Elsewhere these tensors are contiguous (block stride 16 KiB: 256 features x TM samples x ES bytes in
-// both modes).  act_ptr / the hidden, streamed-dW and ray-gradient kernels take the row's block stride.
-constexpr int SROW_SLOTS = 9;
-DEN_HD constexpr bool in_srows(int a) { return (a >= A_S0 && a <= A_S0 + 7) || (a >= D_Z0 && a <= D_Z0 + 7); }
+// Block-major rows (r06; ws_layout in den_api.hip): in the layer-major BF16 training layout the
+// activations the hidden launches stream live in one row per wave block -- S_l in 16 KiB slot l
+// (l = 0..7), dz_l over S_{l+1} (l = 0..6; dz_7 in slot 8) and dz_b's 8 tiles (D_ZB8) in slot 9 -- so
+// each of those launches reads and writes within one SROW_BYTES row (profiles/stream_probe: 6.23 TB/s
+// for a hidden launch's pattern there, 5.1-5.8 TB/s for three tensors 8 GiB apart).  The bottleneck
+// and G, which only the head backward reads, stay contiguous (in the rows too: the same step time, the
+// head 0.17 ms slower and the hidden launches 0.025 ms faster, profiles/r06ac_ab.jsonl).  Every other
+// layout keeps contiguous tensors; kernels address a wave block through the per-activation block
+// stride of their arguments.
+constexpr int64_t SROW_BYTES = 10 * 16384;
+DEN_HD constexpr int64_t srow_offset(int a) {
+  return (a >= A_S0 && a <= A_S0 + 7) ? (int64_t)(a - A_S0) * 16384
+       : (a >= D_Z0 && a <= D_Z0 + 7) ? (int64_t)(a - D_Z0 + 1) * 16384 : a == D_ZB8 ? 9 * 16384 : -1;
+}
 DEN_HD constexpr int act_width(int mode, int a) {
   return a == A_PE ? PE_PAD : a <= 8 ? WIDTH : a == A_BT ? WIDTH : a == A_VE ? VE_PAD : a == A_G ? WIDTH_COND
        : a <= 19 ? WIDTH : a == D_ZB ? DZB_W : a == D_ZG ? WIDTH_COND : DZR_W;

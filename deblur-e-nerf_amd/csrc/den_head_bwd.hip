@@ -392,7 +392,7 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     // Wave w = bottleneck column tile w (x 4 row tiles), and for w < 4 the (row tile w, ve) tile +
     // row tile w's bias.
     const int64_t wb0 = item * (WGS / TM);  // the item's first wave block
-    auto bt_src = [&](int b) { return A.act[A_BT] + ((wb0 + b) * (WIDTH / TM) + wave) * (int64_t)HB_TILE; };
+    auto bt_src = [&](int b) { return A.act[A_BT] + (wb0 + b) * A.bstride[A_BT] + wave * (int64_t)HB_TILE; };
     hd_dma_tile(bt_src(0), xbuf);
     hd_dma_tile(bt_src(1), xbuf + HB_TILE);
     auto dw_block = [&](int b) {
@@ -430,10 +430,10 @@ __global__ __launch_bounds__(512, 1) void render_head_bwd_kernel(RenderArgs<1> A
     bwd_layer_run<MODE, 1, 1, WIDTH_COND / T::KI, 1, true, true, true>(A, lds, sample, xa, xb, 0, D_ZB8, NoTileHook{},
                                                                        lg_step, gc + 1);
     gc += 1 + bwd_tiles(MODE, 1);
-    // sigma's dz: one bf16 per sample after dz_b's 8-tile blocks (sigma_dz_offset, den_geom.h)
+    // sigma's dz: one bf16 per sample in its own array (A.sigma_dz, den_geom.h D_ZB8)
     if (grp == 0) {
       const int64_t wb = __builtin_amdgcn_readfirstlane((int)(sample / TM));
-      *(__bf16*)(A.act[D_ZB] + sigma_dz_offset((int64_t)A.n_rays * A.n_samples / TM, wb) + c * 2) = (__bf16)g4[0];
+      *(__bf16*)(A.sigma_dz + wb * 64 + c * 2) = (__bf16)g4[0];
     }
     HD_T(4);
     // block 7 (its tile was issued in step 5; step 7's wait covered it)

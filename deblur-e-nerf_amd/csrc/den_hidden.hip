@@ -77,7 +77,8 @@ struct HiddenArgs {
   float* partial;     // [gridDim.x][8][9][64][16]
   int64_t n_blocks;   // 32-sample wave blocks
   int64_t per_wg;     // blocks per workgroup
-  int64_t bs_dz_in, bs_s, bs_dz_out;  // bytes from one wave block to the next (den_geom.h SROW_SLOTS rows)
+  int64_t bs_dz_in, bs_s, bs_dz_out;  // bytes from one wave block to the next (den_geom.h SROW_BYTES rows)
+  const char* sigma_dz;               // LB: sigma's dz, one bf16 per sample
 };
 
 // 16-byte LDS slot that holds tile lane `lane`'s fragment f inside a 1 KiB piece:
@@ -121,7 +122,7 @@ __device__ __forceinline__ void hb_dma_untracked(const char* src, char* dst) {
   }
 }
 
-// LB: sigma's 32 bf16 dz of a wave block (64 B, sigma_dz_offset) into LDS, by lanes 0..3;
+// LB: sigma's 32 bf16 dz of a wave block (64 B of HiddenArgs.sigma_dz) into LDS, by lanes 0..3;
 // every wave issues it (the same bytes), so each wave's DMA count per block stays uniform
 __device__ __forceinline__ void hb_dma_sigma(const char* src, char* dst) {
   const int lane = threadIdx.x & 63;
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   auto blk = [&](int64_t it) { return b0 + it; };
   auto fetch = [&](int64_t b, char* dst) {
     hb_dma_untracked(P.dz_in + b * P.bs_dz_in, dst);
-    if constexpr (LB) hb_dma_sigma(P.dz_in + sigma_dz_offset(P.n_blocks, b), dst + HB_BLOCK);
+    if constexpr (LB) hb_dma_sigma(P.sigma_dz + b * 64, dst + HB_BLOCK);
     hb_dma_untracked(P.s_in + b * P.bs_s, dst + DZ_STAGED);
   };
 #pragma unroll

@@ -181,7 +181,7 @@ struct RayGradMlp {
   const char* dz0;      // workspace tensors of the render (mode layout): dz of L0, L5 (256 wide), Lg (128)
   const char* dz5;
   const char* dzg;
-  int64_t bs0, bs5, bsg;  // bytes per wave block of each (den_geom.h SROW_SLOTS rows for dz0 / dz5)
+  int64_t bs0, bs5, bsg;  // bytes per wave block of each (den_geom.h SROW_BYTES rows in the BF16 layout)
   float scale;          // the mode's input-column scale (den_geom.h col_scale: 1 in F32, KAPPA in BF16)
 };
 

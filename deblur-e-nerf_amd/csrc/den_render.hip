@@ -54,7 +54,8 @@ struct RenderArgs {
   int64_t n_items;        // forward: 256-sample (BF16) / 128-sample (F32) blocks, walked by a persistent grid
   int density_act;        // den_render_desc.density_activation
   int keep_dzg;           // den_render_desc.ray_grad: the BF16 head backward also stores dz_g (D_ZG)
-  int64_t srow;           // bytes per wave block of S_0..S_7 / dz_0..dz_7 (den_geom.h in_srows)
+  int64_t bstride[NACT + 1];  // bytes from one wave block of each activation (and D_ZB8) to the next
+  char* sigma_dz;         // layer-major BF16: sigma's dz, one bf16 per sample (den_geom.h D_ZB8)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -65,9 +66,7 @@ template <int MODE, typename AT>
 __device__ __forceinline__ char* act_ptr(const AT& A, int a, int64_t sample, int tile) {
   constexpr int TM = Tr<MODE>::TM, ES = es_of(MODE);
   const int64_t wb = __builtin_amdgcn_readfirstlane((int)(sample / TM));  // uniform across the wave
-  if (a == D_ZB8) return A.act[D_ZB] + (wb * (WIDTH / TM) + tile) * (int64_t)(TM * TM * ES);  // (den_geom.h)
-  if (in_srows(a)) return A.act[a] + wb * A.srow + tile * (int64_t)(TM * TM * ES);
-  return A.act[a] + (wb * (act_width(MODE, a) / TM) + tile) * (int64_t)(TM * TM * ES);
+  return A.act[a == D_ZB8 ? D_ZB : a] + wb * A.bstride[a] + tile * (int64_t)(TM * TM * ES);
 }
 
 // The backward ring's LDS-DMA through inline asm (untracked: the compiler then does not make the
@@ -1195,10 +1194,10 @@ __global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderArgs<MODE> A) 
   // sigma head row(s) of Lb as extra fake tile(s) appended to the DZB fragments
   if constexpr (MODE == 1 && LAST_J == 1) {
     // Lb runs layer-major (hidden_bwd_kernel<true>): dz_b as 8-tile blocks, then sigma's dz as one
-    // bf16 per sample (D_ZB8 / sigma_dz_offset, den_geom.h)
+    // bf16 per sample (D_ZB8 / sigma_dz, den_geom.h)
     if (grp == 0) {
       const int64_t wb = __builtin_amdgcn_readfirstlane((int)(sample / TM));
-      *(__bf16*)(A.act[D_ZB] + sigma_dz_offset((int64_t)A.n_rays * A.n_samples / TM, wb) + c * 2) = (__bf16)dzs[0];
+      *(__bf16*)(A.sigma_dz + wb * 64 + c * 2) = (__bf16)dzs[0];
     }
   } else {
     constexpr int EXTRA_T = (DZB_W - WIDTH) / TM;  // sigma tile + zero padding
