@@ -25,6 +25,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
+#ifndef SHAPE16_PF
+#define SHAPE16_PF 0
+#endif
+
 namespace {
 
 constexpr int WAVES = 8;
@@ -98,6 +102,26 @@ __device__ __forceinline__ void layer16(const char* lds, const bf16x8 (&bin)[16]
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[h][cb][r] = bias;
+#if SHAPE16_PF
+    // A fragments one k-block ahead in a second register set (no write to a register an in-flight
+    // MFMA still reads: the hazard s_nops of the plain loop)
+    bf16x8 a[2][2];
+    a[0][0] = *(const bf16x8*)(lds + ((2 * p) * 8) * 1024 + lane * 16);
+    a[0][1] = *(const bf16x8*)(lds + ((2 * p + 1) * 8) * 1024 + lane * 16);
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      const int c = kb & 1;
+      if (kb + 1 < 8) {
+        a[c ^ 1][0] = *(const bf16x8*)(lds + ((2 * p) * 8 + kb + 1) * 1024 + lane * 16);
+        a[c ^ 1][1] = *(const bf16x8*)(lds + ((2 * p + 1) * 8 + kb + 1) * 1024 + lane * 16);
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        acc[0][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][0], bin[cb * 8 + kb], acc[0][cb], 0, 0, 0);
+        acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][1], bin[cb * 8 + kb], acc[1][cb], 0, 0, 0);
+      }
+    }
+#else
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb) {
       const bf16x8 a0 = *(const bf16x8*)(lds + ((2 * p) * 8 + kb) * 1024 + lane * 16);
@@ -108,6 +132,7 @@ __device__ __forceinline__ void layer16(const char* lds, const bf16x8 (&bin)[16]
         acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bin[cb * 8 + kb], acc[1][cb], 0, 0, 0);
       }
     }
+#endif
     if (p > 0) epi16(prev, bout, p - 1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll

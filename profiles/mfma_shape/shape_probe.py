@@ -1,6 +1,8 @@
 """A/B of the two bf16 MFMA shapes on the forward's layer body (shape_probe.hip): wall time and the
 clock held, on random data, after >= `warm` seconds of back-to-back launches, alternating shapes.
-usage: python profiles/mfma_shape/shape_probe.py [rounds] [warm_s] [layers]   (build: make -C profiles/mfma_shape)"""
+usage: python profiles/mfma_shape/shape_probe.py [rounds] [warm_s] [layers]   (build: make -C profiles/mfma_shape;
+PROBE_LIB=<path> selects another build, e.g. libshape_probe_pf.so: the 16x16x32 body with its A fragments
+one k-block ahead, make -C profiles/mfma_shape pf)"""
 import ctypes
 import json
 import os
@@ -18,7 +20,7 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     warm = float(sys.argv[2]) if len(sys.argv) > 2 else 2.0
     layers = int(sys.argv[3]) if len(sys.argv) > 3 else 200
-    lib = ctypes.CDLL(os.path.join(HERE, "libshape_probe.so"))
+    lib = ctypes.CDLL(os.environ.get("PROBE_LIB", os.path.join(HERE, "libshape_probe.so")))
     lib.shape_probe_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
                                        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     dev = torch.device("cuda", 0)
