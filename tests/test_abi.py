@@ -100,3 +100,21 @@ def test_ctypes_signatures_match_header_arity():
     counts = _param_counts()
     bad = {n: (len(args), counts[n]) for n, (_, args) in nat._SIGS.items() if n in counts and len(args) != counts[n]}
     assert not bad, bad
+
+
+def test_training_workspace_fits_the_benchmark_shard():
+    """The BF16 training workspace (block-major rows of S_0..S_7 / dz_0..dz_7 / dz_b) stays
+    at ~6.4 KB of activations per sample: configs[1]'s 2^17 x 128 samples and a 2^18-ray shard fit one
+    288 GB MI355X (host-only query, no GPU)."""
+    import ctypes
+    nat, L = _lib()
+    cfg = dict(mode=nat.MODE_BF16, rd=1, aabb=[-1.5] * 3 + [1.5] * 3, near=1.43, far=6.63)
+    for rays in (131072, 262144):
+        desc = nat._desc(cfg, rays, 128, True, True)
+        b = L.den_render_workspace_bytes(ctypes.byref(desc))
+        per_sample = b / (rays * 128)
+        print(f"[{rays} rays] workspace {b / 1e9:.1f} GB = {per_sample:.0f} B per sample")
+        assert 6000 < per_sample < 6700 and b < 250e9
+    # the F32 parity layout keeps contiguous tensors (no rows): ~20 KB per sample
+    desc = nat._desc(dict(cfg, mode=nat.MODE_F32), 4096, 128, True, True)
+    assert L.den_render_workspace_bytes(ctypes.byref(desc)) / (4096 * 128) > 15000
