@@ -144,9 +144,9 @@ def _render_grads(mode, rd, R, n_samples, seed, bwd_path=0):
 @pytest.mark.parametrize("rd,R", [(1, 1024), (3, 1024), (3, 4096)])
 def test_hidden_layer_major_backward_matches_sample_major(rd, R):
     """BF16: the layer-major backward (den_hidden.hip: Lb and L7..L1, several 32-sample blocks per
-    persistent workgroup; the Lr weight gradient fused into render_bwd_kernel<1, 1>) against the
-    sample-major chain + split-K GEMM path on the same bf16 operands -- only f32 summation order
-    differs.  R = 1024: 131072 samples = 4096 wave blocks = 16 per workgroup, 512 render
+    persistent workgroup; the Lr weight gradient fused into render_bwd_kernel<1, 1>; its activations
+    in the block-major rows of den_geom.h SROW_BYTES) against the sample-major chain + split-K GEMM
+    path (contiguous tensors) on the same bf16 operands -- only f32 summation order differs.  R = 1024: 131072 samples = 4096 wave blocks = 16 per workgroup, 512 render
     workgroups (one Lr partial per stage-1 row); R = 4096: 2048 render workgroups (two per row)."""
     c1, g1, b1, _ = _render_grads("bf16", rd, R, 128, seed=21)
     c2, g2, b2, _ = _render_grads("bf16", rd, R, 128, seed=21, bwd_path=1)
