@@ -175,7 +175,8 @@ __device__ __forceinline__ void hb_wait_vm_lgkm0() {
 __device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, float (&sd)[2]) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  __builtin_amdgcn_sched_barrier(0);  // its operands are not read ahead into the previous phase (registers)
+  // (no scheduling fence: with the dot2 row its LDS reads may start under the dW MFMAs' tail, no
+  // spills; Lb 5.398 -> 5.337 ms in ABBA order, profiles/r06ah_ab.jsonl)
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const bf16x8 sv = *(const bf16x8*)(sig + 32 * kk + 16 * (lane >> 5));
