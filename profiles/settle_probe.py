@@ -5,6 +5,7 @@ steps from the start under one settle policy applied right after the workspace i
   none   -- as bench.py before r06
   zero   -- the workspace written once (ws.zero_(), every page touched) and synchronised
   sleep  -- 2 s idle
+  second -- a second buffer of the workspace's size allocated and kept (never used)
 usage: python profiles/settle_probe.py POLICY [windows] [steps_per_window]"""
 import json
 import os
@@ -37,6 +38,8 @@ def main():
         torch.cuda.synchronize()
     elif policy == "sleep":
         time.sleep(2.0)
+    elif policy == "second":
+        spare = torch.empty_like(ts.ws)  # noqa: F841 (kept alive for the whole run)
     out = {"policy": policy, "setup_s": round(time.perf_counter() - t_alloc, 2), "windows": []}
     nat.timing_enable(True)
     nat.timing_collect()
