@@ -399,9 +399,9 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   {
     TimedLaunch timed_(lb ? T_HIDDEN_LB : T_HIDDEN_BWD, s);
     if (lb)
-      hipLaunchKernelGGL(hidden_bwd_kernel<true>, dim3((unsigned)grid), dim3(HB_THREADS), 0, s, H);
+      hipLaunchKernelGGL(hidden_bwd_kernel<true>, dim3((unsigned)grid), dim3(HbCfg<true>::THREADS), 0, s, H);
     else
-      hipLaunchKernelGGL(hidden_bwd_kernel<false>, dim3((unsigned)grid), dim3(HB_THREADS), 0, s, H);
+      hipLaunchKernelGGL(hidden_bwd_kernel<false>, dim3((unsigned)grid), dim3(HbCfg<false>::THREADS), 0, s, H);
   }
   DEN_LAUNCHED();
   if (lb) return launch_dwstream_reduce(d, L, ws, 9, 8, 0, 9, L_B, WIDTH, 0, 1, grad, s);

@@ -3,10 +3,11 @@
 //
 // One launch per layer l (transposed layer j = 10 - l; Lb = l 8, j 2), one persistent workgroup per CU
 // sweeping a contiguous range of 32-sample wave blocks of the wave-block-major activation tensors
-// (den_geom.h).  Per block, wave w of 4 (one per SIMD, 512 VGPRs) owns rows [64w, 64w + 64):
-//   chain : dS_{l-1} = W_l^T dz_l                (A = W_l^T row tiles 2w, 2w+1 held in VGPRs for
+// (den_geom.h).  Per block, wave w owns HbCfg::RT W^T row tiles (L7..L1: 8 waves, two per SIMD at
+// 256 registers, row tile w; Lb: 4 waves, one per SIMD at 512 registers, row tiles 2w, 2w + 1):
+//   chain : dS_{l-1} = W_l^T dz_l                (A = the wave's W_l^T row tiles held in registers for
 //           dz_{l-1} = dS_{l-1} * (1 - 2^-S'_{l-1})   the whole launch, B = dz_l fragments from LDS)
-//   dW    : dW_l[rows 64w..][all 256] += dz_l (x) S'_{l-1},  db_l += dz_l
+//   dW    : dW_l[the wave's rows][all 256] += dz_l (x) S'_{l-1},  db_l += dz_l
 //           (k = samples: both operands by ds_read_b64_tr_b16 from the same LDS blocks; the bias from
 //           VALU sums of the dz operand), accumulated in registers over the whole range, written once as a
 //           split-K partial for dw_reduce_kernel (den_dw.hip layout, MT = NT = 8).
@@ -21,8 +22,16 @@
 
 namespace den {
 
-constexpr int HB_WAVES = 4;
-constexpr int HB_THREADS = 64 * HB_WAVES;
+// Waves per workgroup: L7..L1 run 8 (two per SIMD at 256 registers, one W^T row tile each: 4.559 ->
+// 4.327 ms per launch against 4 waves at 512 registers, ABBA order, profiles/r06ar_ab.jsonl); Lb keeps
+// 4 (two row tiles per wave: its 17th k-step and sigma row spill at 256 registers).
+template <bool LB>
+struct HbCfg {
+  static constexpr int WAVES = LB ? 4 : 8;
+  static constexpr int RT = 8 / WAVES;         // W^T row tiles per wave
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int STORE_OPS = 2 * RT;     // dz_{l-1} stores per wave per block
+};
 constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
 constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
 constexpr int HB_SIG = 256;            // LB: LDS bytes for sigma's bf16[32] dz of a block (aligned)
@@ -38,7 +47,6 @@ constexpr int HB_PF = 4;          // dz_l fragments read ahead of the chain MFMA
 constexpr int HB_DEPTH_LB = 3;    // blocks in flight ahead of the computed one (Lb: 33 KiB slots, <= 4 fit)
 constexpr int HB_DEPTH_L = DEN_HB_DEPTH_L;  // L7..L1 (32 KiB slots: up to 4 ahead in 160 KiB; 4 measured
                                             // no faster with the block-major rows, profiles/r06y_ab.jsonl)
-constexpr int HB_STORE_OPS = 4;                          // dz_{l-1} stores per wave per block
 
 typedef short hb_v4i16 __attribute__((ext_vector_type(4)));
 
@@ -92,11 +100,12 @@ __device__ __forceinline__ int hb_slot(int lane, int f) {
 
 // LDS-DMA of one 16 KiB block (pieces pc = 2t + f of 1 KiB): the destination of an LDS-DMA
 // instruction is linear, so lane p fetches the tile lane whose fragment belongs in slot p.
+template <int WAVES>
 __device__ __forceinline__ void hb_dma(const char* src, char* dst) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int q = 0; q < 16 / HB_WAVES; ++q) {
-    const int pc = q * HB_WAVES + wave;  // wave-uniform
+  for (int q = 0; q < 16 / WAVES; ++q) {
+    const int pc = q * WAVES + wave;  // wave-uniform
     __builtin_amdgcn_global_load_lds((const void*)(src + pc * 1024 + hb_slot(lane, pc & 1) * 16),
                                      (lds_ptr_t)(dst + pc * 1024), 16, 0, 0);
   }
@@ -106,15 +115,16 @@ __device__ __forceinline__ void hb_dma(const char* src, char* dst) {
 // every LDS read wait vmcnt(0) for the prefetches in flight (it cannot tell the ring slots apart);
 // hidden_bwd_kernel waits for them explicitly (hb_wait_vm_lgkm0 + barrier).  The "memory" clobber
 // keeps LDS reads and global stores in program order around it.
+template <int WAVES>
 __device__ __forceinline__ void hb_dma_untracked(const char* src, char* dst) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // per-lane 32-bit offsets (two: the slot permutation depends on the fragment parity); the 64-bit
   // base stays in SGPRs (saddr form), so the ring needs no per-instruction VGPR address pairs
   const uint32_t off0 = (uint32_t)hb_slot(lane, 0) * 16, off1 = (uint32_t)hb_slot(lane, 1) * 16;
 #pragma unroll
-  for (int q = 0; q < 16 / HB_WAVES; ++q) {
+  for (int q = 0; q < 16 / WAVES; ++q) {
     // wave-uniform piece index (readfirstlane is 32-bit: never pass it a 64-bit pointer)
-    const int pc = __builtin_amdgcn_readfirstlane(q * HB_WAVES + wave);
+    const int pc = __builtin_amdgcn_readfirstlane(q * WAVES + wave);
     const char* base = src + pc * 1024;
     const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(dst + pc * 1024));
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"((pc & 1) ? off1 : off0),
@@ -172,7 +182,8 @@ __device__ __forceinline__ void hb_wait_vm_lgkm0() {
 // dependent 32x32x16 MFMAs into one accumulator per block (tile 2w in column 0, 2w + 1 in column 16 of
 // a 16-register tile) -- 703 cycles per block of the Lb launch's 5.5 k (DEN_HIDDEN_PROF,
 // profiles/r06c_hidden_prof.json), the MFMA chain's latency exposed -- and frees 14 registers.
-__device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, float (&sd)[2]) {
+__device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, float (&sd)[HbCfg<true>::RT]) {
+  constexpr int HB_RT = HbCfg<true>::RT;
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // (no scheduling fence: with the dot2 row its LDS reads may start under the dW MFMAs' tail, no
@@ -181,8 +192,8 @@ __device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, flo
   for (int kk = 0; kk < 2; ++kk) {
     const bf16x8 sv = *(const bf16x8*)(sig + 32 * kk + 16 * (lane >> 5));
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const bf16x8 a = hb_tr_frag(sb + (2 * wave + t) * HB_TILE, kk);
+    for (int t = 0; t < HB_RT; ++t) {
+      const bf16x8 a = hb_tr_frag(sb + (HB_RT * wave + t) * HB_TILE, kk);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const bf16x2_t x = {a[2 * q], a[2 * q + 1]}, y = {sv[2 * q], sv[2 * q + 1]};
@@ -200,8 +211,10 @@ __device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, flo
 // products (hb_sigma_dw).
 template <bool LB>
 __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, int64_t b,
-                                         const bf16x8 (&wt)[2][LB ? 17 : 16], f32x16 (&dw)[2][8], float (&db)[2],
-                                         float (&sd)[2], float& sdb, HbProf& hp) {
+                                         const bf16x8 (&wt)[HbCfg<LB>::RT][LB ? 17 : 16],
+                                         f32x16 (&dw)[HbCfg<LB>::RT][8], float (&db)[HbCfg<LB>::RT],
+                                         float (&sd)[HbCfg<LB>::RT], float& sdb, HbProf& hp) {
+  constexpr int HB_RT = HbCfg<LB>::RT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int DZ_BYTES = LB ? HB_BLOCK + HB_SIG : HB_BLOCK;
   const char* dzb = cur;
@@ -210,23 +223,23 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
   // chain: both row tiles of this wave share each dz_l fragment (K = 256, 16 k-steps): one LDS read
   // feeds two independent MFMAs, and the reads run HB_PF k-steps ahead of their use (issued
   // one per k-step, the compiler waited out the LDS latency before every MFMA)
-  f32x16 accs[2];
+  f32x16 accs[HB_RT];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < HB_RT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) accs[t][r] = 0.0f;
   // the epilogue's S'_{l-1} fragments (the activation derivative's input), read before the chain so
   // that their LDS latency hides under its 32 MFMAs instead of opening each tile's epilogue
-  bf16x8 sf[2][2];
+  bf16x8 sf[HB_RT][2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < HB_RT; ++t)
 #pragma unroll
-    for (int f = 0; f < 2; ++f) sf[t][f] = hb_frag(sb + (2 * wave + t) * HB_TILE, f);
+    for (int f = 0; f < 2; ++f) sf[t][f] = hb_frag(sb + (HB_RT * wave + t) * HB_TILE, f);
   __builtin_amdgcn_sched_barrier(0);  // (left alone, the compiler sinks these reads back to their use)
   // L7..L1: the epilogue's 32 activation-derivative factors 1 - 2^-S', computed in the chain MFMAs'
   // shadow (r06, profiles/r06v_ab.jsonl: 4.639 -> 4.607 ms per launch in ABBA order; Lb's 17th k-step
   // leaves no registers for them)
-  float dv[2][16];
+  float dv[HB_RT][16];
   {
     bf16x8 bq[HB_PF];
 #pragma unroll
@@ -235,12 +248,13 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     for (int k = 0; k < 16; ++k) {
       const bf16x8 cur = bq[k % HB_PF];
       if (k + HB_PF < 16) bq[k % HB_PF] = hb_frag(dzb + ((k + HB_PF) >> 1) * HB_TILE, (k + HB_PF) & 1);
-      accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[0][k], cur, accs[0], 0, 0, 0);
-      accs[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[1][k], cur, accs[1], 0, 0, 0);
-      if constexpr (!LB) {  // two of the derivative factors per k-step
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int t = k >> 3, r = 2 * (k & 7) + e;
+      for (int t = 0; t < HB_RT; ++t)
+        accs[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[t][k], cur, accs[t], 0, 0, 0);
+      if constexpr (!LB) {  // HB_RT of the derivative factors per k-step
+#pragma unroll
+        for (int e = 0; e < HB_RT; ++e) {
+          const int q = k * HB_RT + e, t = q >> 4, r = q & 15;
           dv[t][r] = dsoftplus2_scaled_from_out((float)sf[t][r >> 3][r & 7]);
         }
       }
@@ -250,14 +264,15 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     // B fragment of the sigma k-step: sample c = lane (lanes 0..31) has sigma at stored position 0
     const __bf16 z = *(const __bf16*)(sig + 2 * (lane & 31)), zz = (__bf16)0.0f;
     const bf16x8 bs = {lane < 32 ? z : zz, zz, zz, zz, zz, zz, zz, zz};
-    accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[0][16], bs, accs[0], 0, 0, 0);
-    accs[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[1][16], bs, accs[1], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < HB_RT; ++t)
+      accs[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[t][16], bs, accs[t], 0, 0, 0);
     sdb += (float)bs[0];
   }
   hp.mark(1);
   // then the activation derivative
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < HB_RT; ++t) {
     f32x16 acc = accs[t];
     const bf16x8 s0 = sf[t][0], s1 = sf[t][1];
 #pragma unroll
@@ -272,7 +287,7 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     // dz_{l-1} tile: stored now, the weight-gradient MFMAs below cover its write latency
     bf16x8 of[2];
     acc_to_frags<1>(acc, of);
-    char* d = P.dz_out + b * P.bs_dz_out + (2 * wave + t) * HB_TILE + lane * 16;  // dz_{l-1}: 8 tiles per block
+    char* d = P.dz_out + b * P.bs_dz_out + (HB_RT * wave + t) * HB_TILE + lane * 16;  // dz_{l-1}: 8 tiles per block
     __builtin_nontemporal_store(of[0], (bf16x8*)d);
     __builtin_nontemporal_store(of[1], (bf16x8*)(d + 1024));
     // keep the scheduler from hoisting the next phase's LDS reads here (register pressure: W^T lives
@@ -283,19 +298,19 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
   // weight / bias gradients over the block's 32 samples (two k-steps of 16)
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
-    const bf16x8 a0 = hb_tr_frag(dzb + (2 * wave) * HB_TILE, kk);
-    const bf16x8 a1 = hb_tr_frag(dzb + (2 * wave + 1) * HB_TILE, kk);
+    bf16x8 a[HB_RT];
+#pragma unroll
+    for (int t = 0; t < HB_RT; ++t) a[t] = hb_tr_frag(dzb + (HB_RT * wave + t) * HB_TILE, kk);
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
       const bf16x8 bb = hb_tr_frag(sb + n * HB_TILE, kk);
-      dw[0][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bb, dw[0][n], 0, 0, 0);
-      dw[1][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bb, dw[1][n], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < HB_RT; ++t) dw[t][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], bb, dw[t][n], 0, 0, 0);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      db[0] += (float)a0[j];
-      db[1] += (float)a1[j];
-    }
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int t = 0; t < HB_RT; ++t) db[t] += (float)a[t][j];
   }
   hp.mark(3);
   // sigma's weight-gradient row last (placed between the chain and the epilogue or before the dW
@@ -308,7 +323,8 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
 
 template <bool LB>
 DEN_CODE_ALIGN  // page-aligned code (r04y A/B)
-__global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P) {
+__global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(HiddenArgs P) {
+  constexpr int HB_WAVES = HbCfg<LB>::WAVES, HB_RT = HbCfg<LB>::RT, HB_STORE_OPS = HbCfg<LB>::STORE_OPS;
   // HB_RING LDS slots of [dz_l block | S'_{l-1} block]; HB_DEPTH blocks in flight ahead of the one
   // being computed.  Each wave waits for its own part of block b+1 at the end of block b (vmcnt; the
   // younger prefetches and stores stay in flight), then the workgroup barrier publishes every part.
@@ -334,30 +350,33 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
   const int64_t n_it = b0 < P.n_blocks ? (b0 + P.per_wg < P.n_blocks ? P.per_wg : P.n_blocks - b0) : 0;
   auto blk = [&](int64_t it) { return b0 + it; };
   auto fetch = [&](int64_t b, char* dst) {
-    hb_dma_untracked(P.dz_in + b * P.bs_dz_in, dst);
+    hb_dma_untracked<HB_WAVES>(P.dz_in + b * P.bs_dz_in, dst);
     if constexpr (LB) hb_dma_sigma(P.sigma_dz + b * 64, dst + HB_BLOCK);
-    hb_dma_untracked(P.s_in + b * P.bs_s, dst + DZ_STAGED);
+    hb_dma_untracked<HB_WAVES>(P.s_in + b * P.bs_s, dst + DZ_STAGED);
   };
 #pragma unroll
   for (int u = 0; u < HB_DEPTH; ++u)
     if (u < n_it) fetch(blk(u), lds + u * SLOT);
 
   // W_l^T row tiles 2w, 2w+1: packed [row tile][kappa][lane][8] = the chain's A fragments
-  bf16x8 wt[2][KST];
+  bf16x8 wt[HB_RT][KST];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < HB_RT; ++t)
 #pragma unroll
     for (int k = 0; k < KST; ++k)
-      wt[t][k] = *(const bf16x8*)(P.w + (int64_t)(2 * wave + t) * ROW_BYTES + k * 1024 + lane * 16);
-  f32x16 dw[2][8];
+      wt[t][k] = *(const bf16x8*)(P.w + (int64_t)(HB_RT * wave + t) * ROW_BYTES + k * 1024 + lane * 16);
+  f32x16 dw[HB_RT][8];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < HB_RT; ++t)
 #pragma unroll
     for (int n = 0; n < 8; ++n)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dw[t][n][r] = 0.0f;
-  float db[2] = {0.0f, 0.0f};  // bias partial: feature (lane & 31) of row tile 2w + t, this lane's samples
-  float sd[2] = {0.0f, 0.0f};  // LB: sigma's weight-gradient row, stored position lane & 31 of S7 tile 2w + t
+  float db[HB_RT], sd[HB_RT];  // bias partial: feature (lane & 31) of row tile HB_RT w + t, this lane's
+                               // samples; LB: sigma's weight-gradient row, stored position lane & 31 of S7
+                               // tile HB_RT w + t
+#pragma unroll
+  for (int t = 0; t < HB_RT; ++t) db[t] = sd[t] = 0.0f;
   float sdb = 0.0f;  // LB: sigma's bias gradient (lanes 0..31)
   HbProf hp;
   hp.init();
@@ -388,19 +407,21 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
 #ifdef DEN_HIDDEN_PROF
   hp.p[7] = hp.t - hp_start;
   if (blockIdx.x < 256 && lane == 0) {
+    // (the first four waves of the workgroup: the 8-wave L7..L1 launches record waves 0..3)
+    if (wave < 4)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) den_hidden_prof[((LB ? 256 : 0) + blockIdx.x) * 32 + wave * 8 + q] = hp.p[q];
+      for (int q = 0; q < 8; ++q) den_hidden_prof[((LB ? 256 : 0) + blockIdx.x) * 32 + wave * 8 + q] = hp.p[q];
   }
 #endif
   // split-K partial of this workgroup (dw_gemm_kernel layout: [wg][mt][nt][lane][16]); the bias
   // goes where that layout's ones tile (nt = 8) keeps it: column 0 = lanes 0 and 32, row m in
   // register (m & 3) + 4 (m >> 3) of lane 32 ((m >> 2) & 1)
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < HB_RT; ++t) {
     const float bsum = db[t] + __shfl_xor(db[t], 32, 64);
     if (lane < 32) {
       const int m = lane;
-      float* o = P.partial + (((int64_t)blockIdx.x * MTA + 2 * wave + t) * 9 + 8) * 1024;
+      float* o = P.partial + (((int64_t)blockIdx.x * MTA + HB_RT * wave + t) * 9 + 8) * 1024;
       o[(32 * ((m >> 2) & 1)) * 16 + (m & 3) + 4 * (m >> 3)] = bsum;
     }
   }
@@ -409,9 +430,9 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
     // column 32 n + lane; every other element of the tiles written as zero.  Stored position q of S7
     // tile 2w + nn: sd[nn] of lanes q and q + 32 (the two sample halves)
 #pragma unroll
-    for (int nn = 0; nn < 2; ++nn) {
+    for (int nn = 0; nn < HB_RT; ++nn) {
       const float v = sd[nn] + __shfl_xor(sd[nn], 32, 64);
-      float* o = P.partial + (((int64_t)blockIdx.x * MTA + 8) * 9 + 2 * wave + nn) * 1024 + lane * 16;
+      float* o = P.partial + (((int64_t)blockIdx.x * MTA + 8) * 9 + HB_RT * wave + nn) * 1024 + lane * 16;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         f32x4 z = {q == 0 && lane < 32 ? v : 0.0f, 0.0f, 0.0f, 0.0f};
@@ -429,10 +450,10 @@ __global__ __launch_bounds__(HB_THREADS, 1) void hidden_bwd_kernel(HiddenArgs P)
     }
   }
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < HB_RT; ++t)
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
-      float* o = P.partial + (((int64_t)blockIdx.x * MTA + 2 * wave + t) * 9 + n) * 1024 + lane * 16;
+      float* o = P.partial + (((int64_t)blockIdx.x * MTA + HB_RT * wave + t) * 9 + n) * 1024 + lane * 16;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         f32x4 v = {dw[t][n][4 * q], dw[t][n][4 * q + 1], dw[t][n][4 * q + 2], dw[t][n][4 * q + 3]};
