@@ -3,8 +3,7 @@
 //
 // One launch per layer l (transposed layer j = 10 - l; Lb = l 8, j 2), one persistent workgroup per CU
 // sweeping a contiguous range of 32-sample wave blocks of the wave-block-major activation tensors
-// (den_geom.h).  Per block, wave w owns HbCfg::RT W^T row tiles (L7..L1: 8 waves, two per SIMD at
-// 256 registers, row tile w; Lb: 4 waves, one per SIMD at 512 registers, row tiles 2w, 2w + 1):
+// (den_geom.h).  Per block, wave w of 8 (two per SIMD at 256 registers) owns W^T row tile w:
 //   chain : dS_{l-1} = W_l^T dz_l                (A = the wave's W_l^T row tiles held in registers for
 //           dz_{l-1} = dS_{l-1} * (1 - 2^-S'_{l-1})   the whole launch, B = dz_l fragments from LDS)
 //   dW    : dW_l[the wave's rows][all 256] += dz_l (x) S'_{l-1},  db_l += dz_l
@@ -22,15 +21,19 @@
 
 namespace den {
 
-// Waves per workgroup: L7..L1 run 8 (two per SIMD at 256 registers, one W^T row tile each: 4.559 ->
-// 4.327 ms per launch against 4 waves at 512 registers, ABBA order, profiles/r06ar_ab.jsonl); Lb keeps
-// 4 (two row tiles per wave: its 17th k-step and sigma row spill at 256 registers).
+// Waves per workgroup: 8 (two per SIMD at 256 registers, one W^T row tile each).  L7..L1: 4.559 ->
+// 4.327 ms per launch against 4 waves at 512 registers (ABBA order, profiles/r06ar_ab.jsonl); Lb: 5.211
+// -> 4.934 ms per launch with its sigma k-step W^T fragment in LDS, the S' fragments read in the
+// epilogue and dz fragments read one k-step ahead (profiles/r06at_ab.jsonl; held in registers, these
+// spill at 256; 2 ahead measured 4.960).
 template <bool LB>
 struct HbCfg {
-  static constexpr int WAVES = LB ? 4 : 8;
+  static constexpr int WAVES = 8;
   static constexpr int RT = 8 / WAVES;         // W^T row tiles per wave
   static constexpr int THREADS = 64 * WAVES;
   static constexpr int STORE_OPS = 2 * RT;     // dz_{l-1} stores per wave per block
+  // Lb: the sigma k-step's W^T fragment lives in LDS (its registers would spill)
+  static constexpr bool WT16_LDS = LB;
 };
 constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
 constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
@@ -40,7 +43,8 @@ constexpr int HB_SIG = 256;            // LB: LDS bytes for sigma's bf16[32] dz 
 // help); dz_l fragments read 4 k-steps ahead; the epilogue and the dW MFMAs kept in separate phases
 // (overlapping them, in compiler order or a pinned interleave, was 1-2 ms per step slower).
 constexpr int HB_GRID_MAX = 256;  // persistent workgroups (one per CU)
-constexpr int HB_PF = 4;          // dz_l fragments read ahead of the chain MFMAs
+constexpr int HB_PF_L = 4;        // dz_l fragments read ahead of the chain MFMAs
+constexpr int HB_PF_LB = 1;       // (Lb: registers, see HbCfg)
 #ifndef DEN_HB_DEPTH_L
 #define DEN_HB_DEPTH_L 3
 #endif
@@ -175,12 +179,12 @@ __device__ __forceinline__ void hb_wait_vm_lgkm0() {
 
 // One 32-sample block from its LDS slot: the chain (dz_{l-1} stored), then the dW / db accumulation.
 // Sigma's weight-gradient row of one block (LB, see hb_block): dW_sigma[q] = sum_n dz_sigma[n] S7[n][q]
-// for the wave's S7 tiles 2w, 2w + 1 by VALU dot products: the transposed fragment of an S7 tile
+// for the wave's S7 tile w by VALU dot products: the transposed fragment of an S7 tile
 // (hb_tr_frag: lane l holds stored position l & 31 of the tile at samples 16 kk + 8 (l >> 5) + j) times
-// the same eight samples' sigma dz, four v_dot2c_f32_bf16 per fragment, into one f32 per tile and lane
+// the same eight samples' sigma dz, four v_dot2c_f32_bf16 per fragment, into one f32 per lane
 // (the two lane halves hold the two sample halves; added at the end).  r06: this replaced four
-// dependent 32x32x16 MFMAs into one accumulator per block (tile 2w in column 0, 2w + 1 in column 16 of
-// a 16-register tile) -- 703 cycles per block of the Lb launch's 5.5 k (DEN_HIDDEN_PROF,
+// dependent 32x32x16 MFMAs into one accumulator per block (at 4 waves: tile 2w in column 0, 2w + 1 in
+// column 16 of a 16-register tile) -- 703 cycles per block of the Lb launch's 5.5 k (DEN_HIDDEN_PROF,
 // profiles/r06c_hidden_prof.json), the MFMA chain's latency exposed -- and frees 14 registers.
 __device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, float (&sd)[HbCfg<true>::RT]) {
   constexpr int HB_RT = HbCfg<true>::RT;
@@ -207,14 +211,15 @@ __device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, flo
 // bottleneck tiles, sigma's dz arrives as 32 bf16 per block (staged after them); the chain takes it as
 // a 17th k-step whose B fragment holds sigma at stored position 0 (W_b^T's sigma column; the rest of
 // that k-step and the 18th are zero padding).  Sigma's weight-gradient row would be a ninth row tile
-// of 8 more accumulator tiles; instead wave w forms the row for its S7 tiles 2w, 2w + 1 by VALU dot
-// products (hb_sigma_dw).
+// of 8 more accumulator tiles; instead wave w forms the row for its S7 tile w by VALU dot products
+// (hb_sigma_dw).
 template <bool LB>
-__device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, int64_t b,
+__device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, const bf16x8* wt16, int64_t b,
                                          const bf16x8 (&wt)[HbCfg<LB>::RT][LB ? 17 : 16],
                                          f32x16 (&dw)[HbCfg<LB>::RT][8], float (&db)[HbCfg<LB>::RT],
                                          float (&sd)[HbCfg<LB>::RT], float& sdb, HbProf& hp) {
   constexpr int HB_RT = HbCfg<LB>::RT;
+  constexpr int HB_PF = LB ? HB_PF_LB : HB_PF_L;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int DZ_BYTES = LB ? HB_BLOCK + HB_SIG : HB_BLOCK;
   const char* dzb = cur;
@@ -234,7 +239,8 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
 #pragma unroll
   for (int t = 0; t < HB_RT; ++t)
 #pragma unroll
-    for (int f = 0; f < 2; ++f) sf[t][f] = hb_frag(sb + (HB_RT * wave + t) * HB_TILE, f);
+    for (int f = 0; f < 2; ++f)
+      if constexpr (!HbCfg<LB>::WT16_LDS) sf[t][f] = hb_frag(sb + (HB_RT * wave + t) * HB_TILE, f);
   __builtin_amdgcn_sched_barrier(0);  // (left alone, the compiler sinks these reads back to their use)
   // L7..L1: the epilogue's 32 activation-derivative factors 1 - 2^-S', computed in the chain MFMAs'
   // shadow (r06, profiles/r06v_ab.jsonl: 4.639 -> 4.607 ms per launch in ABBA order; Lb's 17th k-step
@@ -266,7 +272,9 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
     const bf16x8 bs = {lane < 32 ? z : zz, zz, zz, zz, zz, zz, zz, zz};
 #pragma unroll
     for (int t = 0; t < HB_RT; ++t)
-      accs[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[t][16], bs, accs[t], 0, 0, 0);
+      accs[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(HbCfg<LB>::WT16_LDS ? wt16[(HB_RT * wave + t) * 64 + lane]
+                                                                                    : wt[t][16],
+                                                        bs, accs[t], 0, 0, 0);
     sdb += (float)bs[0];
   }
   hp.mark(1);
@@ -274,7 +282,9 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, i
 #pragma unroll
   for (int t = 0; t < HB_RT; ++t) {
     f32x16 acc = accs[t];
-    const bf16x8 s0 = sf[t][0], s1 = sf[t][1];
+    // (Lb reads them here: held across its chain they would spill)
+    const bf16x8 s0 = HbCfg<LB>::WT16_LDS ? hb_frag(sb + (HB_RT * wave + t) * HB_TILE, 0) : sf[t][0];
+    const bf16x8 s1 = HbCfg<LB>::WT16_LDS ? hb_frag(sb + (HB_RT * wave + t) * HB_TILE, 1) : sf[t][1];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       if constexpr (!LB) {
@@ -342,6 +352,7 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
   constexpr int YOUNGER = HB_STORE_OPS + (HB_DEPTH - 1) * (DMA_OPS + HB_STORE_OPS);
   static_assert(HB_RING * SLOT <= 160 * 1024, "hidden ring exceeds the LDS");
   __shared__ __attribute__((aligned(16))) char lds[HB_RING * SLOT];
+  __shared__ bf16x8 wt16[HbCfg<LB>::WT16_LDS ? 8 * 64 : 1];
   DEN_CLOCK_BEGIN();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // a contiguous range of P.per_wg blocks per workgroup (r03: strided by the grid, so that all
@@ -358,13 +369,17 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
   for (int u = 0; u < HB_DEPTH; ++u)
     if (u < n_it) fetch(blk(u), lds + u * SLOT);
 
-  // W_l^T row tiles 2w, 2w+1: packed [row tile][kappa][lane][8] = the chain's A fragments
+  // W_l^T row tile w: packed [row tile][kappa][lane][8] = the chain's A fragments
   bf16x8 wt[HB_RT][KST];
 #pragma unroll
   for (int t = 0; t < HB_RT; ++t)
 #pragma unroll
     for (int k = 0; k < KST; ++k)
       wt[t][k] = *(const bf16x8*)(P.w + (int64_t)(HB_RT * wave + t) * ROW_BYTES + k * 1024 + lane * 16);
+  if constexpr (HbCfg<LB>::WT16_LDS) {
+#pragma unroll
+    for (int t = 0; t < HB_RT; ++t) wt16[(HB_RT * wave + t) * 64 + lane] = wt[t][16];
+  }
   f32x16 dw[HB_RT][8];
 #pragma unroll
   for (int t = 0; t < HB_RT; ++t)
@@ -394,7 +409,7 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
     // prefetch block it + HB_DEPTH into the slot block it - 1 used (free since the last barrier)
     if (it + HB_DEPTH < n_it) fetch(blk(it + HB_DEPTH), lds + ((u + HB_DEPTH) % HB_RING) * SLOT);
     hp.mark(0);
-    hb_block<LB>(P, lds + u * SLOT, blk(it), wt, dw, db, sd, sdb, hp);
+    hb_block<LB>(P, lds + u * SLOT, wt16, blk(it), wt, dw, db, sd, sdb, hp);
     if (it + HB_DEPTH < n_it) hb_wait_vm_lgkm0<YOUNGER>();
     else hb_wait_vm_lgkm0<0>();
     hp.mark(5);
@@ -407,7 +422,7 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
 #ifdef DEN_HIDDEN_PROF
   hp.p[7] = hp.t - hp_start;
   if (blockIdx.x < 256 && lane == 0) {
-    // (the first four waves of the workgroup: the 8-wave L7..L1 launches record waves 0..3)
+    // (the first four waves of the workgroup)
     if (wave < 4)
 #pragma unroll
       for (int q = 0; q < 8; ++q) den_hidden_prof[((LB ? 256 : 0) + blockIdx.x) * 32 + wave * 8 + q] = hp.p[q];
@@ -428,7 +443,7 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
   if constexpr (LB) {
     // row tile 8 = [sigma, 31 padding rows]: sigma is accumulator row 0 (lanes 0..31, register 0),
     // column 32 n + lane; every other element of the tiles written as zero.  Stored position q of S7
-    // tile 2w + nn: sd[nn] of lanes q and q + 32 (the two sample halves)
+    // tile w: sd[0] of lanes q and q + 32 (the two sample halves)
 #pragma unroll
     for (int nn = 0; nn < HB_RT; ++nn) {
       const float v = sd[nn] + __shfl_xor(sd[nn], 32, 64);
