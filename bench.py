@@ -41,8 +41,10 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (default: WORLD_SIZE under a torch.distributed launcher, else 1)")
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    # every process's first ~10 steps run slow (76 -> 67 ms under a kernel trace with no idle time
+    # between kernels, profiles/r06ax_gaps.jsonl): the default times the steady state
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--rays", type=int, default=131072)
     ap.add_argument("--samples", type=int, default=128)
     ap.add_argument("--rd", type=int, default=1)

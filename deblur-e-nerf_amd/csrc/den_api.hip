@@ -581,9 +581,9 @@ int den_debug_clock(uint64_t* out) {
 #endif
 
 #ifdef DEN_HIDDEN_PROF
-// experiment builds only: per-wave phase cycles of the last L7..L1 and Lb launches (2 x 256 WGs x 4 waves x 8)
+// experiment builds only: per-wave phase cycles of the last L7..L1 and Lb launches (2 x 256 WGs x 8 waves x 8)
 int den_debug_hidden_prof(uint64_t* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(den_hidden_prof), sizeof(uint64_t) * 2 * 256 * 4 * 8) == hipSuccess
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(den_hidden_prof), sizeof(uint64_t) * 2 * 256 * 8 * 8) == hipSuccess
              ? DEN_OK
              : DEN_EHIP;
 }

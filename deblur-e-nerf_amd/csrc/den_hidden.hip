@@ -78,7 +78,7 @@ struct HbProf {
 #endif
 };
 #ifdef DEN_HIDDEN_PROF
-__device__ uint64_t den_hidden_prof[2 * 256 * 4 * 8];
+__device__ uint64_t den_hidden_prof[2 * 256 * 8 * 8];
 #endif
 
 struct HiddenArgs {
@@ -137,7 +137,8 @@ __device__ __forceinline__ void hb_dma_untracked(const char* src, char* dst) {
 }
 
 // LB: sigma's 32 bf16 dz of a wave block (64 B of HiddenArgs.sigma_dz) into LDS, by lanes 0..3;
-// every wave issues it (the same bytes), so each wave's DMA count per block stays uniform
+// every wave issues it (the same bytes), so each wave's DMA count per block stays uniform (issued by one
+// wave only, with its own vmcnt budget: Lb 5.162 -> 5.195 ms, no gain, profiles/r06aw_ab.jsonl)
 __device__ __forceinline__ void hb_dma_sigma(const char* src, char* dst) {
   const int lane = threadIdx.x & 63;
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)dst);
@@ -240,11 +241,13 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, c
   for (int t = 0; t < HB_RT; ++t)
 #pragma unroll
     for (int f = 0; f < 2; ++f)
-      if constexpr (!HbCfg<LB>::WT16_LDS) sf[t][f] = hb_frag(sb + (HB_RT * wave + t) * HB_TILE, f);
+      if constexpr (!LB) sf[t][f] = hb_frag(sb + (HB_RT * wave + t) * HB_TILE, f);
   __builtin_amdgcn_sched_barrier(0);  // (left alone, the compiler sinks these reads back to their use)
   // L7..L1: the epilogue's 32 activation-derivative factors 1 - 2^-S', computed in the chain MFMAs'
-  // shadow (r06, profiles/r06v_ab.jsonl: 4.639 -> 4.607 ms per launch in ABBA order; Lb's 17th k-step
-  // leaves no registers for them)
+  // shadow (r06, profiles/r06v_ab.jsonl: 4.639 -> 4.607 ms per launch in ABBA order).  Lb has no
+  // registers for them: there it is 16 exp2 in the epilogue (+260 cycles per block against L1, phase
+  // split profiles/r06aw_hidden_prof.json), but the same factors in its chain spill 12 registers and
+  // computed right after its sigma k-step still 8
   float dv[HB_RT][16];
   {
     bf16x8 bq[HB_PF];
@@ -276,6 +279,7 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, c
                                                                                     : wt[t][16],
                                                         bs, accs[t], 0, 0, 0);
     sdb += (float)bs[0];
+
   }
   hp.mark(1);
   // then the activation derivative
@@ -283,8 +287,8 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, c
   for (int t = 0; t < HB_RT; ++t) {
     f32x16 acc = accs[t];
     // (Lb reads them here: held across its chain they would spill)
-    const bf16x8 s0 = HbCfg<LB>::WT16_LDS ? hb_frag(sb + (HB_RT * wave + t) * HB_TILE, 0) : sf[t][0];
-    const bf16x8 s1 = HbCfg<LB>::WT16_LDS ? hb_frag(sb + (HB_RT * wave + t) * HB_TILE, 1) : sf[t][1];
+    const bf16x8 s0 = LB ? hb_frag(sb + (HB_RT * wave + t) * HB_TILE, 0) : sf[t][0];
+    const bf16x8 s1 = LB ? hb_frag(sb + (HB_RT * wave + t) * HB_TILE, 1) : sf[t][1];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       if constexpr (!LB) {
@@ -422,10 +426,8 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
 #ifdef DEN_HIDDEN_PROF
   hp.p[7] = hp.t - hp_start;
   if (blockIdx.x < 256 && lane == 0) {
-    // (the first four waves of the workgroup)
-    if (wave < 4)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) den_hidden_prof[((LB ? 256 : 0) + blockIdx.x) * 32 + wave * 8 + q] = hp.p[q];
+    for (int q = 0; q < 8; ++q) den_hidden_prof[((LB ? 256 : 0) + blockIdx.x) * 64 + wave * 8 + q] = hp.p[q];
   }
 #endif
   // split-K partial of this workgroup (dw_gemm_kernel layout: [wg][mt][nt][lane][16]); the bias

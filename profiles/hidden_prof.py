@@ -38,9 +38,9 @@ def main():
     torch.cuda.synchronize()
     nat.timing_enable(False)
     kt = nat.timing_collect()
-    buf = np.zeros(2 * 256 * 4 * 8, dtype=np.uint64)
+    buf = np.zeros(2 * 256 * 8 * 8, dtype=np.uint64)
     assert lib.den_debug_hidden_prof(buf.ctypes.data) == 0
-    p = buf.reshape(2, 256, 4, 8).astype(np.float64)
+    p = buf.reshape(2, 256, 8, 8).astype(np.float64)
     out = {"kernel_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kt.items() if v[1]}, "launches": {}}
     n_blocks = a.rays * a.samples // 32
     for s, name in enumerate(("L1", "Lb")):
@@ -50,8 +50,9 @@ def main():
             v = p[s, :, :, q]
             row[ph] = {"cyc_per_block": round(float(v.mean()) / (n_blocks / 256), 1),
                        "share": round(float(v.mean() / tot.mean()), 4)}
-        # by wave (one per SIMD): the barrier share tells which wave finishes its block last
-        row["barrier_share_by_wave"] = [round(float(p[s, :, w, 6].mean() / tot.mean()), 4) for w in range(4)]
+        # by wave (8, two per SIMD): the barrier share tells which wave finishes its block last
+        row["barrier_share_by_wave"] = [round(float(p[s, :, w, 6].mean() / tot.mean()), 4) for w in range(8)]
+        row["dma_issue_share_by_wave"] = [round(float(p[s, :, w, 0].mean() / tot.mean()), 4) for w in range(8)]
         out["launches"][name] = row
     print(json.dumps(out), flush=True)
 
