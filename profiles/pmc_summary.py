@@ -147,10 +147,12 @@ def main(out_dir, tag, prefix=""):
     with open(os.path.join(out_dir, prefix + "prof", "run_kernel_stats.csv")) as f:
         for r in csv.DictReader(f):
             rows.append(r)
+    # the traced command (PROF_CMD, set by the gpu script; the r02-r06fin3 scripts ran this default)
+    cmd = os.environ.get("PROF_CMD", "python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-gemm-peak")
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
-             "Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python bench.py --steps 5 --warmup 2 "
-             "--no-cpu-baseline --no-gemm-peak` (" + (f"profiles/gpu_{prefix[:-1]}.sh" if prefix else "profiles/gpu_r02a.sh, gpu_r02g.sh")
-             + "); 7 train steps + 3 phase-timing reps per kernel.", "",
+             f"Command: `rocprofv3 --kernel-trace --stats --output-format csv -- {cmd}` ("
+             + (f"profiles/gpu_{prefix[:-1]}.sh" if prefix else "profiles/gpu_r02a.sh, gpu_r02g.sh")
+             + "); W + K train steps + 3 phase-timing reps per kernel.", "",
              "| kernel | calls | avg ms | total % |", "|---|---|---|---|"]
     for r in rows[:20]:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | "
