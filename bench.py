@@ -171,9 +171,11 @@ PHASE_REPS = 3
 # 2 x 128).  BF16 (the layer-major backward):
 #   render_head_bwd : compositing adjoint, Lr^T (rd x 128) + the fused Lr weight gradient (rd x 128),
 #                     Lg^T (128 x 256, bottleneck part) + the fused Lg weight gradient (128 x 283)
-#   hidden_bwd      : 7 launches (L7..L1), each dX (256 x 256) + dW (256 x 256)
+#   hidden_bwd      : 7 launches (L7..L1), each dX (256 x 256) + dW (256 x 256); L5 also the pe columns of
+#                     its dW (256 x 63) and L1 dW_0 (256 x 63): the pe fold (den_hidden.hip PEM)
 #   hidden_bwd_lb   : 1 launch (Lb), dX (256 x 257) + dW (257 x 256)
-#   dwstream        : the weight gradients of L0 (256 x 63) and of L5's pe columns (256 x 63)
+#   dwstream        : the weight gradients of L0 (256 x 63) and of L5's pe columns (256 x 63) when they are
+#                     not folded (den_render_ray_grad's workspace, -DDEN_NO_PE_FOLD builds)
 # F32 (the sample-major parity path):
 #   render_bwd      : the whole dX chain, Lr^T, Lg^T, Lb^T (257 x 256), L7^T..L1^T (7 x 256 x 256)
 #   dw_gemm         : every layer's weight gradient (the forward's MACs)
@@ -182,7 +184,7 @@ def flop_per_sample(rd, mode="bf16"):
     if mode == "bf16":
         return {"render_fwd_kernel": 2.0 * fwd,
                 "render_head_bwd_kernel": 2.0 * (2 * rd * 128 + 128 * 256 + 128 * 283),
-                "hidden_bwd_kernel": 2.0 * 7 * 2 * 256 * 256,
+                "hidden_bwd_kernel": 2.0 * (7 * 2 * 256 * 256 + 2 * 256 * 63),
                 "hidden_bwd_lb_kernel": 2.0 * 2 * 257 * 256,
                 "dwstream_kernel": 2.0 * (256 * 63 * 2)}
     return {"render_fwd_kernel": 2.0 * fwd,
@@ -194,14 +196,15 @@ def flop_per_sample(rd, mode="bf16"):
 BF16_KERNEL_NAMES = {"render_bwd_kernel": "render_head_bwd_kernel", "dw_gemm_kernel": "dwstream_kernel"}
 
 # algorithmic HBM bytes per sample and STEP of each BF16 kernel:
-#   hidden_bwd: L7..L1 each read dz_l + a_(l-1) and write dz_(l-1), 256 bf16 each = 1536 B;
+#   hidden_bwd: L7..L1 each read dz_l + a_(l-1) and write dz_(l-1), 256 bf16 each = 1536 B; L5 and L1 also
+#     read pe (128 B), and L1 keeps dz_0 on chip (-512 B): 7 x 1536 + 2 x 128 - 512 = 10496 B;
 #   hidden_bwd_lb: reads dz_b (257 bf16) + S7, writes dz_7 = 1538 B;
 #   render_fwd: the activations + record it stores for the backward, S0..S7 + bottleneck + G + pe +
 #     record (4096 + 512 + 256 + 128 + 16 B; ve is recomputed by the head backward, not stored);
 #   render_head_bwd: the record + G + bottleneck read, dz_b (256 bottleneck + sigma) written
 #     (16 + 256 + 512 + 514 B; dz_g stays on chip);
 #   dwstream: dz_0 + dz_5 + pe read = 1152 B
-BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536, "hidden_bwd_lb_kernel": 1538, "render_fwd_kernel": 5008,
+BYTES_PER_SAMPLE = {"hidden_bwd_kernel": 7 * 1536 + 2 * 128 - 512, "hidden_bwd_lb_kernel": 1538, "render_fwd_kernel": 5008,
                     "render_head_bwd_kernel": 1298, "dwstream_kernel": 1152}
 
 

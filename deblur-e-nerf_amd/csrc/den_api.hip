@@ -99,7 +99,7 @@ struct WsLayout {
   size_t act[NACT];
   int64_t bstride[NACT + 1];  // bytes from one wave block of each activation (and D_ZB8) to the next
   size_t sigma_dz;            // layer-major BF16: sigma's dz, one bf16 per sample (den_geom.h D_ZB8)
-  size_t rec, bkgd_partial, dw_partial, lr_partial, lr_stage1, total;
+  size_t rec, bkgd_partial, dw_partial, lr_partial, lr_stage1, pe_partial, total;
   int splits;
   int64_t per_split;
 };
@@ -118,6 +118,15 @@ inline int64_t hidden_grid(const den_render_desc* d) { return cap_grid(d, hidden
 // BF16 backward: layer-major hidden layers (den_hidden.hip) unless the descriptor selects the
 // sample-major chain + split-K GEMMs of the F32 mode (bwd_path = 1, A/B comparisons).
 inline bool use_hidden_path(const den_render_desc* d) { return d->mode == DEN_MODE_BF16 && d->bwd_path == 0; }
+// ... with the pe weight gradients folded into the L1 / L5 launches (den_hidden.hip PEM) unless
+// den_render_ray_grad will read dz_0, which the folded L1 launch keeps on chip
+inline bool use_pe_fold(const den_render_desc* d) {
+#ifdef DEN_NO_PE_FOLD
+  return false;
+#else
+  return use_hidden_path(d) && d->train && !d->ray_grad;
+#endif
+}
 
 WsLayout ws_layout(const den_render_desc* d) {
   WsLayout L{};
@@ -184,6 +193,10 @@ WsLayout ws_layout(const den_render_desc* d) {
     L.lr_stage1 = off;
     off += align256((size_t)LR_G1 * LR_PART * 4);
   }
+  // the folded pe weight gradients' split-K partials (den_dwstream.hip's [wg][16][3] layout), written
+  // by the L5 and L1 launches, reduced after both
+  L.pe_partial = off;
+  if (use_pe_fold(d)) off += align256((size_t)hidden_grid(n) * 16 * 3 * 1024 * 4);
   L.total = off;
   return L;
 }
@@ -323,9 +336,9 @@ int launch_dwstream(const den_render_desc* d, const WsLayout& L, char* ws, int a
 // `layer`'s gradient (red_n1 / n1_feat / bias as in launch_dw).
 int launch_dwstream_reduce(const den_render_desc* d, const WsLayout& L, char* ws, int MT_ALL, int NT_ALL, int mt0,
                            int MT, int layer, int red_n1, int n1_feat, int bias, float* grad, hipStream_t s,
-                           int splits = -1) {
+                           int splits = -1, size_t region = (size_t)-1) {
   DwReduceArgs R{};
-  R.partial = (float*)(ws + L.dw_partial);
+  R.partial = (float*)(ws + (region == (size_t)-1 ? L.dw_partial : region));
   R.splits = splits > 0 ? splits : (int)hidden_grid(d);
   R.MT = MT;
   R.NT = NT_ALL;
@@ -394,14 +407,25 @@ int launch_hidden(const den_render_desc* d, const den_render_io* io, const WsLay
   H.bs_s = L.bstride[A_S0 + l - 1];
   H.bs_dz_out = L.bstride[D_Z0 + l - 1];
   H.sigma_dz = ws + L.sigma_dz;
+  // the pe fold: L5 adds dW_5's pe columns, L1 dW_0 (dz_0 then stays on chip)
+  const int pem = use_pe_fold(d) ? (l == 5 ? 1 : l == 1 ? 2 : 0) : 0;
+  H.pe = ws + L.act[A_PE];
+  H.bs_pe = L.bstride[A_PE];
+  H.pe_partial = (float*)(ws + L.pe_partial);
+  H.pe_mt0 = l == 5 ? 8 : 0;
   const int64_t grid = hidden_grid(d);
   H.per_wg = (H.n_blocks + grid - 1) / grid;
   {
     TimedLaunch timed_(lb ? T_HIDDEN_LB : T_HIDDEN_BWD, s);
+    const dim3 g((unsigned)grid), t(HbCfg<false>::THREADS);
     if (lb)
-      hipLaunchKernelGGL(hidden_bwd_kernel<true>, dim3((unsigned)grid), dim3(HbCfg<true>::THREADS), 0, s, H);
+      hipLaunchKernelGGL((hidden_bwd_kernel<true, 0>), g, dim3(HbCfg<true>::THREADS), 0, s, H);
+    else if (pem == 1)
+      hipLaunchKernelGGL((hidden_bwd_kernel<false, 1>), g, t, 0, s, H);
+    else if (pem == 2)
+      hipLaunchKernelGGL((hidden_bwd_kernel<false, 2>), g, t, 0, s, H);
     else
-      hipLaunchKernelGGL(hidden_bwd_kernel<false>, dim3((unsigned)grid), dim3(HbCfg<false>::THREADS), 0, s, H);
+      hipLaunchKernelGGL((hidden_bwd_kernel<false, 0>), g, t, 0, s, H);
   }
   DEN_LAUNCHED();
   if (lb) return launch_dwstream_reduce(d, L, ws, 9, 8, 0, 9, L_B, WIDTH, 0, 1, grad, s);
@@ -511,10 +535,14 @@ int render_bwd_impl(const den_render_desc* d, const den_render_io* io, const den
   }
   if (!(parts & 2)) return DEN_OK;
   if (hidden) {
-    // streamed, operand-sharing weight gradients (den_dwstream.hip): L0 and L5's pe columns
-    if ((rc = launch_dwstream<8, 16, 2, 2, DWS_NW1, 3, 1>(d, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s)) != DEN_OK) return rc;
-    if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s)) != DEN_OK) return rc;
+    // L0's and L5's pe-column weight gradients: folded into the L1 / L5 launches (part 1 wrote their
+    // partials), else streamed by one operand-sharing launch (den_dwstream.hip) over dz_0, dz_5 and pe
+    const bool fold = use_pe_fold(d);
+    const size_t region = fold ? L.pe_partial : L.dw_partial;
+    if (!fold && (rc = launch_dwstream<8, 16, 2, 2, DWS_NW1, 3, 1>(d, L, ws, D_Z0 + 0, D_Z0 + 5, A_PE, -1, s)) != DEN_OK)
+      return rc;
+    if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 0, 8, 0, 64, 0, 1, G, s, -1, region)) != DEN_OK) return rc;
+    if ((rc = launch_dwstream_reduce(d, L, ws, 16, 2, 8, 8, 5, 0, WIDTH, 0, G, s, -1, region)) != DEN_OK) return rc;
     // (Lb's weight gradient comes from its hidden launch, Lr's and Lg's from render_head_bwd_kernel)
     if (g->grad_bkgd) {
       hipLaunchKernelGGL(sum_partials_kernel, dim3(d->radiance_dim), dim3(1024), 0, s, d->radiance_dim, d->n_rays,

@@ -38,6 +38,25 @@ struct HbCfg {
 constexpr int HB_TILE = 2048;          // one 32 x 32 BF16 tile of a wave block
 constexpr int HB_BLOCK = 8 * HB_TILE;  // the 256 features of one 32-sample wave block
 constexpr int HB_SIG = 256;            // LB: LDS bytes for sigma's bf16[32] dz of a block (aligned)
+// The pe weight-gradient fold (PEM; possible once a wave holds one W^T row tile):
+// L5 (PEM 1) also forms dW_5's pe columns from its dz_5 operand; L1 (PEM 2) forms dW_0 = dz_0 (x) pe and
+// db_0 from the dz_0 it computes, which then never leaves the chip (each wave stages its tile in LDS
+// for the transposed read).  pe (the forward's stored copy, 2 tiles per wave block) arrives as a third
+// part of each ring slot, one 1 KiB piece from each of waves 0..3.  The partials take
+// den_dwstream.hip's [wg][16][3] layout (L1 row tiles 0..7 with the bias, L5 8..15), so the streamed
+// launch's two reductions read them unchanged.  Both variants trade the chain's dz read-ahead and the
+// early derivative factors (L7..L1's) for the 32 registers of the two pe accumulator tiles.
+constexpr int HB_PE = 2 * HB_TILE;     // PEM: pe bytes per wave block
+// PEM: the ring runs fewer blocks ahead (L5 two: 3 slots of 36 KiB; L1 one: 2 slots, beside its dz_0
+// stages), and the last hb_wtl_k k-steps of the waves' W^T fragments live in the LDS this frees (8 KiB
+// each, 4 registers per lane each; L1 at 4 of them and two ahead still spilled 12)
+#ifndef DEN_HB_DEPTH_PE2
+#define DEN_HB_DEPTH_PE2 1
+#endif
+template <int PEM> constexpr int hb_depth_pe() { return PEM == 1 ? 2 : DEN_HB_DEPTH_PE2; }
+template <int PEM> constexpr int hb_wtl_k() {  // (LDS: L5 156 KiB, L1 152 KiB)
+  return PEM == 1 ? 6 : PEM == 2 ? (DEN_HB_DEPTH_PE2 == 1 ? 8 : 4) : 0;
+}
 // Measured (r02/r03): one persistent workgroup per CU; non-temporal dz_l / S'_{l-1}
 // loads and dz_{l-1} stores (streamed once; cached stores were slower); 3 blocks in flight (4 did not
 // help); dz_l fragments read 4 k-steps ahead; the epilogue and the dW MFMAs kept in separate phases
@@ -91,6 +110,10 @@ struct HiddenArgs {
   int64_t per_wg;     // blocks per workgroup
   int64_t bs_dz_in, bs_s, bs_dz_out;  // bytes from one wave block to the next (den_geom.h SROW_BYTES rows)
   const char* sigma_dz;               // LB: sigma's dz, one bf16 per sample
+  const char* pe;                     // PEM: the stored pe (2 tiles per wave block)
+  int64_t bs_pe;
+  float* pe_partial;                  // PEM: [gridDim.x][16][3][64][16] (den_dwstream.hip layout)
+  int pe_mt0;                         // PEM: first row tile (L1 0, L5 8)
 };
 
 // 16-byte LDS slot that holds tile lane `lane`'s fragment f inside a 1 KiB piece:
@@ -145,6 +168,18 @@ __device__ __forceinline__ void hb_dma_sigma(const char* src, char* dst) {
   if (lane < 4)
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"((uint32_t)lane * 16),
                  "s"(src), "s"(m0) : "memory", "m0");
+}
+
+// PEM: the pe block of a wave block (4 x 1 KiB pieces, the slot permutation of hb_dma) by waves 0..3
+__device__ __forceinline__ void hb_dma_pe(const char* src, char* dst) {
+  const int lane = threadIdx.x & 63;
+  const int pc = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (pc < 4) {
+    const uint32_t off = (uint32_t)hb_slot(lane, pc & 1) * 16;
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)(dst + pc * 1024));
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"(off), "s"(src + pc * 1024),
+                 "s"(m0) : "memory", "m0");
+  }
 }
 
 // This lane's own fragment f of a tile in LDS (the chain's B operand / the stored activation).
@@ -214,18 +249,23 @@ __device__ __forceinline__ void hb_sigma_dw(const char* sig, const char* sb, flo
 // that k-step and the 18th are zero padding).  Sigma's weight-gradient row would be a ninth row tile
 // of 8 more accumulator tiles; instead wave w forms the row for its S7 tile w by VALU dot products
 // (hb_sigma_dw).
-template <bool LB>
-__device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, const bf16x8* wt16, int64_t b,
-                                         const bf16x8 (&wt)[HbCfg<LB>::RT][LB ? 17 : 16],
+template <bool LB, int PEM>
+__device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, const bf16x8* wt16,
+                                         const bf16x8* wtl, char* stage,
+                                         int64_t b, const bf16x8 (&wt)[HbCfg<LB>::RT][LB ? 17 : 16],
                                          f32x16 (&dw)[HbCfg<LB>::RT][8], float (&db)[HbCfg<LB>::RT],
-                                         float (&sd)[HbCfg<LB>::RT], float& sdb, HbProf& hp) {
+                                         float (&sd)[HbCfg<LB>::RT], float& sdb, f32x16 (&dwp)[2], float& db0,
+                                         HbProf& hp) {
   constexpr int HB_RT = HbCfg<LB>::RT;
-  constexpr int HB_PF = LB ? HB_PF_LB : HB_PF_L;
+  static_assert(PEM == 0 || (!LB && HB_RT == 1), "the pe fold is for L1 / L5 at one row tile per wave");
+  constexpr bool EARLY = !LB && PEM == 0;  // S' prefetch + derivative factors in the chain's shadow
+  constexpr int HB_PF = EARLY ? HB_PF_L : HB_PF_LB;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int DZ_BYTES = LB ? HB_BLOCK + HB_SIG : HB_BLOCK;
   const char* dzb = cur;
   const char* sig = cur + HB_BLOCK;  // LB: sigma's dz, bf16[32]
   const char* sb = cur + DZ_BYTES;
+  const char* peb = sb + HB_BLOCK;   // PEM: the block's pe tiles
   // chain: both row tiles of this wave share each dz_l fragment (K = 256, 16 k-steps): one LDS read
   // feeds two independent MFMAs, and the reads run HB_PF k-steps ahead of their use (issued
   // one per k-step, the compiler waited out the LDS latency before every MFMA)
@@ -241,7 +281,7 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, c
   for (int t = 0; t < HB_RT; ++t)
 #pragma unroll
     for (int f = 0; f < 2; ++f)
-      if constexpr (!LB) sf[t][f] = hb_frag(sb + (HB_RT * wave + t) * HB_TILE, f);
+      if constexpr (EARLY) sf[t][f] = hb_frag(sb + (HB_RT * wave + t) * HB_TILE, f);
   __builtin_amdgcn_sched_barrier(0);  // (left alone, the compiler sinks these reads back to their use)
   // L7..L1: the epilogue's 32 activation-derivative factors 1 - 2^-S', computed in the chain MFMAs'
   // shadow (r06, profiles/r06v_ab.jsonl: 4.639 -> 4.607 ms per launch in ABBA order).  Lb has no
@@ -253,14 +293,23 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, c
     bf16x8 bq[HB_PF];
 #pragma unroll
     for (int p = 0; p < HB_PF; ++p) bq[p] = hb_frag(dzb + (p >> 1) * HB_TILE, p & 1);
+    // PEM: k-steps [KL, 16) of the wave's W^T from LDS (wtl), each read one k-step ahead; the
+    // scheduling fence per k-step keeps the compiler from hoisting them all (their registers are the
+    // point)
+    constexpr int KL = 16 - hb_wtl_k<PEM>();
+    bf16x8 wn;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const bf16x8 cur = bq[k % HB_PF];
       if (k + HB_PF < 16) bq[k % HB_PF] = hb_frag(dzb + ((k + HB_PF) >> 1) * HB_TILE, (k + HB_PF) & 1);
+      static_assert(PEM == 0 || HB_RT == 1, "");
+      const bf16x8 wa = k >= KL ? wn : wt[0][k < KL ? k : 0];
+      if (PEM && k + 1 >= KL && k + 1 < 16) wn = wtl[((k + 1 - KL) * 8 + wave) * 64 + lane];
 #pragma unroll
       for (int t = 0; t < HB_RT; ++t)
-        accs[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wt[t][k], cur, accs[t], 0, 0, 0);
-      if constexpr (!LB) {  // HB_RT of the derivative factors per k-step
+        accs[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(PEM ? wa : wt[t][k], cur, accs[t], 0, 0, 0);
+      if constexpr (PEM) __builtin_amdgcn_sched_barrier(0);
+      if constexpr (EARLY) {  // HB_RT of the derivative factors per k-step
 #pragma unroll
         for (int e = 0; e < HB_RT; ++e) {
           const int q = k * HB_RT + e, t = q >> 4, r = q & 15;
@@ -287,11 +336,11 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, c
   for (int t = 0; t < HB_RT; ++t) {
     f32x16 acc = accs[t];
     // (Lb reads them here: held across its chain they would spill)
-    const bf16x8 s0 = LB ? hb_frag(sb + (HB_RT * wave + t) * HB_TILE, 0) : sf[t][0];
-    const bf16x8 s1 = LB ? hb_frag(sb + (HB_RT * wave + t) * HB_TILE, 1) : sf[t][1];
+    const bf16x8 s0 = !EARLY ? hb_frag(sb + (HB_RT * wave + t) * HB_TILE, 0) : sf[t][0];
+    const bf16x8 s1 = !EARLY ? hb_frag(sb + (HB_RT * wave + t) * HB_TILE, 1) : sf[t][1];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      if constexpr (!LB) {
+      if constexpr (EARLY) {
         acc[r] = acc[r] * dv[t][r];
       } else {
         const float sv = (float)(r < 8 ? s0[r] : s1[r - 8]);
@@ -301,9 +350,16 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, c
     // dz_{l-1} tile: stored now, the weight-gradient MFMAs below cover its write latency
     bf16x8 of[2];
     acc_to_frags<1>(acc, of);
-    char* d = P.dz_out + b * P.bs_dz_out + (HB_RT * wave + t) * HB_TILE + lane * 16;  // dz_{l-1}: 8 tiles per block
-    __builtin_nontemporal_store(of[0], (bf16x8*)d);
-    __builtin_nontemporal_store(of[1], (bf16x8*)(d + 1024));
+    if constexpr (PEM == 2) {
+      // dz_0 stays on chip: the wave's tile into its LDS stage (hb_slot order, read back transposed by
+      // the pe phase below; LDS operations of one wave complete in order)
+      *(bf16x8*)(stage + hb_slot(lane, 0) * 16) = of[0];
+      *(bf16x8*)(stage + 1024 + hb_slot(lane, 1) * 16) = of[1];
+    } else {
+      char* d = P.dz_out + b * P.bs_dz_out + (HB_RT * wave + t) * HB_TILE + lane * 16;  // dz_{l-1}: 8 tiles per block
+      __builtin_nontemporal_store(of[0], (bf16x8*)d);
+      __builtin_nontemporal_store(of[1], (bf16x8*)(d + 1024));
+    }
     // keep the scheduler from hoisting the next phase's LDS reads here (register pressure: W^T lives
     // in 128 VGPRs and dW in all 256 AGPRs for the whole launch)
     __builtin_amdgcn_sched_barrier(0);
@@ -320,11 +376,31 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, c
       const bf16x8 bb = hb_tr_frag(sb + n * HB_TILE, kk);
 #pragma unroll
       for (int t = 0; t < HB_RT; ++t) dw[t][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], bb, dw[t][n], 0, 0, 0);
+      if constexpr (PEM == 2) {  // (registers: at most four S' fragments in flight)
+        if (n % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+      }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int t = 0; t < HB_RT; ++t) db[t] += (float)a[t][j];
+    if constexpr (PEM == 1) {  // dW_5's pe columns: the same dz_5 operand against the pe tiles
+#pragma unroll
+      for (int n = 0; n < 2; ++n) dwp[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], hb_tr_frag(peb + n * HB_TILE, kk),
+                                                                                    dwp[n], 0, 0, 0);
+    }
+  }
+  if constexpr (PEM == 2) {  // dW_0 = dz_0 (x) pe and db_0 from the staged dz_0 tile
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 a0 = hb_tr_frag(stage, kk);
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        dwp[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, hb_tr_frag(peb + n * HB_TILE, kk), dwp[n], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) db0 += (float)a0[j];
+    }
   }
   hp.mark(3);
   // sigma's weight-gradient row last (placed between the chain and the epilogue or before the dW
@@ -335,15 +411,16 @@ __device__ __forceinline__ void hb_block(const HiddenArgs& P, const char* cur, c
   }
 }
 
-template <bool LB>
+template <bool LB, int PEM>
 DEN_CODE_ALIGN  // page-aligned code (r04y A/B)
 __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(HiddenArgs P) {
-  constexpr int HB_WAVES = HbCfg<LB>::WAVES, HB_RT = HbCfg<LB>::RT, HB_STORE_OPS = HbCfg<LB>::STORE_OPS;
+  constexpr int HB_WAVES = HbCfg<LB>::WAVES, HB_RT = HbCfg<LB>::RT;
+  constexpr int HB_STORE_OPS = PEM == 2 ? 0 : HbCfg<LB>::STORE_OPS;  // (PEM 2: dz_0 is not stored)
   // HB_RING LDS slots of [dz_l block | S'_{l-1} block]; HB_DEPTH blocks in flight ahead of the one
   // being computed.  Each wave waits for its own part of block b+1 at the end of block b (vmcnt; the
   // younger prefetches and stores stay in flight), then the workgroup barrier publishes every part.
   constexpr int DZ_STAGED = LB ? HB_BLOCK + HB_SIG : HB_BLOCK;  // bytes of them staged
-  constexpr int SLOT = DZ_STAGED + HB_BLOCK;
+  constexpr int SLOT = DZ_STAGED + HB_BLOCK + (PEM ? HB_PE : 0);
   constexpr int KST = LB ? 17 : 16;              // chain k-steps
   constexpr int ROW_BYTES = (LB ? 288 : 256) * 64;  // packed W^T row tile (chunk_bytes_K(bwd_K))
   constexpr int MTA = LB ? 9 : 8;                // partial row tiles
@@ -351,14 +428,25 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
   // vector-memory ops a wave issues after its DMA of block b+1 by the end of block b (issue order:
   // stores(b-2), DMA(b+2), stores(b-1), DMA(b+3), stores(b)); the asm DMAs clobber "memory", so the
   // stores keep their program order around them
-  constexpr int HB_DEPTH = LB ? HB_DEPTH_LB : HB_DEPTH_L;
+  constexpr int HB_DEPTH = LB ? HB_DEPTH_LB : PEM ? hb_depth_pe<PEM>() : HB_DEPTH_L;
   constexpr int HB_RING = HB_DEPTH + 1;
   constexpr int YOUNGER = HB_STORE_OPS + (HB_DEPTH - 1) * (DMA_OPS + HB_STORE_OPS);
-  static_assert(HB_RING * SLOT <= 160 * 1024, "hidden ring exceeds the LDS");
-  __shared__ __attribute__((aligned(16))) char lds[HB_RING * SLOT];
-  __shared__ bf16x8 wt16[HbCfg<LB>::WT16_LDS ? 8 * 64 : 1];
+  constexpr int YOUNGER_PE = YOUNGER + (PEM ? HB_DEPTH - 1 : 0);  // PEM, waves 0..3: + their pe pieces
+  // LDS: the ring, then LB's sigma k-step W^T fragments (8 KiB), PEM's last HB_WTL_K W^T k-steps
+  // (8 KiB each) and PEM 2's dz_0 stages (2 KiB per wave)
+  constexpr int WT16_BYTES = HbCfg<LB>::WT16_LDS ? 8 * 64 * 16 : 0;
+  constexpr int WTL_K = hb_wtl_k<PEM>();
+  constexpr int WTL_BYTES = WTL_K * 8 * 64 * 16;
+  constexpr int STAGE_BYTES = PEM == 2 ? HB_WAVES * HB_TILE : 0;
+  constexpr int LDS_TOTAL = HB_RING * SLOT + WT16_BYTES + WTL_BYTES + STAGE_BYTES;
+  static_assert(LDS_TOTAL <= 160 * 1024, "hidden ring exceeds the LDS");
+  __shared__ __attribute__((aligned(16))) char lds[LDS_TOTAL];
+  const bf16x8* wt16 = (const bf16x8*)(lds + HB_RING * SLOT);
+  const bf16x8* wtl = (const bf16x8*)(lds + HB_RING * SLOT + WT16_BYTES);
   DEN_CLOCK_BEGIN();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  char* stage = lds + HB_RING * SLOT + WT16_BYTES + WTL_BYTES + wave * HB_TILE;  // PEM 2
+  const bool pe_wave = PEM && __builtin_amdgcn_readfirstlane(wave) < 4;
   // a contiguous range of P.per_wg blocks per workgroup (r03: strided by the grid, so that all
   // workgroups sweep one address window, measured the same)
   const int64_t b0 = (int64_t)blockIdx.x * P.per_wg;
@@ -368,6 +456,7 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
     hb_dma_untracked<HB_WAVES>(P.dz_in + b * P.bs_dz_in, dst);
     if constexpr (LB) hb_dma_sigma(P.sigma_dz + b * 64, dst + HB_BLOCK);
     hb_dma_untracked<HB_WAVES>(P.s_in + b * P.bs_s, dst + DZ_STAGED);
+    if constexpr (PEM) hb_dma_pe(P.pe + b * P.bs_pe, dst + DZ_STAGED + HB_BLOCK);
   };
 #pragma unroll
   for (int u = 0; u < HB_DEPTH; ++u)
@@ -382,7 +471,13 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
       wt[t][k] = *(const bf16x8*)(P.w + (int64_t)(HB_RT * wave + t) * ROW_BYTES + k * 1024 + lane * 16);
   if constexpr (HbCfg<LB>::WT16_LDS) {
 #pragma unroll
-    for (int t = 0; t < HB_RT; ++t) wt16[(HB_RT * wave + t) * 64 + lane] = wt[t][16];
+    for (int t = 0; t < HB_RT; ++t) ((bf16x8*)wt16)[(HB_RT * wave + t) * 64 + lane] = wt[t][16];
+  }
+  if constexpr (PEM) {
+#pragma unroll
+    for (int q = 0; q < WTL_K; ++q)
+#pragma unroll
+      for (int t = 0; t < HB_RT; ++t) ((bf16x8*)wtl)[(q * 8 + HB_RT * wave + t) * 64 + lane] = wt[t][16 - WTL_K + q];
   }
   f32x16 dw[HB_RT][8];
 #pragma unroll
@@ -397,6 +492,12 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
 #pragma unroll
   for (int t = 0; t < HB_RT; ++t) db[t] = sd[t] = 0.0f;
   float sdb = 0.0f;  // LB: sigma's bias gradient (lanes 0..31)
+  f32x16 dwp[2];     // PEM: the pe weight-gradient tiles of the wave's row tile (pe columns 0..31, 32..63)
+  float db0 = 0.0f;  // PEM 2: db_0 partial, feature (lane & 31) of row tile w, this lane's samples
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dwp[n][r] = 0.0f;
   HbProf hp;
   hp.init();
 #ifdef DEN_HIDDEN_PROF
@@ -413,9 +514,13 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
     // prefetch block it + HB_DEPTH into the slot block it - 1 used (free since the last barrier)
     if (it + HB_DEPTH < n_it) fetch(blk(it + HB_DEPTH), lds + ((u + HB_DEPTH) % HB_RING) * SLOT);
     hp.mark(0);
-    hb_block<LB>(P, lds + u * SLOT, wt16, blk(it), wt, dw, db, sd, sdb, hp);
-    if (it + HB_DEPTH < n_it) hb_wait_vm_lgkm0<YOUNGER>();
-    else hb_wait_vm_lgkm0<0>();
+    hb_block<LB, PEM>(P, lds + u * SLOT, wt16, wtl, stage, blk(it), wt, dw, db, sd, sdb, dwp, db0, hp);
+    if (it + HB_DEPTH < n_it) {
+      if (pe_wave) hb_wait_vm_lgkm0<YOUNGER_PE>();
+      else hb_wait_vm_lgkm0<YOUNGER>();
+    } else {
+      hb_wait_vm_lgkm0<0>();
+    }
     hp.mark(5);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -466,6 +571,22 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
       }
     }
   }
+  if constexpr (PEM) {
+    // pe partial ([wg][16][3] tiles): row tile pe_mt0 + w, pe column tiles 0, 1; L1's db_0 in the ones
+    // tile (nt 2) where the hidden bias goes (above); L5's ones tile is never read (bias 0)
+    float* o = P.pe_partial + (((int64_t)blockIdx.x * 16 + P.pe_mt0 + wave) * 3) * 1024;
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4 v = {dwp[n][4 * q], dwp[n][4 * q + 1], dwp[n][4 * q + 2], dwp[n][4 * q + 3]};
+        *(f32x4*)(o + n * 1024 + lane * 16 + 4 * q) = v;
+      }
+    if constexpr (PEM == 2) {
+      const float bsum = db0 + __shfl_xor(db0, 32, 64);
+      if (lane < 32) o[2 * 1024 + (32 * ((lane >> 2) & 1)) * 16 + (lane & 3) + 4 * (lane >> 3)] = bsum;
+    }
+  }
 #pragma unroll
   for (int t = 0; t < HB_RT; ++t)
 #pragma unroll
@@ -479,7 +600,9 @@ __global__ __launch_bounds__(HbCfg<LB>::THREADS, 1) void hidden_bwd_kernel(Hidde
     }
 }
 
-template __global__ void hidden_bwd_kernel<false>(HiddenArgs);
-template __global__ void hidden_bwd_kernel<true>(HiddenArgs);
+template __global__ void hidden_bwd_kernel<false, 0>(HiddenArgs);
+template __global__ void hidden_bwd_kernel<false, 1>(HiddenArgs);
+template __global__ void hidden_bwd_kernel<false, 2>(HiddenArgs);
+template __global__ void hidden_bwd_kernel<true, 0>(HiddenArgs);
 
 }  // namespace den

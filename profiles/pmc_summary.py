@@ -21,7 +21,7 @@ KERNELS = ("render_fwd_kernel", "render_head_bwd_kernel", "render_bwd_kernel", "
 
 
 def short(name):
-    if "hidden_bwd_kernel<true>" in name:  # the Lb launch (den_hidden.hip, LB = true)
+    if "hidden_bwd_kernel<true" in name:  # the Lb launch (den_hidden.hip, LB = true)
         return "hidden_bwd_lb_kernel"
     for k in KERNELS:
         if k in name:
