@@ -210,7 +210,10 @@ int den_render_bwd(const den_render_desc* desc, const den_render_io* io,
                    const den_render_grad* grad, void* stream);
 /* den_render_bwd in two stream-ordered halves (for profiling / overlap):
  * part 1 = compositing adjoint + MLP dz chain (one kernel), part 2 = weight /
- * bias / background gradients from the dz written by part 1. */
+ * bias / background gradients from the dz written by part 1.  On the BF16
+ * layer-major path part 1 also writes the hidden layers' gradients, and (unless
+ * desc.ray_grad) the L0 / L5-pe weight-gradient partials that part 2 reduces: call
+ * part 2 after part 1 on the same desc / io / workspace. */
 int den_render_bwd_part(const den_render_desc* desc, const den_render_io* io,
                         const den_render_grad* grad, int32_t part, void* stream);
 
